@@ -1,0 +1,249 @@
+#!/usr/bin/env python3
+"""Headline benchmark: GiB/s AEAD seal+open, device-resident, 1200 B packets (BASELINE.json metric).
+
+A "step" = one seal pass (AEAD + 5-byte HP mask, as the TX path does) plus one open pass over one batch of
+synthetic packets already resident in HBM.  Default workload = BASELINE.json configs[1]:
+AES-128-GCM seal+open, 1 Mi x 1200 B packets, single key, per GPU.
+Multi-GPU (torchrun, one process per GPU): every rank seals/opens its own shard (weak scaling, no collective);
+gloo on CPU tensors carries only the barrier and the max-over-ranks time.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--suite aes128gcm|aes256gcm|chacha20poly1305]
+                    [--packets N] [--pt BYTES] [--keys K] [--mode device|e2e]
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "s2n-quic_amd"))
+import numpy as np  # noqa: E402
+
+import qpp  # noqa: E402
+
+qpp.lib()  # load the engine (and its HIP runtime) before anything else touches the GPU
+
+SUITES = {"aes128gcm": 1, "aes256gcm": 2, "chacha20poly1305": 3}
+METRIC = "GiB/s AEAD seal+open, device-resident, 1200 B packets at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s; 6.29 measured copy)
+GiB = float(1 << 30)
+
+
+def seal_bytes_per_packet(pt, aad, hp=True):
+    # read AAD + PT + descriptor(24); write CT + tag(16) + mask(5)
+    return aad + pt + 24 + pt + 16 + (5 if hp else 0)
+
+
+def open_bytes_per_packet(pt, aad):
+    # read AAD + CT + tag + descriptor; write PT + status(1)
+    return aad + pt + 16 + 24 + pt + 1
+
+
+def cpu_baseline(suite, pt, aad, seconds):
+    """The reference's per-packet CPU loop (OpenSSL EVP stand-in for aws-lc) on this host's cores."""
+    path = os.path.join(ROOT, "oracle", "libcpubase.so")
+    if not os.path.exists(path):
+        return None
+    L = ctypes.CDLL(path)
+    L.cpubase_run.restype = ctypes.c_double
+    L.cpubase_run.argtypes = [ctypes.c_int] * 6 + [ctypes.c_double, ctypes.POINTER(ctypes.c_int)]
+    L.cpubase_impl.restype = ctypes.c_char_p
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    threads = max(1, min(16, cores))  # the GPU box's CPU share is 16
+    ok = ctypes.c_int()
+    gibs = L.cpubase_run(suite, threads, 4096, pt, aad, 1, seconds, ctypes.byref(ok))
+    return {
+        "value": round(gibs, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+        "sample": (f"{L.cpubase_impl().decode()} EVP per-packet seal+HP+open loop (stand-in for aws-lc-rs, "
+                   f"which cannot be built offline), {threads} threads x 4 Ki x {pt} B packets "
+                   f"(BASELINE configs[0] shape), {seconds:.1f} s wall, all tags verified={bool(ok.value)}"),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--suite", default="aes128gcm", choices=sorted(SUITES))
+    ap.add_argument("--packets", type=int, default=1 << 20, help="packets per GPU")
+    ap.add_argument("--pt", type=int, default=1200, help="payload bytes per packet")
+    ap.add_argument("--aad", type=int, default=21, help="short header: 0x43 || DCID16 || PN4")
+    ap.add_argument("--keys", type=int, default=1)
+    ap.add_argument("--mode", default="device", choices=["device", "e2e"])
+    ap.add_argument("--cpu-seconds", type=float, default=1.5)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local_rank = int(os.environ.get("LOCAL_RANK", 0))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist_mod
+
+        dist = dist_mod
+        dist.init_process_group("gloo")  # CPU only: barrier + max over ranks; the data path has no collective
+
+    def barrier():
+        if dist:
+            dist.barrier()
+
+    def max_over_ranks(x):
+        if not dist:
+            return x
+        t = torch.tensor([x], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    suite = SUITES[args.suite]
+    ctx = qpp.Context(local_rank)
+    rng = np.random.default_rng(0x5eed0000 + 1)
+    keys = [ctx.key(suite, rng.integers(0, 256, qpp.HASH_LEN[suite], dtype=np.uint8).tobytes()) for _ in range(args.keys)]
+    n, pt, aad = args.packets, args.pt, args.aad
+    descs, arena = qpp.make_batch(n, pt, [k.slot for k in keys], seed=0x5eed0000 + 1 + 7919 * rank, aad_len=aad,
+                                  pn_base=rank * n)
+    flags = qpp.HP_MASK_OUT | (qpp.ONLY_CHACHA if suite == 3 else qpp.ONLY_AES)
+    d_desc, d_mask, d_status = ctx.alloc(descs.nbytes), ctx.alloc(5 * n), ctx.alloc(n)
+    d_desc.upload(descs)
+    s = ctx.stream
+
+    if args.mode == "e2e":
+        return e2e(args, ctx, keys, descs, arena, d_desc, d_mask, d_status, flags, rank, world, barrier, max_over_ranks)
+
+    d_arena = ctx.alloc(arena.nbytes)
+    d_arena.upload(arena)
+    del arena
+
+    def step(ev=None):
+        if ev:
+            ctx.record(ev[0], s)
+        ctx.seal_batch(d_desc, n, d_arena, d_mask, d_status, flags, stream=s)
+        if ev:
+            ctx.record(ev[1], s)
+        ctx.open_batch(d_desc, n, d_arena, d_status, flags & ~qpp.HP_MASK_OUT, stream=s)
+        if ev:
+            ctx.record(ev[2], s)
+
+    for _ in range(args.warmup):
+        step()
+    ctx.sync(s)
+    st = d_status.download(dtype=np.int8)
+    if not (st == 0).all():
+        raise SystemExit(f"rank {rank}: {int((st != 0).sum())} packets failed to open during warmup")
+
+    evs = [(ctx.event(), ctx.event(), ctx.event()) for _ in range(args.steps)]
+    e0, e1 = ctx.event(), ctx.event()
+    barrier()
+    ctx.sync(s)
+    ctx.record(e0, s)
+    for k in range(args.steps):
+        step(evs[k])
+    ctx.record(e1, s)
+    ctx.sync(s)
+    barrier()
+    t_ms = ctx.elapsed_ms(e0, e1)
+    seal_ms = [ctx.elapsed_ms(a, b) for a, b, _ in evs]
+    open_ms = [ctx.elapsed_ms(b, c) for _, b, c in evs]
+    t_max = max_over_ranks(t_ms)
+
+    payload = 2.0 * n * pt * args.steps * world  # seal + open, all ranks
+    value = payload / (t_max / 1e3) / GiB
+    seal_avg = float(np.mean(seal_ms))
+    achieved = n * seal_bytes_per_packet(pt, aad) / (seal_avg / 1e3) / 1e9
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(t_max / args.steps, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (seeded PCG64 payload bytes, 21 B short-header AAD, PN = base + i)",
+            "config": {
+                "workload": (f"{qpp.SUITE_NAMES[suite]} seal(+HP mask)+open, {n} x {pt} B packets per GPU, "
+                             f"{args.keys} key(s)" + (" (BASELINE configs[1])" if suite == 1 and pt == 1200 and
+                                                     args.keys == 1 and n == 1 << 20 else "")),
+                "suite": args.suite, "packets_per_gpu": n, "payload_bytes": pt, "aad_bytes": aad, "keys": args.keys,
+                "hp_mask": True, "parallelism": f"packet shards x{world}, no collective",
+                "seal_ms": round(seal_avg, 4), "open_ms": round(float(np.mean(open_ms)), 4),
+            },
+            "roofline": {
+                "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "kernel": "aes_gcm_kernel<seal> + plan (per seal call)" if suite != 3 else "chacha_kernel<seal>",
+                "bytes_per_packet": seal_bytes_per_packet(pt, aad),
+            },
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu:
+            out["cpu_baseline"] = cpu_baseline(suite, pt, aad, args.cpu_seconds)
+        print(json.dumps(out), flush=True)
+    ctx.close()
+
+
+def e2e(args, ctx, keys, descs, arena, d_desc, d_mask, d_status, flags, rank, world, barrier, max_over_ranks):
+    """End-to-end: packets start and end in pinned host memory (the UDP socket buffer of the reference,
+    quic/s2n-quic-platform/src/socket/io/tx.rs:204-268).  Chunks are pipelined: H2D on one stream, seal+open
+    on the compute stream, D2H on a third, with events between them."""
+    n, pt = args.packets, args.pt
+    stride = arena.size // n
+    chunks = 8
+    per = (n + chunks - 1) // chunks
+    h_in = ctx.host_alloc(arena.nbytes)
+    h_in[:] = arena
+    h_out = ctx.host_alloc(arena.nbytes)
+    d_arena = ctx.alloc(arena.nbytes)
+    sc, sh, sd = ctx.stream, ctx.new_stream(), ctx.new_stream()
+    lib = qpp.lib()
+    # per-chunk descriptors with offsets relative to the chunk
+    d_descs = []
+    for c in range(chunks):
+        lo, hi = c * per, min(n, (c + 1) * per)
+        dd = descs[lo:hi].copy()
+        dd["off"] -= dd["off"][0]
+        b = ctx.alloc(dd.nbytes)
+        b.upload(dd)
+        d_descs.append((b, lo, hi))
+
+    def run():
+        evh = [ctx.event() for _ in range(chunks)]
+        evc = [ctx.event() for _ in range(chunks)]
+        for c, (b, lo, hi) in enumerate(d_descs):
+            off, nb = lo * stride, (hi - lo) * stride
+            lib.qpp_memcpy_h2d(ctx.handle, d_arena.ptr + off, h_in.ctypes.data + off, nb, sh)
+            ctx.record(evh[c], sh)
+            ctx.wait(sc, evh[c])
+            ctx.seal_batch(b, hi - lo, d_arena.ptr + off, d_mask.ptr + 5 * lo, None, flags, stream=sc)
+            ctx.open_batch(b, hi - lo, d_arena.ptr + off, d_status.ptr + lo, flags & ~qpp.HP_MASK_OUT, stream=sc)
+            ctx.record(evc[c], sc)
+            ctx.wait(sd, evc[c])
+            lib.qpp_memcpy_d2h(ctx.handle, h_out.ctypes.data + off, d_arena.ptr + off, nb, sd)
+        ctx.sync(sd)
+
+    for _ in range(args.warmup):
+        run()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run()
+    t = time.perf_counter() - t0
+    barrier()
+    t = max_over_ranks(t)
+    pay = np.s_[:, args.aad:args.aad + pt]  # tags stay behind in the buffer after open
+    assert (h_out.reshape(n, stride)[pay] == arena.reshape(n, stride)[pay]).all(), "e2e round trip mismatch"
+    if rank == 0:
+        print(json.dumps({
+            "metric": "GiB/s AEAD seal+open end-to-end (pinned host -> HBM -> pinned host), 1200 B packets",
+            "value": round(2.0 * n * pt * args.steps * world / t / GiB, 3), "unit": "GiB/s", "n_gpus": world,
+            "steps": args.steps, "ms_per_step": round(1e3 * t / args.steps, 3), "chunks": chunks,
+            "h2d_d2h_bytes_per_step": 2 * arena.nbytes, "suite": args.suite,
+        }), flush=True)
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,175 @@
+/*
+ * qpp.h — C ABI of the MI355X QUIC packet-protection engine (libqpp.so).
+ *
+ * Drop-in boundary for quic/s2n-quic-crypto (aws/s2n-quic 0.88.0).  Each entry point names the
+ * reference interface it replaces (paths relative to the reference repository root).
+ *
+ * Two faces, as SURVEY.md §8(b) describes:
+ *   - per-packet functions mirroring the Key / HeaderKey / OneRttKey traits
+ *     (quic/s2n-quic-core/src/crypto/{key.rs:8-35, header_crypto.rs:11-31, one_rtt.rs:11-14});
+ *     each one is a batch of one run on the GPU (synchronous);
+ *   - batch functions over device-resident packet arenas, which the kernels and bench use.
+ *
+ * Rules: no exceptions cross the ABI; plain pointers and sizes only; a qpp_ctx is used by one
+ * host thread at a time and owns one GPU; a qpp_key may be used from one thread at a time
+ * (the traits are Send, not Sync).  All memory passed in is owned by the caller.
+ */
+#ifndef QPP_H
+#define QPP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define QPP_ABI_VERSION 1
+
+/* Cipher suites (quic/s2n-quic-crypto/src/cipher_suite.rs:250-301). */
+typedef enum qpp_suite {
+    QPP_SUITE_TLS_AES_128_GCM_SHA256 = 1,
+    QPP_SUITE_TLS_AES_256_GCM_SHA384 = 2,
+    QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256 = 3,
+} qpp_suite;
+
+/* Return codes (quic/s2n-quic-core/src/crypto/packet_protection.rs:24-40), plus two the ABI needs. */
+typedef enum qpp_status {
+    QPP_OK = 0,
+    QPP_DECODE_ERROR = 1,   /* packet_protection::Error::DECODE_ERROR (e.g. sample out of range) */
+    QPP_DECRYPT_ERROR = 2,  /* packet_protection::Error::DECRYPT_ERROR (bad tag / short input) */
+    QPP_INTERNAL_ERROR = 3, /* packet_protection::Error::INTERNAL_ERROR (seal failure, bad capacity) */
+    QPP_UNSUPPORTED = 4,    /* NegotiatedCipherSuite::new returned None (cipher_suite/negotiated.rs:52-68) */
+    QPP_DEVICE_ERROR = 5,   /* no MI355X / HIP runtime failure: the engine fails loudly, never falls back */
+} qpp_status;
+
+typedef enum qpp_endpoint { QPP_ENDPOINT_CLIENT = 0, QPP_ENDPOINT_SERVER = 1 } qpp_endpoint;
+
+typedef struct qpp_ctx qpp_ctx;
+typedef struct qpp_key qpp_key;
+
+/* ------------------------------------------------------------------ context (one per GPU) */
+
+/* Opens GPU `device` (HIP ordinal).  QPP_DEVICE_ERROR if there is no usable gfx950 device. */
+int qpp_ctx_create(int device, qpp_ctx **out);
+void qpp_ctx_destroy(qpp_ctx *ctx);
+/* Default stream used by the per-packet functions and by batch calls given stream == NULL. */
+void *qpp_ctx_stream(qpp_ctx *ctx);
+int qpp_ctx_synchronize(qpp_ctx *ctx);
+int qpp_abi_version(void);
+
+/* ------------------------------------------------------------------ keys */
+
+/* TLS_*::new(secret) -> (Self, HeaderKey): key/iv/hp = HKDF-Expand-Label(secret, "quic key"/"quic iv"/"quic hp")
+ * (quic/s2n-quic-crypto/src/cipher_suite.rs:52-63,85-103; header_key.rs:33-49; iv.rs:14-24).
+ * secret_len must equal the suite's hash length (32 for SHA-256 suites, 48 for SHA-384). */
+int qpp_key_new(qpp_ctx *ctx, int suite, const uint8_t *secret, size_t secret_len, qpp_key **out);
+/* Raw key material (fixtures, Retry/other consumers).  A raw key has no secret: update fails. */
+int qpp_key_new_raw(qpp_ctx *ctx, int suite, const uint8_t *key, size_t key_len, const uint8_t iv[12],
+                    const uint8_t *hp, size_t hp_len, qpp_key **out);
+/* TLS_*::update / OneRttKey::derive_next_key: secret' = Expand-Label(secret, "quic ku", Hash.len);
+ * key/iv re-derived; the header-protection key is carried over unchanged (RFC 9001 §6)
+ * (cipher_suite.rs:68-83, one_rtt.rs:11-14). */
+int qpp_key_update(const qpp_key *key, qpp_key **out);
+/* Zeroizes host and device copies (cipher_suite.rs:106-114,189-193). */
+void qpp_key_free(qpp_key *key);
+/* Index of this key in its context's device key table: the value to put in qpp_pkt.key_idx. */
+uint32_t qpp_key_slot(const qpp_key *key);
+int qpp_key_suite(const qpp_key *key);
+/* Key::tag_len (16), HeaderKey::{sealing,opening}_sample_len (16), Key::aead_{confidentiality,integrity}_limit
+ * (cipher_suite.rs:158-175, 247-301). */
+size_t qpp_tag_len(const qpp_key *key);
+size_t qpp_sample_len(const qpp_key *key);
+uint64_t qpp_confidentiality_limit(const qpp_key *key);
+uint64_t qpp_integrity_limit(const qpp_key *key);
+/* Test introspection: copies the derived key (16/32), iv (12) and hp (16/32) bytes. */
+int qpp_key_material(const qpp_key *key, uint8_t *key_out, uint8_t iv_out[12], uint8_t *hp_out);
+
+/* InitialKey::new_{client,server}(dcid): AES-128-GCM keys from the Initial salt
+ * (quic/s2n-quic-crypto/src/initial.rs:29-80).  Returns the endpoint's sealer and opener. */
+int qpp_initial_keys(qpp_ctx *ctx, int endpoint, const uint8_t *dcid, size_t dcid_len,
+                     qpp_key **sealer, qpp_key **opener);
+
+/* ------------------------------------------------------------------ per packet (trait mirror) */
+
+/* Key::encrypt(pn, header, payload): payload[0..payload_len) plaintext is sealed in place and the
+ * 16-byte tag is written at payload + payload_len; payload_cap must be >= payload_len + 16
+ * (aead/default.rs:44-62; cipher_suite.rs:146-156).  QPP_INTERNAL_ERROR on bad capacity. */
+int qpp_seal(qpp_key *key, uint64_t pn, const uint8_t *header, size_t header_len,
+             uint8_t *payload, size_t payload_len, size_t payload_cap);
+/* seal_in_place_scatter (aead/default.rs:44-62): in_out sealed in place; the ciphertext of extra_in is
+ * written to extra_out_and_tag[0..extra_len) and the tag after it (extra_out_and_tag holds extra_len+16). */
+int qpp_seal_scatter(qpp_key *key, uint64_t pn, const uint8_t *header, size_t header_len,
+                     uint8_t *in_out, size_t in_len, const uint8_t *extra_in, size_t extra_len,
+                     uint8_t *extra_out_and_tag);
+/* Key::decrypt(pn, header, payload): payload = ciphertext || tag (payload_len bytes);
+ * on success payload[0..payload_len-16) holds the plaintext.  QPP_DECRYPT_ERROR on a bad tag or
+ * payload_len < 16 (cipher_suite.rs:117-144; aead/default.rs:65-93); on a bad tag the
+ * plaintext region is zeroed so unauthenticated plaintext is never released. */
+int qpp_open(const qpp_key *key, uint64_t pn, const uint8_t *header, size_t header_len,
+             uint8_t *payload, size_t payload_len);
+/* HeaderKey::{sealing,opening}_header_protection_mask(sample) -> [u8; 5] (header_key.rs:10-30,52-56). */
+int qpp_hp_mask(const qpp_key *key, const uint8_t *sample, size_t sample_len, uint8_t mask[5]);
+
+/* ------------------------------------------------------------------ batches (device-resident) */
+
+/* One packet of a batch.  The packet's bytes live in a device arena at `off`:
+ *   [off, off+aad_len)                 AAD = header || packet-number bytes (the `header` of Key::encrypt)
+ *   [off+aad_len, off+aad_len+pt_len)  payload (plaintext for seal, ciphertext for open)
+ *   [.. +pt_len, .. +pt_len+16)        tag (written by seal, read by open)
+ * The HP sample is at off + aad_len - pn_len + 4 (payload.rs:151-169: header_len + 4). */
+typedef struct qpp_pkt {
+    uint64_t pn;       /* full packet number (62-bit) -> Iv::nonce (iv.rs:27-39) */
+    uint32_t key_idx;  /* qpp_key_slot() of the key to use */
+    uint32_t off;      /* byte offset of the packet in the arena */
+    uint16_t aad_len;  /* header length including the packet-number bytes */
+    uint16_t pt_len;   /* payload length, tag excluded */
+    uint8_t pn_len;    /* 1..4 packet-number bytes (header protection) */
+    uint8_t flags;     /* reserved, 0 */
+    uint16_t reserved;
+} qpp_pkt;             /* 24 bytes */
+
+/* Batch flags */
+#define QPP_HP_MASK_OUT 0x1u   /* write the 5-byte HP mask of packet i to masks[5*i] */
+#define QPP_HP_APPLY 0x2u      /* apply the mask to the header in place (header_crypto.rs:80-95) */
+#define QPP_ONLY_AES 0x10u     /* hint: every key in the batch is an AES-GCM key */
+#define QPP_ONLY_CHACHA 0x20u  /* hint: every key in the batch is ChaCha20-Poly1305 */
+
+/* Seal n packets: all pointers are device pointers (descs, arena, masks, status); masks may be NULL
+ * unless QPP_HP_MASK_OUT; status may be NULL (per-packet QPP_OK / QPP_DECODE_ERROR when the HP sample
+ * does not fit).  stream = hipStream_t or NULL for the context's stream.  Asynchronous. */
+int qpp_seal_batch(qpp_ctx *ctx, const qpp_pkt *descs, size_t n, uint8_t *arena, uint8_t *masks,
+                   int8_t *status, uint32_t flags, void *stream);
+/* Open n packets in place; status[i] = QPP_OK or QPP_DECRYPT_ERROR (payload zeroed on failure). */
+int qpp_open_batch(qpp_ctx *ctx, const qpp_pkt *descs, size_t n, uint8_t *arena, int8_t *status,
+                   uint32_t flags, void *stream);
+/* Header-protection masks for n packets: sample at off + aad_len - pn_len + 4 (for receive, pass
+ * aad_len = header_len and pn_len = 0).  masks[5*i]. */
+int qpp_hp_mask_batch(qpp_ctx *ctx, const qpp_pkt *descs, size_t n, const uint8_t *arena, uint8_t *masks,
+                      void *stream);
+
+/* ------------------------------------------------------------------ device plumbing */
+
+int qpp_dev_alloc(qpp_ctx *ctx, size_t bytes, void **out);
+void qpp_dev_free(qpp_ctx *ctx, void *ptr);
+int qpp_host_alloc(qpp_ctx *ctx, size_t bytes, void **out); /* pinned host memory */
+void qpp_host_free(qpp_ctx *ctx, void *ptr);
+int qpp_memcpy_h2d(qpp_ctx *ctx, void *dst, const void *src, size_t bytes, void *stream);
+int qpp_memcpy_d2h(qpp_ctx *ctx, void *dst, const void *src, size_t bytes, void *stream);
+int qpp_memset_d(qpp_ctx *ctx, void *dst, int value, size_t bytes, void *stream);
+int qpp_stream_create(qpp_ctx *ctx, void **out);
+void qpp_stream_destroy(qpp_ctx *ctx, void *stream);
+int qpp_stream_synchronize(qpp_ctx *ctx, void *stream);
+int qpp_event_create(qpp_ctx *ctx, void **out);
+void qpp_event_destroy(qpp_ctx *ctx, void *event);
+int qpp_event_record(qpp_ctx *ctx, void *event, void *stream);
+int qpp_event_elapsed_ms(qpp_ctx *ctx, void *start, void *stop, float *ms);
+/* Makes `stream` wait for `event` (copy/compute overlap across streams). */
+int qpp_stream_wait_event(qpp_ctx *ctx, void *stream, void *event);
+/* Last HIP error string of this context (for diagnostics). */
+const char *qpp_ctx_last_error(qpp_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

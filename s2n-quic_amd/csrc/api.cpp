@@ -1,0 +1,577 @@
+// api.cpp — host runtime behind include/qpp.h: contexts (one per GPU), the device key table, per-packet
+// trait mirrors (a batch of one on the GPU) and the batch entry points.  No CPU fallback exists: every
+// byte of payload is sealed/opened by the HIP kernels; without a gfx950 device the calls fail with
+// QPP_DEVICE_ERROR.
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "qpp_internal.h"
+
+using namespace qpp;
+
+struct qpp_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    // device key table + host mirror
+    DevKey *d_keys = nullptr;
+    uint32_t key_cap = 0;
+    std::vector<DevKey> h_keys;
+    std::vector<uint32_t> free_slots;
+    uint32_t next_slot = 0;
+    uint32_t dirty_lo = UINT32_MAX, dirty_hi = 0;
+    // plan scratch
+    PlanBuffers plan{};
+    uint32_t plan_n_cap = 0, plan_key_cap = 0;
+    // per-packet staging
+    uint8_t *d_stage = nullptr, *h_stage = nullptr;
+    size_t stage_cap = 0;
+    qpp_pkt *d_desc1 = nullptr;
+    int8_t *d_status1 = nullptr;
+    uint8_t *d_mask1 = nullptr;
+    PlanBuffers plan1{};  // host-built plan for a single AES packet
+    std::string last_error;
+};
+
+struct qpp_key {
+    qpp_ctx *ctx = nullptr;
+    int suite = 0;
+    uint32_t slot = 0;
+    bool has_secret = false;
+    uint8_t secret[48] = {0};
+    uint8_t key[32] = {0};
+    uint8_t iv[12] = {0};
+    uint8_t hp[32] = {0};
+};
+
+namespace {
+
+bool fail(qpp_ctx *ctx, hipError_t e, const char *what) {
+    if (e == hipSuccess) return false;
+    if (ctx) ctx->last_error = std::string(what) + ": " + hipGetErrorString(e);
+    return true;
+}
+#define HIP_TRY(ctx, expr)                                      \
+    do {                                                        \
+        if (fail((ctx), (expr), #expr)) return QPP_DEVICE_ERROR; \
+    } while (0)
+
+bool valid_suite(int s) {
+    return s == QPP_SUITE_TLS_AES_128_GCM_SHA256 || s == QPP_SUITE_TLS_AES_256_GCM_SHA384 ||
+           s == QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256;
+}
+
+int grow_keys(qpp_ctx *ctx, uint32_t need) {
+    if (need <= ctx->key_cap) return QPP_OK;
+    uint32_t cap = std::max<uint32_t>(64, ctx->key_cap);
+    while (cap < need) cap *= 2;
+    DevKey *nk = nullptr;
+    HIP_TRY(ctx, hipDeviceSynchronize());
+    HIP_TRY(ctx, hipMalloc(&nk, sizeof(DevKey) * cap));
+    HIP_TRY(ctx, hipMemset(nk, 0, sizeof(DevKey) * cap));
+    if (ctx->d_keys) {
+        HIP_TRY(ctx, hipMemcpy(nk, ctx->d_keys, sizeof(DevKey) * ctx->key_cap, hipMemcpyDeviceToDevice));
+        HIP_TRY(ctx, hipFree(ctx->d_keys));
+    }
+    ctx->d_keys = nk;
+    ctx->h_keys.resize(cap);
+    ctx->key_cap = cap;
+    return QPP_OK;
+}
+
+// Pushes pending key records to HBM and derives H / H*x^m on the GPU (key setup kernel).
+int flush_keys(qpp_ctx *ctx, hipStream_t s) {
+    if (ctx->dirty_lo >= ctx->dirty_hi) return QPP_OK;
+    const uint32_t lo = ctx->dirty_lo, cnt = ctx->dirty_hi - ctx->dirty_lo;
+    HIP_TRY(ctx, hipStreamSynchronize(s));
+    HIP_TRY(ctx, hipMemcpy(ctx->d_keys + lo, ctx->h_keys.data() + lo, sizeof(DevKey) * cnt, hipMemcpyHostToDevice));
+    HIP_TRY(ctx, launch_key_setup(ctx->d_keys, lo, cnt, s));
+    ctx->dirty_lo = UINT32_MAX;
+    ctx->dirty_hi = 0;
+    return QPP_OK;
+}
+
+int ensure_plan(qpp_ctx *ctx, uint32_t n) {
+    if (n <= ctx->plan_n_cap && ctx->key_cap <= ctx->plan_key_cap) return QPP_OK;
+    HIP_TRY(ctx, hipDeviceSynchronize());
+    PlanBuffers &p = ctx->plan;
+    hipFree(p.counts); hipFree(p.cursor); hipFree(p.istart); hipFree(p.perm); hipFree(p.work); hipFree(p.n_work);
+    const uint32_t ncap = std::max(n, ctx->plan_n_cap), kcap = ctx->key_cap;
+    HIP_TRY(ctx, hipMalloc(&p.counts, sizeof(uint32_t) * kcap));
+    HIP_TRY(ctx, hipMalloc(&p.cursor, sizeof(uint32_t) * kcap));
+    HIP_TRY(ctx, hipMalloc(&p.istart, sizeof(uint32_t) * (kcap + 1)));
+    HIP_TRY(ctx, hipMalloc(&p.perm, sizeof(uint32_t) * std::max<uint32_t>(ncap, 1)));
+    HIP_TRY(ctx, hipMalloc(&p.work, sizeof(WorkItem) * (plan_max_work(ncap, kcap) + 1)));
+    HIP_TRY(ctx, hipMalloc(&p.n_work, sizeof(uint32_t)));
+    ctx->plan_n_cap = ncap;
+    ctx->plan_key_cap = kcap;
+    return QPP_OK;
+}
+
+int ensure_stage(qpp_ctx *ctx, size_t bytes) {
+    if (bytes <= ctx->stage_cap) return QPP_OK;
+    size_t cap = std::max<size_t>(4096, ctx->stage_cap);
+    while (cap < bytes) cap *= 2;
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (ctx->d_stage) hipFree(ctx->d_stage);
+    if (ctx->h_stage) hipHostFree(ctx->h_stage);
+    HIP_TRY(ctx, hipMalloc(&ctx->d_stage, cap));
+    HIP_TRY(ctx, hipHostMalloc(&ctx->h_stage, cap, hipHostMallocDefault));
+    ctx->stage_cap = cap;
+    return QPP_OK;
+}
+
+uint32_t alloc_slot(qpp_ctx *ctx) {
+    if (!ctx->free_slots.empty()) {
+        uint32_t s = ctx->free_slots.back();
+        ctx->free_slots.pop_back();
+        return s;
+    }
+    return ctx->next_slot++;
+}
+
+// Fills the slot's host record from the key's material and marks it dirty.
+int install(qpp_key *k) {
+    qpp_ctx *ctx = k->ctx;
+    k->slot = alloc_slot(ctx);
+    int rc = grow_keys(ctx, k->slot + 1);
+    if (rc) return rc;
+    DevKey &d = ctx->h_keys[k->slot];
+    memset(&d, 0, sizeof d);
+    d.suite = (uint32_t)k->suite;
+    d.live = 1;
+    memcpy(d.iv, k->iv, 12);
+    if (k->suite == QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256) {
+        memcpy(d.rk, k->key, 32);
+        memcpy(d.hp_rk, k->hp, 32);
+    } else {
+        const size_t kl = suite_key_len(k->suite);
+        d.nr = (uint32_t)aes_expand_key(k->key, kl, d.rk);
+        d.hp_nr = (uint32_t)aes_expand_key(k->hp, kl, d.hp_rk);
+    }
+    ctx->dirty_lo = std::min(ctx->dirty_lo, k->slot);
+    ctx->dirty_hi = std::max(ctx->dirty_hi, k->slot + 1);
+    return QPP_OK;
+}
+
+void derive(qpp_key *k) {
+    const size_t hl = suite_hash_len(k->suite), kl = suite_key_len(k->suite);
+    hkdf_expand_label(hl, k->secret, "quic key", k->key, kl);
+    hkdf_expand_label(hl, k->secret, "quic iv", k->iv, 12);
+    hkdf_expand_label(hl, k->secret, "quic hp", k->hp, kl);
+}
+
+bool is_aes(int suite) { return suite != QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256; }
+
+// One packet through the batch kernels: stage = [pad4 | header | payload | tag].
+int run_one(const qpp_key *k, bool seal, uint64_t pn, const uint8_t *header, size_t header_len, const uint8_t *payload,
+            size_t payload_len, uint8_t *out, uint8_t *tag_out, int8_t *status_out) {
+    qpp_ctx *ctx = k->ctx;
+    if (header_len > 0xffff || payload_len > 0xffff) return QPP_INTERNAL_ERROR;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    const size_t total = 16 + header_len + payload_len + 16;
+    int rc = ensure_stage(ctx, total);
+    if (rc) return rc;
+    rc = flush_keys(ctx, ctx->stream);
+    if (rc) return rc;
+    uint8_t *h = ctx->h_stage;
+    memset(h, 0, total);
+    memcpy(h + 16, header, header_len);
+    memcpy(h + 16 + header_len, payload, payload_len);
+    if (!seal) memcpy(h + 16 + header_len + payload_len, tag_out, 16);
+    qpp_pkt d{};
+    d.pn = pn;
+    d.key_idx = k->slot;
+    d.off = 16;
+    d.aad_len = (uint16_t)header_len;
+    d.pt_len = (uint16_t)payload_len;
+    hipStream_t s = ctx->stream;
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->d_stage, h, total, hipMemcpyHostToDevice, s));
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->d_desc1, &d, sizeof d, hipMemcpyHostToDevice, s));
+    if (is_aes(k->suite)) {
+        // host-built plan for one packet: perm = {0}, one work item on this key
+        const uint32_t zero = 0, one = 1;
+        WorkItem w{k->slot, 0, 1, ctx->h_keys[k->slot].nr};
+        HIP_TRY(ctx, hipMemcpyAsync(ctx->plan1.perm, &zero, 4, hipMemcpyHostToDevice, s));
+        HIP_TRY(ctx, hipMemcpyAsync(ctx->plan1.work, &w, sizeof w, hipMemcpyHostToDevice, s));
+        HIP_TRY(ctx, hipMemcpyAsync(ctx->plan1.n_work, &one, 4, hipMemcpyHostToDevice, s));
+        // grid = plan_max_work(1, key_cap); only work item 0 exists
+        HIP_TRY(ctx, launch_aes_gcm(seal, ctx->d_keys, ctx->d_desc1, ctx->plan1, 1, 0, ctx->d_stage, ctx->d_mask1,
+                                    ctx->d_status1, 0, s));
+    } else {
+        HIP_TRY(ctx, launch_chacha(seal, ctx->d_keys, ctx->d_desc1, 1, ctx->d_stage, ctx->d_mask1, ctx->d_status1, 0, s));
+    }
+    int8_t st = QPP_OK;
+    HIP_TRY(ctx, hipMemcpyAsync(h, ctx->d_stage, total, hipMemcpyDeviceToHost, s));
+    HIP_TRY(ctx, hipMemcpyAsync(&st, ctx->d_status1, 1, hipMemcpyDeviceToHost, s));
+    HIP_TRY(ctx, hipStreamSynchronize(s));
+    memcpy(out, h + 16 + header_len, payload_len);
+    if (seal) memcpy(tag_out, h + 16 + header_len + payload_len, 16);
+    *status_out = st;
+    secure_zero(h, total);
+    return QPP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int qpp_abi_version(void) { return QPP_ABI_VERSION; }
+
+int qpp_ctx_create(int device, qpp_ctx **out) {
+    if (!out) return QPP_INTERNAL_ERROR;
+    *out = nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count) return QPP_DEVICE_ERROR;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return QPP_DEVICE_ERROR;
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return QPP_DEVICE_ERROR;  // kernels are built for gfx950 only
+    qpp_ctx *ctx = new qpp_ctx();
+    ctx->device = device;
+    int rc = QPP_OK;
+    do {
+        if (fail(ctx, hipSetDevice(device), "hipSetDevice")) { rc = QPP_DEVICE_ERROR; break; }
+        if (fail(ctx, hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking), "stream")) { rc = QPP_DEVICE_ERROR; break; }
+        if (fail(ctx, hipMalloc(&ctx->d_desc1, sizeof(qpp_pkt)), "alloc")) { rc = QPP_DEVICE_ERROR; break; }
+        if (fail(ctx, hipMalloc(&ctx->d_status1, 16), "alloc")) { rc = QPP_DEVICE_ERROR; break; }
+        if (fail(ctx, hipMalloc(&ctx->d_mask1, 16), "alloc")) { rc = QPP_DEVICE_ERROR; break; }
+        if (fail(ctx, hipMalloc(&ctx->plan1.perm, 16), "alloc")) { rc = QPP_DEVICE_ERROR; break; }
+        if (fail(ctx, hipMalloc(&ctx->plan1.work, sizeof(WorkItem) * 2), "alloc")) { rc = QPP_DEVICE_ERROR; break; }
+        if (fail(ctx, hipMalloc(&ctx->plan1.n_work, 16), "alloc")) { rc = QPP_DEVICE_ERROR; break; }
+        rc = grow_keys(ctx, 64);
+    } while (0);
+    if (rc) {
+        qpp_ctx_destroy(ctx);
+        return rc;
+    }
+    *out = ctx;
+    return QPP_OK;
+}
+
+void qpp_ctx_destroy(qpp_ctx *ctx) {
+    if (!ctx) return;
+    hipSetDevice(ctx->device);
+    hipDeviceSynchronize();
+    if (ctx->d_keys) { hipMemset(ctx->d_keys, 0, sizeof(DevKey) * ctx->key_cap); hipFree(ctx->d_keys); }
+    secure_zero(ctx->h_keys.data(), sizeof(DevKey) * ctx->h_keys.size());
+    PlanBuffers &p = ctx->plan;
+    hipFree(p.counts); hipFree(p.cursor); hipFree(p.istart); hipFree(p.perm); hipFree(p.work); hipFree(p.n_work);
+    hipFree(ctx->plan1.perm); hipFree(ctx->plan1.work); hipFree(ctx->plan1.n_work);
+    hipFree(ctx->d_stage);
+    if (ctx->h_stage) hipHostFree(ctx->h_stage);
+    hipFree(ctx->d_desc1); hipFree(ctx->d_status1); hipFree(ctx->d_mask1);
+    if (ctx->stream) hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+void *qpp_ctx_stream(qpp_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
+
+int qpp_ctx_synchronize(qpp_ctx *ctx) {
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    HIP_TRY(ctx, hipDeviceSynchronize());
+    return QPP_OK;
+}
+
+const char *qpp_ctx_last_error(qpp_ctx *ctx) { return ctx ? ctx->last_error.c_str() : "no context"; }
+
+// ---------------------------------------------------------------- keys
+
+int qpp_key_new(qpp_ctx *ctx, int suite, const uint8_t *secret, size_t secret_len, qpp_key **out) {
+    if (!ctx || !out || !secret) return QPP_INTERNAL_ERROR;
+    *out = nullptr;
+    if (!valid_suite(suite)) return QPP_UNSUPPORTED;
+    if (secret_len != suite_hash_len(suite)) return QPP_INTERNAL_ERROR;
+    qpp_key *k = new qpp_key();
+    k->ctx = ctx;
+    k->suite = suite;
+    k->has_secret = true;
+    memcpy(k->secret, secret, secret_len);
+    derive(k);
+    int rc = install(k);
+    if (rc) { qpp_key_free(k); return rc; }
+    *out = k;
+    return QPP_OK;
+}
+
+int qpp_key_new_raw(qpp_ctx *ctx, int suite, const uint8_t *key, size_t key_len, const uint8_t iv[12],
+                    const uint8_t *hp, size_t hp_len, qpp_key **out) {
+    if (!ctx || !out || !key || !iv || !hp) return QPP_INTERNAL_ERROR;
+    *out = nullptr;
+    if (!valid_suite(suite)) return QPP_UNSUPPORTED;
+    if (key_len != suite_key_len(suite) || hp_len != suite_key_len(suite)) return QPP_INTERNAL_ERROR;
+    qpp_key *k = new qpp_key();
+    k->ctx = ctx;
+    k->suite = suite;
+    memcpy(k->key, key, key_len);
+    memcpy(k->iv, iv, 12);
+    memcpy(k->hp, hp, hp_len);
+    int rc = install(k);
+    if (rc) { qpp_key_free(k); return rc; }
+    *out = k;
+    return QPP_OK;
+}
+
+int qpp_key_update(const qpp_key *key, qpp_key **out) {
+    if (!key || !out) return QPP_INTERNAL_ERROR;
+    *out = nullptr;
+    if (!key->has_secret) return QPP_INTERNAL_ERROR;
+    qpp_key *k = new qpp_key();
+    k->ctx = key->ctx;
+    k->suite = key->suite;
+    k->has_secret = true;
+    const size_t hl = suite_hash_len(key->suite);
+    hkdf_expand_label(hl, key->secret, "quic ku", k->secret, hl);
+    derive(k);
+    memcpy(k->hp, key->hp, sizeof k->hp);  // RFC 9001 §6: the header protection key is not updated
+    int rc = install(k);
+    if (rc) { qpp_key_free(k); return rc; }
+    *out = k;
+    return QPP_OK;
+}
+
+void qpp_key_free(qpp_key *key) {
+    if (!key) return;
+    qpp_ctx *ctx = key->ctx;
+    if (ctx && key->slot < ctx->key_cap && ctx->h_keys[key->slot].live) {
+        hipSetDevice(ctx->device);
+        secure_zero(&ctx->h_keys[key->slot], sizeof(DevKey));
+        hipMemset(ctx->d_keys + key->slot, 0, sizeof(DevKey));  // synchronous: zeroize the device copy
+        ctx->free_slots.push_back(key->slot);
+    }
+    secure_zero(key, sizeof *key);
+    delete key;
+}
+
+uint32_t qpp_key_slot(const qpp_key *key) { return key ? key->slot : UINT32_MAX; }
+int qpp_key_suite(const qpp_key *key) { return key ? key->suite : 0; }
+size_t qpp_tag_len(const qpp_key *) { return 16; }
+size_t qpp_sample_len(const qpp_key *) { return 16; }
+uint64_t qpp_confidentiality_limit(const qpp_key *key) {
+    // cipher_suite.rs:261,281,298 (RFC 9001 §6.6)
+    return key && key->suite == QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256 ? (1ULL << 62) : (1ULL << 23);
+}
+uint64_t qpp_integrity_limit(const qpp_key *key) {
+    // cipher_suite.rs:262,282,299
+    return key && key->suite == QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256 ? (1ULL << 36) : (1ULL << 52);
+}
+
+int qpp_key_material(const qpp_key *key, uint8_t *key_out, uint8_t iv_out[12], uint8_t *hp_out) {
+    if (!key) return QPP_INTERNAL_ERROR;
+    const size_t kl = suite_key_len(key->suite);
+    if (key_out) memcpy(key_out, key->key, kl);
+    if (iv_out) memcpy(iv_out, key->iv, 12);
+    if (hp_out) memcpy(hp_out, key->hp, kl);
+    return QPP_OK;
+}
+
+int qpp_initial_keys(qpp_ctx *ctx, int endpoint, const uint8_t *dcid, size_t dcid_len, qpp_key **sealer,
+                     qpp_key **opener) {
+    // quic/s2n-quic-crypto/src/initial.rs:29-68; salt quic/s2n-quic-core/src/crypto/initial.rs:29
+    static const uint8_t salt[20] = {0x38, 0x76, 0x2c, 0xf7, 0xf5, 0x59, 0x34, 0xb3, 0x4d, 0x17,
+                                     0x9a, 0xe6, 0xa4, 0xc8, 0x0c, 0xad, 0xcc, 0xbb, 0x7f, 0x0a};
+    if (!ctx || !sealer || !opener || (!dcid && dcid_len)) return QPP_INTERNAL_ERROR;
+    uint8_t prk[32], client[32], server[32];
+    hkdf_extract(32, salt, sizeof salt, dcid, dcid_len, prk);
+    hkdf_expand_label(32, prk, "client in", client, 32);
+    hkdf_expand_label(32, prk, "server in", server, 32);
+    const bool is_client = endpoint == QPP_ENDPOINT_CLIENT;
+    int rc = qpp_key_new(ctx, QPP_SUITE_TLS_AES_128_GCM_SHA256, is_client ? client : server, 32, sealer);
+    if (!rc) {
+        rc = qpp_key_new(ctx, QPP_SUITE_TLS_AES_128_GCM_SHA256, is_client ? server : client, 32, opener);
+        if (rc) { qpp_key_free(*sealer); *sealer = nullptr; }
+    }
+    secure_zero(prk, sizeof prk); secure_zero(client, sizeof client); secure_zero(server, sizeof server);
+    return rc;
+}
+
+// ---------------------------------------------------------------- per packet
+
+int qpp_seal(qpp_key *key, uint64_t pn, const uint8_t *header, size_t header_len, uint8_t *payload, size_t payload_len,
+             size_t payload_cap) {
+    if (!key || (!header && header_len) || (!payload && payload_len)) return QPP_INTERNAL_ERROR;
+    if (payload_cap < payload_len + 16) return QPP_INTERNAL_ERROR;
+    int8_t st;
+    int rc = run_one(key, true, pn, header, header_len, payload, payload_len, payload, payload + payload_len, &st);
+    return rc ? rc : st;
+}
+
+int qpp_seal_scatter(qpp_key *key, uint64_t pn, const uint8_t *header, size_t header_len, uint8_t *in_out,
+                     size_t in_len, const uint8_t *extra_in, size_t extra_len, uint8_t *extra_out_and_tag) {
+    if (!key || (!in_out && in_len) || (!extra_in && extra_len) || !extra_out_and_tag) return QPP_INTERNAL_ERROR;
+    std::vector<uint8_t> flat(in_len + extra_len);
+    if (in_len) memcpy(flat.data(), in_out, in_len);
+    if (extra_len) memcpy(flat.data() + in_len, extra_in, extra_len);
+    int8_t st;
+    int rc = run_one(key, true, pn, header, header_len, flat.data(), flat.size(), flat.data(), extra_out_and_tag + extra_len, &st);
+    if (!rc) {
+        if (in_len) memcpy(in_out, flat.data(), in_len);
+        if (extra_len) memcpy(extra_out_and_tag, flat.data() + in_len, extra_len);
+    }
+    secure_zero(flat.data(), flat.size());
+    return rc ? rc : st;
+}
+
+int qpp_open(const qpp_key *key, uint64_t pn, const uint8_t *header, size_t header_len, uint8_t *payload,
+             size_t payload_len) {
+    if (!key || (!header && header_len) || (!payload && payload_len)) return QPP_INTERNAL_ERROR;
+    if (payload_len < 16) return QPP_DECRYPT_ERROR;  // cipher_suite.rs:126-129
+    uint8_t tag[16];
+    memcpy(tag, payload + payload_len - 16, 16);
+    int8_t st;
+    int rc = run_one(key, false, pn, header, header_len, payload, payload_len - 16, payload, tag, &st);
+    return rc ? rc : st;
+}
+
+int qpp_hp_mask(const qpp_key *key, const uint8_t *sample, size_t sample_len, uint8_t mask[5]) {
+    if (!key || !sample || !mask || sample_len < 16) return QPP_INTERNAL_ERROR;
+    qpp_ctx *ctx = key->ctx;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    int rc = ensure_stage(ctx, 64);
+    if (rc) return rc;
+    rc = flush_keys(ctx, ctx->stream);
+    if (rc) return rc;
+    memset(ctx->h_stage, 0, 64);
+    memcpy(ctx->h_stage + 4, sample, 16);
+    qpp_pkt d{};
+    d.key_idx = key->slot;  // off = aad_len = pn_len = 0: sample at offset 4
+    hipStream_t s = ctx->stream;
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->d_stage, ctx->h_stage, 64, hipMemcpyHostToDevice, s));
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->d_desc1, &d, sizeof d, hipMemcpyHostToDevice, s));
+    HIP_TRY(ctx, launch_hp_mask(ctx->d_keys, ctx->d_desc1, 1, ctx->d_stage, ctx->d_mask1, s));
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->h_stage + 32, ctx->d_mask1, 5, hipMemcpyDeviceToHost, s));
+    HIP_TRY(ctx, hipStreamSynchronize(s));
+    memcpy(mask, ctx->h_stage + 32, 5);
+    return QPP_OK;
+}
+
+// ---------------------------------------------------------------- batches
+
+int qpp_seal_batch(qpp_ctx *ctx, const qpp_pkt *descs, size_t n, uint8_t *arena, uint8_t *masks, int8_t *status,
+                   uint32_t flags, void *stream) {
+    if (!ctx || (n && (!descs || !arena))) return QPP_INTERNAL_ERROR;
+    if ((flags & QPP_HP_MASK_OUT) && !masks) return QPP_INTERNAL_ERROR;
+    if (n > UINT32_MAX) return QPP_INTERNAL_ERROR;
+    if (!n) return QPP_OK;
+    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    int rc = flush_keys(ctx, s);
+    if (rc) return rc;
+    if (!(flags & QPP_ONLY_CHACHA)) {
+        rc = ensure_plan(ctx, (uint32_t)n);
+        if (rc) return rc;
+        HIP_TRY(ctx, launch_plan(ctx->d_keys, ctx->key_cap, descs, (uint32_t)n, ctx->plan, s));
+        HIP_TRY(ctx, launch_aes_gcm(true, ctx->d_keys, descs, ctx->plan, (uint32_t)n, ctx->key_cap, arena, masks, status,
+                                    flags, s));
+    }
+    if (!(flags & QPP_ONLY_AES))
+        HIP_TRY(ctx, launch_chacha(true, ctx->d_keys, descs, (uint32_t)n, arena, masks, status, flags, s));
+    return QPP_OK;
+}
+
+int qpp_open_batch(qpp_ctx *ctx, const qpp_pkt *descs, size_t n, uint8_t *arena, int8_t *status, uint32_t flags,
+                   void *stream) {
+    if (!ctx || (n && (!descs || !arena || !status))) return QPP_INTERNAL_ERROR;
+    if (n > UINT32_MAX) return QPP_INTERNAL_ERROR;
+    if (!n) return QPP_OK;
+    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    int rc = flush_keys(ctx, s);
+    if (rc) return rc;
+    if (!(flags & QPP_ONLY_CHACHA)) {
+        rc = ensure_plan(ctx, (uint32_t)n);
+        if (rc) return rc;
+        HIP_TRY(ctx, launch_plan(ctx->d_keys, ctx->key_cap, descs, (uint32_t)n, ctx->plan, s));
+        HIP_TRY(ctx, launch_aes_gcm(false, ctx->d_keys, descs, ctx->plan, (uint32_t)n, ctx->key_cap, arena, nullptr,
+                                    status, 0, s));
+    }
+    if (!(flags & QPP_ONLY_AES))
+        HIP_TRY(ctx, launch_chacha(false, ctx->d_keys, descs, (uint32_t)n, arena, nullptr, status, 0, s));
+    return QPP_OK;
+}
+
+int qpp_hp_mask_batch(qpp_ctx *ctx, const qpp_pkt *descs, size_t n, const uint8_t *arena, uint8_t *masks,
+                      void *stream) {
+    if (!ctx || (n && (!descs || !arena || !masks))) return QPP_INTERNAL_ERROR;
+    if (!n) return QPP_OK;
+    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    int rc = flush_keys(ctx, s);
+    if (rc) return rc;
+    HIP_TRY(ctx, launch_hp_mask(ctx->d_keys, descs, (uint32_t)n, arena, masks, s));
+    return QPP_OK;
+}
+
+// ---------------------------------------------------------------- plumbing
+
+int qpp_dev_alloc(qpp_ctx *ctx, size_t bytes, void **out) {
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    HIP_TRY(ctx, hipMalloc(out, bytes ? bytes : 1));
+    return QPP_OK;
+}
+void qpp_dev_free(qpp_ctx *ctx, void *ptr) {
+    if (!ptr) return;
+    hipSetDevice(ctx->device);
+    hipFree(ptr);
+}
+int qpp_host_alloc(qpp_ctx *ctx, size_t bytes, void **out) {
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    HIP_TRY(ctx, hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault));
+    return QPP_OK;
+}
+void qpp_host_free(qpp_ctx *, void *ptr) {
+    if (ptr) hipHostFree(ptr);
+}
+int qpp_memcpy_h2d(qpp_ctx *ctx, void *dst, const void *src, size_t bytes, void *stream) {
+    HIP_TRY(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, stream ? (hipStream_t)stream : ctx->stream));
+    return QPP_OK;
+}
+int qpp_memcpy_d2h(qpp_ctx *ctx, void *dst, const void *src, size_t bytes, void *stream) {
+    HIP_TRY(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, stream ? (hipStream_t)stream : ctx->stream));
+    return QPP_OK;
+}
+int qpp_memset_d(qpp_ctx *ctx, void *dst, int value, size_t bytes, void *stream) {
+    HIP_TRY(ctx, hipMemsetAsync(dst, value, bytes, stream ? (hipStream_t)stream : ctx->stream));
+    return QPP_OK;
+}
+int qpp_stream_create(qpp_ctx *ctx, void **out) {
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    hipStream_t s;
+    HIP_TRY(ctx, hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    *out = (void *)s;
+    return QPP_OK;
+}
+void qpp_stream_destroy(qpp_ctx *, void *stream) {
+    if (stream) hipStreamDestroy((hipStream_t)stream);
+}
+int qpp_stream_synchronize(qpp_ctx *ctx, void *stream) {
+    HIP_TRY(ctx, hipStreamSynchronize(stream ? (hipStream_t)stream : ctx->stream));
+    return QPP_OK;
+}
+int qpp_event_create(qpp_ctx *ctx, void **out) {
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    hipEvent_t e;
+    HIP_TRY(ctx, hipEventCreate(&e));
+    *out = (void *)e;
+    return QPP_OK;
+}
+void qpp_event_destroy(qpp_ctx *, void *event) {
+    if (event) hipEventDestroy((hipEvent_t)event);
+}
+int qpp_event_record(qpp_ctx *ctx, void *event, void *stream) {
+    HIP_TRY(ctx, hipEventRecord((hipEvent_t)event, stream ? (hipStream_t)stream : ctx->stream));
+    return QPP_OK;
+}
+int qpp_event_elapsed_ms(qpp_ctx *ctx, void *start, void *stop, float *ms) {
+    HIP_TRY(ctx, hipEventSynchronize((hipEvent_t)stop));
+    HIP_TRY(ctx, hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)stop));
+    return QPP_OK;
+}
+
+int qpp_stream_wait_event(qpp_ctx *ctx, void *stream, void *event) {
+    HIP_TRY(ctx, hipStreamWaitEvent(stream ? (hipStream_t)stream : ctx->stream, (hipEvent_t)event, 0));
+    return QPP_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,270 @@
+// chacha.hip — ChaCha20-Poly1305 seal/open + the standalone header-protection mask kernel (gfx950).
+//
+// Replaces, for TLS_CHACHA20_POLY1305_SHA256 (quic/s2n-quic-crypto/src/cipher_suite.rs:270-284,
+// cipher_suite/ring.rs:121), aws-lc-rs's RFC 8439 AEAD behind <LessSafeKey as Aead>::{encrypt,decrypt}
+// (src/aead/default.rs:44-93) and quic::CHACHA20 HeaderProtectionKey::new_mask (src/header_key.rs:52-56):
+//   mask = ChaCha20(hp, counter = LE32(sample[0..4]), nonce = sample[4..16]) over 5 zero bytes.
+//
+// Mapping: one lane per packet, pure VALU (ARX + 26-bit-limb Poly1305), no LDS, so keys are per
+// lane and a mixed-key batch needs no grouping.  Each iteration produces one 64-byte keystream block,
+// seals 4 x 16 bytes and absorbs them into Poly1305.
+#include "device_common.h"
+
+namespace qpp {
+namespace {
+using namespace dev;
+
+__device__ __forceinline__ uint32_t rotl(uint32_t v, int c) { return __builtin_amdgcn_alignbit(v, v, 32 - c); }
+
+#define QR(a, b, c, d)                \
+    a += b; d ^= a; d = rotl(d, 16);  \
+    c += d; b ^= c; b = rotl(b, 12);  \
+    a += b; d ^= a; d = rotl(d, 8);   \
+    c += d; b ^= c; b = rotl(b, 7);
+
+// RFC 8439 §2.3 block function: out[16] = keystream words
+__device__ __forceinline__ void chacha_block(const uint32_t k[8], uint32_t ctr, uint32_t n0, uint32_t n1, uint32_t n2,
+                                             uint32_t out[16]) {
+    uint32_t x[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u, k[0], k[1], k[2], k[3],
+                      k[4], k[5], k[6], k[7], ctr, n0, n1, n2};
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+        QR(x[0], x[4], x[8], x[12]);
+        QR(x[1], x[5], x[9], x[13]);
+        QR(x[2], x[6], x[10], x[14]);
+        QR(x[3], x[7], x[11], x[15]);
+        QR(x[0], x[5], x[10], x[15]);
+        QR(x[1], x[6], x[11], x[12]);
+        QR(x[2], x[7], x[8], x[13]);
+        QR(x[3], x[4], x[9], x[14]);
+    }
+    const uint32_t in[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u, k[0], k[1], k[2], k[3],
+                             k[4], k[5], k[6], k[7], ctr, n0, n1, n2};
+#pragma unroll
+    for (int i = 0; i < 16; i++) out[i] = x[i] + in[i];
+}
+
+// Poly1305 (RFC 8439 §2.5) in 5 x 26-bit limbs; every block of the AEAD MAC stream is a full 16-byte
+// block (AAD and ciphertext are zero-padded), so the 2^128 bit is always set.
+struct Poly1305 {
+    uint32_t r0, r1, r2, r3, r4, s1, s2, s3, s4;
+    uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0, h4 = 0;
+
+    __device__ __forceinline__ void init(uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
+        r0 = k0 & 0x3ffffff;
+        r1 = ((k0 >> 26) | (k1 << 6)) & 0x3ffff03;
+        r2 = ((k1 >> 20) | (k2 << 12)) & 0x3ffc0ff;
+        r3 = ((k2 >> 14) | (k3 << 18)) & 0x3f03fff;
+        r4 = (k3 >> 8) & 0x00fffff;
+        s1 = r1 * 5; s2 = r2 * 5; s3 = r3 * 5; s4 = r4 * 5;
+    }
+    __device__ __forceinline__ void block(uint4 m) {
+        h0 += m.x & 0x3ffffff;
+        h1 += ((m.x >> 26) | (m.y << 6)) & 0x3ffffff;
+        h2 += ((m.y >> 20) | (m.z << 12)) & 0x3ffffff;
+        h3 += ((m.z >> 14) | (m.w << 18)) & 0x3ffffff;
+        h4 += (m.w >> 8) | (1u << 24);
+        uint64_t d0 = (uint64_t)h0 * r0 + (uint64_t)h1 * s4 + (uint64_t)h2 * s3 + (uint64_t)h3 * s2 + (uint64_t)h4 * s1;
+        uint64_t d1 = (uint64_t)h0 * r1 + (uint64_t)h1 * r0 + (uint64_t)h2 * s4 + (uint64_t)h3 * s3 + (uint64_t)h4 * s2;
+        uint64_t d2 = (uint64_t)h0 * r2 + (uint64_t)h1 * r1 + (uint64_t)h2 * r0 + (uint64_t)h3 * s4 + (uint64_t)h4 * s3;
+        uint64_t d3 = (uint64_t)h0 * r3 + (uint64_t)h1 * r2 + (uint64_t)h2 * r1 + (uint64_t)h3 * r0 + (uint64_t)h4 * s4;
+        uint64_t d4 = (uint64_t)h0 * r4 + (uint64_t)h1 * r3 + (uint64_t)h2 * r2 + (uint64_t)h3 * r1 + (uint64_t)h4 * r0;
+        uint32_t c;
+        c = (uint32_t)(d0 >> 26); h0 = (uint32_t)d0 & 0x3ffffff;
+        d1 += c; c = (uint32_t)(d1 >> 26); h1 = (uint32_t)d1 & 0x3ffffff;
+        d2 += c; c = (uint32_t)(d2 >> 26); h2 = (uint32_t)d2 & 0x3ffffff;
+        d3 += c; c = (uint32_t)(d3 >> 26); h3 = (uint32_t)d3 & 0x3ffffff;
+        d4 += c; c = (uint32_t)(d4 >> 26); h4 = (uint32_t)d4 & 0x3ffffff;
+        h0 += c * 5; c = h0 >> 26; h0 &= 0x3ffffff;
+        h1 += c;
+    }
+    // tag = (h mod p + s) mod 2^128
+    __device__ __forceinline__ uint4 finish(uint32_t s0w, uint32_t s1w, uint32_t s2w, uint32_t s3w) {
+        uint32_t c;
+        c = h1 >> 26; h1 &= 0x3ffffff; h2 += c;
+        c = h2 >> 26; h2 &= 0x3ffffff; h3 += c;
+        c = h3 >> 26; h3 &= 0x3ffffff; h4 += c;
+        c = h4 >> 26; h4 &= 0x3ffffff; h0 += c * 5;
+        c = h0 >> 26; h0 &= 0x3ffffff; h1 += c;
+        // g = h + 5 - 2^130
+        uint32_t g0 = h0 + 5; c = g0 >> 26; g0 &= 0x3ffffff;
+        uint32_t g1 = h1 + c; c = g1 >> 26; g1 &= 0x3ffffff;
+        uint32_t g2 = h2 + c; c = g2 >> 26; g2 &= 0x3ffffff;
+        uint32_t g3 = h3 + c; c = g3 >> 26; g3 &= 0x3ffffff;
+        uint32_t g4 = h4 + c - (1u << 26);
+        uint32_t sel = (g4 >> 31) - 1;  // all ones if h >= p
+        h0 = (h0 & ~sel) | (g0 & sel); h1 = (h1 & ~sel) | (g1 & sel); h2 = (h2 & ~sel) | (g2 & sel);
+        h3 = (h3 & ~sel) | (g3 & sel); h4 = (h4 & ~sel) | (g4 & sel);
+        uint32_t w0 = h0 | (h1 << 26), w1 = (h1 >> 6) | (h2 << 20), w2 = (h2 >> 12) | (h3 << 14), w3 = (h3 >> 18) | (h4 << 8);
+        uint64_t f = (uint64_t)w0 + s0w; w0 = (uint32_t)f;
+        f = (uint64_t)w1 + s1w + (f >> 32); w1 = (uint32_t)f;
+        f = (uint64_t)w2 + s2w + (f >> 32); w2 = (uint32_t)f;
+        f = (uint64_t)w3 + s3w + (f >> 32); w3 = (uint32_t)f;
+        return make_uint4(w0, w1, w2, w3);
+    }
+};
+
+__device__ __forceinline__ uint32_t chacha_hp_word(const uint32_t hk[8], uint4 sample, uint32_t *w1) {
+    uint32_t ks[16];
+    chacha_block(hk, sample.x, sample.y, sample.z, sample.w, ks);
+    *w1 = ks[1];
+    return ks[0];
+}
+
+__device__ __forceinline__ void apply_mask(uint8_t *base, uint32_t hdr_len, uint32_t pn_len, uint32_t m0, uint32_t m1,
+                                           uint8_t *mask_out, uint32_t flags) {
+    if (flags & QPP_HP_MASK_OUT) {
+        mask_out[0] = (uint8_t)m0; mask_out[1] = (uint8_t)(m0 >> 8); mask_out[2] = (uint8_t)(m0 >> 16);
+        mask_out[3] = (uint8_t)(m0 >> 24); mask_out[4] = (uint8_t)m1;
+    }
+    if (flags & QPP_HP_APPLY) {  // header_crypto.rs:80-95
+        uint8_t b0 = base[0];
+        base[0] = b0 ^ ((uint8_t)m0 & ((b0 & 0x80) ? 0x0f : 0x1f));
+        uint32_t mm = (m0 >> 8) | (m1 << 24);
+        for (uint32_t i = 0; i < pn_len; i++) base[hdr_len + i] ^= (uint8_t)(mm >> (8 * i));
+    }
+}
+
+template <bool SEAL>
+__global__ __launch_bounds__(256) void chacha_kernel(const DevKey *__restrict__ keys, const qpp_pkt *__restrict__ descs,
+                                                    uint32_t n, uint8_t *__restrict__ arena, uint8_t *masks,
+                                                    int8_t *status, uint32_t flags) {
+    const uint32_t pi = blockIdx.x * blockDim.x + threadIdx.x;
+    if (pi >= n) return;
+    const qpp_pkt d = descs[pi];
+    const DevKey *__restrict__ key = keys + d.key_idx;
+    if (key->suite != QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256) return;  // AES packets: aes_gcm_kernel
+    uint32_t k[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) k[i] = key->rk[i];
+    // Iv::nonce (src/iv.rs:27-39)
+    const uint32_t n0 = key->iv[0], n1 = key->iv[1] ^ bswap32((uint32_t)(d.pn >> 32)), n2 = key->iv[2] ^ bswap32((uint32_t)d.pn);
+    uint8_t *base = arena + d.off;
+    const uint32_t aad_len = d.aad_len, len = d.pt_len;
+    uint8_t *pay = base + aad_len;
+
+    uint32_t ks[16];
+    chacha_block(k, 0, n0, n1, n2, ks);  // one-time Poly1305 key
+    Poly1305 mac;
+    mac.init(ks[0], ks[1], ks[2], ks[3]);
+    const uint32_t sw0 = ks[4], sw1 = ks[5], sw2 = ks[6], sw3 = ks[7];
+    for (uint32_t off = 0; off < aad_len; off += 16) {
+        uint4 a = ld16(base + off);
+        if (aad_len - off < 16) a = keep_bytes(a, aad_len - off);
+        mac.block(a);
+    }
+    uint4 c0 = make_uint4(0, 0, 0, 0), c1 = c0;
+    for (uint32_t off = 0, ctr = 1; off < len; off += 64, ctr++) {
+        chacha_block(k, ctr, n0, n1, n2, ks);
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint32_t o = off + 16 * q;
+            if (o < len) {
+                uint4 in = ld16(pay + o);  // in bounds: payload||tag
+                uint4 out = in ^ make_uint4(ks[4 * q], ks[4 * q + 1], ks[4 * q + 2], ks[4 * q + 3]);
+                const uint32_t r = len - o;
+                uint4 c;
+                if (r >= 16) {
+                    st16(pay + o, out);
+                    c = SEAL ? out : in;
+                } else {
+                    out = keep_bytes(out, r);
+                    st_bytes(pay + o, out, r);
+                    c = SEAL ? out : keep_bytes(in, r);
+                }
+                if (o == 0) c0 = c;
+                if (o == 16) c1 = c;
+                mac.block(c);
+            }
+        }
+    }
+    mac.block(make_uint4(aad_len, 0, len, 0));  // le64(aad_len) || le64(ct_len)
+    const uint4 tag = mac.finish(sw0, sw1, sw2, sw3);
+
+    if (SEAL) {
+        st16(pay + len, tag);
+        int8_t st = QPP_OK;
+        if (flags & (QPP_HP_MASK_OUT | QPP_HP_APPLY)) {
+            const uint32_t s = 4 - d.pn_len;
+            if (d.pn_len < 1 || d.pn_len > 4 || len < s) {
+                st = QPP_DECODE_ERROR;
+            } else {
+                uint4 smp;
+                if (len >= 32) {
+                    smp.x = __builtin_amdgcn_alignbyte(c0.y, c0.x, s);
+                    smp.y = __builtin_amdgcn_alignbyte(c0.z, c0.y, s);
+                    smp.z = __builtin_amdgcn_alignbyte(c0.w, c0.z, s);
+                    smp.w = __builtin_amdgcn_alignbyte(c1.x, c0.w, s);
+                } else {
+                    smp = ld16(pay + s);
+                }
+                uint32_t hk[8];
+#pragma unroll
+                for (int i = 0; i < 8; i++) hk[i] = key->hp_rk[i];
+                uint32_t m1, m0 = chacha_hp_word(hk, smp, &m1);
+                apply_mask(base, aad_len - d.pn_len, d.pn_len, m0, m1, masks + 5 * (size_t)pi, flags);
+            }
+        }
+        if (status) status[pi] = st;
+    } else {
+        const uint4 diff = tag ^ ld16(pay + len);
+        const bool ok = (diff.x | diff.y | diff.z | diff.w) == 0;
+        if (!ok) {
+            for (uint32_t o = 0; o < len; o += 16) {
+                if (len - o >= 16) st16(pay + o, make_uint4(0, 0, 0, 0));
+                else st_bytes(pay + o, make_uint4(0, 0, 0, 0), len - o);
+            }
+        }
+        status[pi] = ok ? QPP_OK : QPP_DECRYPT_ERROR;
+    }
+}
+
+// Header-protection masks for any suite, one lane per packet; AES keys use the LDS T-tables with the
+// lane's own round keys.  Sample at off + aad_len - pn_len + 4.
+__global__ __launch_bounds__(1024) void hp_mask_kernel(const DevKey *__restrict__ keys, const qpp_pkt *__restrict__ descs,
+                                                      uint32_t n, const uint8_t *__restrict__ arena, uint8_t *masks) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    build_aes_tables(lds);
+    __syncthreads();
+    const uint32_t pi = blockIdx.x * blockDim.x + threadIdx.x;
+    if (pi >= n) return;
+    const qpp_pkt d = descs[pi];
+    const DevKey *__restrict__ key = keys + d.key_idx;
+    const uint4 smp = ld16(arena + d.off + d.aad_len - d.pn_len + 4);
+    uint32_t m0, m1;
+    if (key->suite == QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256) {
+        uint32_t hk[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) hk[i] = key->hp_rk[i];
+        m0 = chacha_hp_word(hk, smp, &m1);
+    } else {
+        const AesLds aes = make_aes(lds);
+        uint4 m = key->hp_nr == 10 ? aes.encrypt<10>(smp, key->hp_rk) : aes.encrypt<14>(smp, key->hp_rk);
+        m0 = m.x; m1 = m.y;
+    }
+    uint8_t *o = masks + 5 * (size_t)pi;
+    o[0] = (uint8_t)m0; o[1] = (uint8_t)(m0 >> 8); o[2] = (uint8_t)(m0 >> 16); o[3] = (uint8_t)(m0 >> 24); o[4] = (uint8_t)m1;
+}
+
+}  // namespace
+
+hipError_t launch_chacha(bool seal, const DevKey *keys, const qpp_pkt *descs, uint32_t n, uint8_t *arena,
+                         uint8_t *masks, int8_t *status, uint32_t flags, hipStream_t s) {
+    if (!n) return hipSuccess;
+    const dim3 grid((n + 255) / 256), block(256);
+    if (seal)
+        hipLaunchKernelGGL(chacha_kernel<true>, grid, block, 0, s, keys, descs, n, arena, masks, status, flags);
+    else
+        hipLaunchKernelGGL(chacha_kernel<false>, grid, block, 0, s, keys, descs, n, arena, masks, status, flags);
+    return hipGetLastError();
+}
+
+hipError_t launch_hp_mask(const DevKey *keys, const qpp_pkt *descs, uint32_t n, const uint8_t *arena, uint8_t *masks,
+                          hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(hp_mask_kernel, dim3((n + 1023) / 1024), dim3(1024), dev::kLdsAes + 65536, s, keys, descs, n,
+                       arena, masks);
+    return hipGetLastError();
+}
+
+}  // namespace qpp

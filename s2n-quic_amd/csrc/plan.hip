@@ -1,0 +1,144 @@
+// plan.hip — groups the AES packets of a batch by key so that every AES-GCM workgroup serves ONE key
+// (its GHASH tables are per key and live in LDS).  Three small launches, all device-side, so a batch
+// whose descriptors are already in HBM never round-trips to the host:
+//   1. plan_hist   : packets per key (LDS-privatised counts, one global add per touched key per block)
+//   2. plan_scan   : one workgroup: key offsets, work list {key, begin, count<=1024, rounds}, n_work
+//   3. plan_scatter: perm[] = packet indices grouped by key (LDS ranks + one global reservation per key)
+// ChaCha20-Poly1305 packets are skipped (their kernel needs no grouping).
+// The reference has no batching at all (Key::encrypt is per packet); this is the
+// batch former the MI355X design adds in front of the kernels.
+#include "device_common.h"
+
+namespace qpp {
+namespace {
+
+constexpr int kPlanBlock = 1024;
+
+__device__ __forceinline__ bool is_aes(const DevKey *keys, uint32_t k) {
+    return keys[k].suite != QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256;
+}
+
+// key_cap <= kMaxPlanKeys: bins in LDS.  Larger key tables use global atomics directly.
+__global__ __launch_bounds__(kPlanBlock) void plan_hist(const DevKey *__restrict__ keys, uint32_t key_cap,
+                                                       const qpp_pkt *__restrict__ descs, uint32_t n,
+                                                       uint32_t *__restrict__ counts) {
+    __shared__ uint32_t bins[kMaxPlanKeys];
+    const bool local = key_cap <= (uint32_t)kMaxPlanKeys;
+    if (local)
+        for (uint32_t i = threadIdx.x; i < key_cap; i += blockDim.x) bins[i] = 0;
+    __syncthreads();
+    const uint32_t pi = blockIdx.x * blockDim.x + threadIdx.x;
+    if (pi < n) {
+        const uint32_t k = descs[pi].key_idx;
+        if (k < key_cap && is_aes(keys, k)) {
+            if (local) atomicAdd(&bins[k], 1u);
+            else atomicAdd(&counts[k], 1u);
+        }
+    }
+    __syncthreads();
+    if (local)
+        for (uint32_t i = threadIdx.x; i < key_cap; i += blockDim.x)
+            if (bins[i]) atomicAdd(&counts[i], bins[i]);
+}
+
+// Single workgroup.  Exclusive scans over keys of (a) packet counts -> cursor (scatter base per key) and
+// (b) work items per key -> istart; then every thread emits work items w = tid, tid+1024, ... by a binary
+// search of istart (in LDS), so a single key with 16 Ki work items is not written by one lane.
+__global__ __launch_bounds__(kPlanBlock) void plan_scan(const DevKey *__restrict__ keys, uint32_t key_cap,
+                                                       const uint32_t *__restrict__ counts, uint32_t *__restrict__ cursor,
+                                                       uint32_t *__restrict__ istart_g, WorkItem *__restrict__ work,
+                                                       uint32_t *__restrict__ n_work) {
+    __shared__ uint32_t sc[kPlanBlock], si[kPlanBlock];
+    __shared__ uint32_t istart_l[kMaxPlanKeys + 1];
+    __shared__ uint32_t carry_c, carry_i;
+    const bool local = key_cap <= (uint32_t)kMaxPlanKeys;
+    uint32_t *istart = local ? istart_l : istart_g;
+    if (threadIdx.x == 0) { carry_c = 0; carry_i = 0; }
+    __syncthreads();
+    for (uint32_t base = 0; base < key_cap; base += kPlanBlock) {
+        const uint32_t k = base + threadIdx.x;
+        const uint32_t c = k < key_cap ? counts[k] : 0;
+        const uint32_t items = (c + kPacketsPerGroup - 1) / kPacketsPerGroup;
+        sc[threadIdx.x] = c;
+        si[threadIdx.x] = items;
+        __syncthreads();
+        for (uint32_t off = 1; off < kPlanBlock; off <<= 1) {  // Hillis-Steele inclusive scan
+            uint32_t a = threadIdx.x >= off ? sc[threadIdx.x - off] : 0;
+            uint32_t b = threadIdx.x >= off ? si[threadIdx.x - off] : 0;
+            __syncthreads();
+            sc[threadIdx.x] += a;
+            si[threadIdx.x] += b;
+            __syncthreads();
+        }
+        if (k < key_cap) {
+            cursor[k] = carry_c + sc[threadIdx.x] - c;
+            istart[k] = carry_i + si[threadIdx.x] - items;
+        }
+        __syncthreads();
+        if (threadIdx.x == kPlanBlock - 1) { carry_c += sc[threadIdx.x]; carry_i += si[threadIdx.x]; }
+        __syncthreads();
+    }
+    const uint32_t total = carry_i;
+    if (threadIdx.x == 0) { istart[key_cap] = total; *n_work = total; }
+    __syncthreads();
+    for (uint32_t w = threadIdx.x; w < total; w += kPlanBlock) {
+        uint32_t lo = 0, hi = key_cap;  // largest k with istart[k] <= w (keys with no items share a start)
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (istart[mid] <= w) lo = mid; else hi = mid;
+        }
+        const uint32_t i = w - istart[lo];
+        const uint32_t left = counts[lo] - i * kPacketsPerGroup;
+        // cursor[] still holds the key's first perm index: plan_scatter runs after this kernel
+        work[w] = WorkItem{lo, cursor[lo] + i * kPacketsPerGroup,
+                           left < (uint32_t)kPacketsPerGroup ? left : (uint32_t)kPacketsPerGroup, keys[lo].nr};
+    }
+}
+
+__global__ __launch_bounds__(kPlanBlock) void plan_scatter(const DevKey *__restrict__ keys, uint32_t key_cap,
+                                                          const qpp_pkt *__restrict__ descs, uint32_t n,
+                                                          uint32_t *__restrict__ cursor, uint32_t *__restrict__ perm) {
+    __shared__ uint32_t bins[kMaxPlanKeys];
+    const bool local = key_cap <= (uint32_t)kMaxPlanKeys;
+    if (local)
+        for (uint32_t i = threadIdx.x; i < key_cap; i += blockDim.x) bins[i] = 0;
+    __syncthreads();
+    const uint32_t pi = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t k = 0xffffffffu, rank = 0;
+    if (pi < n) {
+        k = descs[pi].key_idx;
+        if (k >= key_cap || !is_aes(keys, k)) k = 0xffffffffu;
+        else if (local) rank = atomicAdd(&bins[k], 1u);
+        else perm[atomicAdd(&cursor[k], 1u)] = pi;
+    }
+    __syncthreads();
+    if (local) {
+        // reserve one contiguous range per touched key; reuse bins[] for the range start
+        for (uint32_t i = threadIdx.x; i < key_cap; i += blockDim.x)
+            if (bins[i]) bins[i] = atomicAdd(&cursor[i], bins[i]);
+        __syncthreads();
+        if (k != 0xffffffffu) perm[bins[k] + rank] = pi;
+    }
+}
+
+}  // namespace
+
+uint32_t plan_max_work(uint32_t n, uint32_t key_cap) {
+    const uint32_t by_packets = (n + kPacketsPerGroup - 1) / kPacketsPerGroup;
+    const uint32_t by_keys = key_cap < n ? key_cap : n;
+    return by_packets + by_keys;
+}
+
+hipError_t launch_plan(const DevKey *keys, uint32_t key_cap, const qpp_pkt *descs, uint32_t n, PlanBuffers pb,
+                       hipStream_t s) {
+    hipError_t e = hipMemsetAsync(pb.counts, 0, sizeof(uint32_t) * key_cap, s);
+    if (e != hipSuccess) return e;
+    const dim3 grid((n + kPlanBlock - 1) / kPlanBlock);
+    hipLaunchKernelGGL(plan_hist, grid, dim3(kPlanBlock), 0, s, keys, key_cap, descs, n, pb.counts);
+    hipLaunchKernelGGL(plan_scan, dim3(1), dim3(kPlanBlock), 0, s, keys, key_cap, pb.counts, pb.cursor, pb.istart, pb.work,
+                       pb.n_work);
+    hipLaunchKernelGGL(plan_scatter, grid, dim3(kPlanBlock), 0, s, keys, key_cap, descs, n, pb.cursor, pb.perm);
+    return hipGetLastError();
+}
+
+}  // namespace qpp

@@ -1,0 +1,106 @@
+// qpp_internal.h — shared between the host runtime (api.cpp, kdf.cpp) and the HIP kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../../include/qpp.h"
+
+namespace qpp {
+
+// ---------------------------------------------------------------- AES S-box, built at compile time
+// From its definition (FIPS-197 §5.1.1): multiplicative inverse in GF(2^8) (x^254) + affine map.
+constexpr uint8_t gf_mul(uint8_t a, uint8_t b) {
+    uint8_t p = 0;
+    for (int i = 0; i < 8; i++) {
+        if (b & 1) p ^= a;
+        a = (uint8_t)((a << 1) ^ ((a & 0x80) ? 0x1b : 0));
+        b >>= 1;
+    }
+    return p;
+}
+constexpr uint8_t gf_inv(uint8_t x) {
+    // x^254 = x^-1 (and 0 -> 0)
+    uint8_t r = 1, b = x;
+    for (int e = 254; e; e >>= 1) {
+        if (e & 1) r = gf_mul(r, b);
+        b = gf_mul(b, b);
+    }
+    return x ? r : 0;
+}
+struct SBox {
+    uint8_t v[256];
+    constexpr SBox() : v() {
+        for (int x = 0; x < 256; x++) {
+            uint8_t i = gf_inv((uint8_t)x), s = i, r = i;
+            for (int k = 0; k < 4; k++) {
+                r = (uint8_t)((r << 1) | (r >> 7));
+                s ^= r;
+            }
+            v[x] = (uint8_t)(s ^ 0x63);
+        }
+    }
+};
+constexpr SBox kSBox{};
+static_assert(kSBox.v[0x00] == 0x63 && kSBox.v[0x53] == 0xed && kSBox.v[0xff] == 0x16, "sbox");
+
+// ---------------------------------------------------------------- device key record
+// One per key slot, in HBM, replicated per GPU context.  Words are little-endian images of the
+// byte strings (dword c of an AES state = column c, row 0 in the low byte).
+struct alignas(16) DevKey {
+    uint32_t suite;      // qpp_suite
+    uint32_t nr;         // AES rounds of the packet key (10/14), 0 for ChaCha
+    uint32_t hp_nr;      // AES rounds of the HP key
+    uint32_t live;       // 1 while the slot holds a key
+    uint32_t iv[4];      // 12-byte iv, iv[3] = 0
+    uint32_t rk[60];     // AES round keys (11/15 x 4 words) | ChaCha key in rk[0..8)
+    uint32_t hp_rk[60];  // AES HP round keys                | ChaCha HP key in hp_rk[0..8)
+    uint32_t H[4];       // GHASH key E_K(0^128)                  (filled on device by key setup)
+    uint32_t V[128][4];  // V[m] = H * x^m in GCM bit order      (filled on device by key setup)
+};
+static_assert(sizeof(DevKey) == 2576, "DevKey layout");
+
+// Grouping of an AES batch by key (GHASH tables are per key and live in LDS).
+struct WorkItem {
+    uint32_t key;    // key slot
+    uint32_t begin;  // first index into perm[]
+    uint32_t count;  // packets (<= kPacketsPerGroup)
+    uint32_t nr;     // AES rounds for this key
+};
+
+constexpr int kPacketsPerGroup = 1024;  // one packet per lane, 16 waves per workgroup
+constexpr int kMaxPlanKeys = 8192;      // keys binned in LDS by the plan kernels (larger tables: global bins)
+
+// ---------------------------------------------------------------- launchers (aes_gcm.hip, chacha.hip, plan.hip)
+struct PlanBuffers {
+    uint32_t *counts;   // [key_cap] packets per key
+    uint32_t *cursor;   // [key_cap] scatter cursors
+    uint32_t *istart;   // [key_cap + 1] first work item per key (used when key_cap > kMaxPlanKeys)
+    uint32_t *perm;     // [n_cap] packet indices grouped by key
+    WorkItem *work;     // [n_cap / kPacketsPerGroup + key_cap + 1]
+    uint32_t *n_work;   // [1]
+};
+
+hipError_t launch_key_setup(DevKey *keys, uint32_t first, uint32_t count, hipStream_t s);
+hipError_t launch_plan(const DevKey *keys, uint32_t key_cap, const qpp_pkt *descs, uint32_t n, PlanBuffers pb,
+                       hipStream_t s);
+uint32_t plan_max_work(uint32_t n, uint32_t key_cap);
+hipError_t launch_aes_gcm(bool seal, const DevKey *keys, const qpp_pkt *descs, const PlanBuffers &pb, uint32_t n,
+                          uint32_t key_cap, uint8_t *arena, uint8_t *masks, int8_t *status, uint32_t flags,
+                          hipStream_t s);
+hipError_t launch_chacha(bool seal, const DevKey *keys, const qpp_pkt *descs, uint32_t n, uint8_t *arena,
+                         uint8_t *masks, int8_t *status, uint32_t flags, hipStream_t s);
+hipError_t launch_hp_mask(const DevKey *keys, const qpp_pkt *descs, uint32_t n, const uint8_t *arena,
+                          uint8_t *masks, hipStream_t s);
+
+// ---------------------------------------------------------------- host key schedule (kdf.cpp)
+size_t suite_key_len(int suite);
+size_t suite_hash_len(int suite);
+void hkdf_expand_label(size_t hash_len, const uint8_t *secret, const char *label, uint8_t *out, size_t out_len);
+void hkdf_extract(size_t hash_len, const uint8_t *salt, size_t salt_len, const uint8_t *ikm, size_t ikm_len,
+                  uint8_t *prk);
+int aes_expand_key(const uint8_t *key, size_t key_len, uint32_t rk[60]);  // returns rounds
+void secure_zero(void *p, size_t n);
+
+}  // namespace qpp

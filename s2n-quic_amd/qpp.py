@@ -1,0 +1,375 @@
+"""Python view of libqpp.so (the C ABI in include/qpp.h), for the tests, bench.py and smoke().
+
+The names mirror the reference's trait surface (quic/s2n-quic-core/src/crypto/key.rs:8-35,
+header_crypto.rs:11-31, one_rtt.rs:11-14) the way a Rust shim over the same ABI would:
+    Key.encrypt(pn, header, payload) -> sealed payload || tag          (Key::encrypt)
+    Key.decrypt(pn, header, payload) -> plaintext, raises DecryptError  (Key::decrypt)
+    Key.header_protection_mask(sample) -> 5 bytes                       (HeaderKey::*_mask)
+    Key.derive_next_key()                                               (OneRttKey::derive_next_key)
+plus the batch entry points over device buffers.
+
+There is NO fallback: if libqpp.so or a gfx950 GPU is missing, Context() raises.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libqpp.so")
+
+SUITE_AES_128_GCM = 1
+SUITE_AES_256_GCM = 2
+SUITE_CHACHA20_POLY1305 = 3
+SUITE_NAMES = {1: "TLS_AES_128_GCM_SHA256", 2: "TLS_AES_256_GCM_SHA384", 3: "TLS_CHACHA20_POLY1305_SHA256"}
+KEY_LEN = {1: 16, 2: 32, 3: 32}
+HASH_LEN = {1: 32, 2: 48, 3: 32}
+
+OK, DECODE_ERROR, DECRYPT_ERROR, INTERNAL_ERROR, UNSUPPORTED, DEVICE_ERROR = 0, 1, 2, 3, 4, 5
+HP_MASK_OUT, HP_APPLY, ONLY_AES, ONLY_CHACHA = 0x1, 0x2, 0x10, 0x20
+ENDPOINT_CLIENT, ENDPOINT_SERVER = 0, 1
+
+# qpp_pkt (24 bytes) as a numpy structured dtype
+PKT_DTYPE = np.dtype([("pn", "<u8"), ("key_idx", "<u4"), ("off", "<u4"), ("aad_len", "<u2"), ("pt_len", "<u2"),
+                      ("pn_len", "u1"), ("flags", "u1"), ("reserved", "<u2")])
+assert PKT_DTYPE.itemsize == 24
+
+# every symbol include/qpp.h declares (tests/test_abi.py checks the library exports them all)
+EXPORTS = [
+    "qpp_abi_version", "qpp_ctx_create", "qpp_ctx_destroy", "qpp_ctx_stream", "qpp_ctx_synchronize",
+    "qpp_ctx_last_error", "qpp_key_new", "qpp_key_new_raw", "qpp_key_update", "qpp_key_free", "qpp_key_slot",
+    "qpp_key_suite", "qpp_tag_len", "qpp_sample_len", "qpp_confidentiality_limit", "qpp_integrity_limit",
+    "qpp_key_material", "qpp_initial_keys", "qpp_seal", "qpp_seal_scatter", "qpp_open", "qpp_hp_mask",
+    "qpp_seal_batch", "qpp_open_batch", "qpp_hp_mask_batch", "qpp_dev_alloc", "qpp_dev_free", "qpp_host_alloc",
+    "qpp_host_free", "qpp_memcpy_h2d", "qpp_memcpy_d2h", "qpp_memset_d", "qpp_stream_create",
+    "qpp_stream_destroy", "qpp_stream_synchronize", "qpp_event_create", "qpp_event_destroy", "qpp_event_record",
+    "qpp_event_elapsed_ms", "qpp_stream_wait_event",
+]
+
+
+class QppError(RuntimeError):
+    def __init__(self, code, what=""):
+        self.code = code
+        names = {1: "DECODE_ERROR", 2: "DECRYPT_ERROR", 3: "INTERNAL_ERROR", 4: "UNSUPPORTED", 5: "DEVICE_ERROR"}
+        super().__init__(f"{names.get(code, code)} {what}".strip())
+
+
+class DecryptError(QppError):
+    """packet_protection::Error::DECRYPT_ERROR"""
+
+
+_lib = None
+vp, u8p, sz, u32, u64 = ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint8), ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint64
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise QppError(DEVICE_ERROR, f"{LIB_PATH} is not built (run __graft_entry__.build())")
+        L = ctypes.CDLL(LIB_PATH)
+        sig = {
+            "qpp_abi_version": (ctypes.c_int, []),
+            "qpp_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(vp)]),
+            "qpp_ctx_destroy": (None, [vp]),
+            "qpp_ctx_stream": (vp, [vp]),
+            "qpp_ctx_synchronize": (ctypes.c_int, [vp]),
+            "qpp_ctx_last_error": (ctypes.c_char_p, [vp]),
+            "qpp_key_new": (ctypes.c_int, [vp, ctypes.c_int, vp, sz, ctypes.POINTER(vp)]),
+            "qpp_key_new_raw": (ctypes.c_int, [vp, ctypes.c_int, vp, sz, vp, vp, sz, ctypes.POINTER(vp)]),
+            "qpp_key_update": (ctypes.c_int, [vp, ctypes.POINTER(vp)]),
+            "qpp_key_free": (None, [vp]),
+            "qpp_key_slot": (u32, [vp]),
+            "qpp_key_suite": (ctypes.c_int, [vp]),
+            "qpp_tag_len": (sz, [vp]),
+            "qpp_sample_len": (sz, [vp]),
+            "qpp_confidentiality_limit": (u64, [vp]),
+            "qpp_integrity_limit": (u64, [vp]),
+            "qpp_key_material": (ctypes.c_int, [vp, vp, vp, vp]),
+            "qpp_initial_keys": (ctypes.c_int, [vp, ctypes.c_int, vp, sz, ctypes.POINTER(vp), ctypes.POINTER(vp)]),
+            "qpp_seal": (ctypes.c_int, [vp, u64, vp, sz, vp, sz, sz]),
+            "qpp_seal_scatter": (ctypes.c_int, [vp, u64, vp, sz, vp, sz, vp, sz, vp]),
+            "qpp_open": (ctypes.c_int, [vp, u64, vp, sz, vp, sz]),
+            "qpp_hp_mask": (ctypes.c_int, [vp, vp, sz, vp]),
+            "qpp_seal_batch": (ctypes.c_int, [vp, vp, sz, vp, vp, vp, u32, vp]),
+            "qpp_open_batch": (ctypes.c_int, [vp, vp, sz, vp, vp, u32, vp]),
+            "qpp_hp_mask_batch": (ctypes.c_int, [vp, vp, sz, vp, vp, vp]),
+            "qpp_dev_alloc": (ctypes.c_int, [vp, sz, ctypes.POINTER(vp)]),
+            "qpp_dev_free": (None, [vp, vp]),
+            "qpp_host_alloc": (ctypes.c_int, [vp, sz, ctypes.POINTER(vp)]),
+            "qpp_host_free": (None, [vp, vp]),
+            "qpp_memcpy_h2d": (ctypes.c_int, [vp, vp, vp, sz, vp]),
+            "qpp_memcpy_d2h": (ctypes.c_int, [vp, vp, vp, sz, vp]),
+            "qpp_memset_d": (ctypes.c_int, [vp, vp, ctypes.c_int, sz, vp]),
+            "qpp_stream_create": (ctypes.c_int, [vp, ctypes.POINTER(vp)]),
+            "qpp_stream_destroy": (None, [vp, vp]),
+            "qpp_stream_synchronize": (ctypes.c_int, [vp, vp]),
+            "qpp_event_create": (ctypes.c_int, [vp, ctypes.POINTER(vp)]),
+            "qpp_event_destroy": (None, [vp, vp]),
+            "qpp_event_record": (ctypes.c_int, [vp, vp, vp]),
+            "qpp_event_elapsed_ms": (ctypes.c_int, [vp, vp, vp, ctypes.POINTER(ctypes.c_float)]),
+            "qpp_stream_wait_event": (ctypes.c_int, [vp, vp, vp]),
+        }
+        assert set(sig) == set(EXPORTS)
+        for name, (res, args) in sig.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _bytes_ptr(b):
+    buf = ctypes.create_string_buffer(bytes(b), max(len(b), 1))
+    return buf
+
+
+class DeviceBuffer:
+    """Raw device allocation owned by a Context."""
+
+    def __init__(self, ctx, nbytes):
+        self.ctx, self.nbytes = ctx, int(nbytes)
+        p = vp()
+        ctx._check(lib().qpp_dev_alloc(ctx.handle, self.nbytes, ctypes.byref(p)), "dev_alloc")
+        self.ptr = p.value
+
+    def upload(self, arr, stream=None, offset=0):
+        a = np.ascontiguousarray(arr)
+        assert offset + a.nbytes <= self.nbytes
+        self.ctx._check(lib().qpp_memcpy_h2d(self.ctx.handle, self.ptr + offset, a.ctypes.data, a.nbytes, stream), "h2d")
+        self.ctx.sync(stream)
+
+    def download(self, nbytes=None, stream=None, dtype=np.uint8, offset=0):
+        nbytes = self.nbytes - offset if nbytes is None else nbytes
+        out = np.empty(nbytes, dtype=np.uint8)
+        self.ctx._check(lib().qpp_memcpy_d2h(self.ctx.handle, out.ctypes.data, self.ptr + offset, nbytes, stream), "d2h")
+        self.ctx.sync(stream)
+        return out.view(dtype)
+
+    def free(self):
+        if self.ptr:
+            lib().qpp_dev_free(self.ctx.handle, self.ptr)
+            self.ptr = None
+
+
+class Context:
+    """One MI355X (qpp_ctx): device key table, default stream, batch entry points."""
+
+    def __init__(self, device=0):
+        h = vp()
+        rc = lib().qpp_ctx_create(int(device), ctypes.byref(h))
+        if rc != OK:
+            raise QppError(rc, f"qpp_ctx_create(device={device}): no usable gfx950 GPU (no CPU fallback exists)")
+        self.handle = h.value
+        self.device = device
+
+    def close(self):
+        if self.handle:
+            lib().qpp_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _check(self, rc, what):
+        if rc != OK:
+            err = lib().qpp_ctx_last_error(self.handle)
+            raise QppError(rc, f"{what}: {err.decode() if err else ''}")
+
+    @property
+    def stream(self):
+        return lib().qpp_ctx_stream(self.handle)
+
+    def sync(self, stream=None):
+        self._check(lib().qpp_stream_synchronize(self.handle, stream), "sync")
+
+    # keys
+    def key(self, suite, secret):
+        h = vp()
+        rc = lib().qpp_key_new(self.handle, suite, _bytes_ptr(secret), len(secret), ctypes.byref(h))
+        if rc != OK:
+            raise QppError(rc, "qpp_key_new")
+        return Key(self, h.value)
+
+    def raw_key(self, suite, key, iv, hp):
+        h = vp()
+        rc = lib().qpp_key_new_raw(self.handle, suite, _bytes_ptr(key), len(key), _bytes_ptr(iv), _bytes_ptr(hp),
+                                   len(hp), ctypes.byref(h))
+        if rc != OK:
+            raise QppError(rc, "qpp_key_new_raw")
+        return Key(self, h.value)
+
+    def initial_keys(self, endpoint, dcid):
+        s, o = vp(), vp()
+        rc = lib().qpp_initial_keys(self.handle, endpoint, _bytes_ptr(dcid), len(dcid), ctypes.byref(s), ctypes.byref(o))
+        if rc != OK:
+            raise QppError(rc, "qpp_initial_keys")
+        return Key(self, s.value), Key(self, o.value)
+
+    def alloc(self, nbytes):
+        return DeviceBuffer(self, nbytes)
+
+    # batches (device pointers)
+    def seal_batch(self, descs, n, arena, masks=None, status=None, flags=0, stream=None):
+        self._check(lib().qpp_seal_batch(self.handle, _ptr(descs), n, _ptr(arena), _ptr(masks), _ptr(status), flags,
+                                         stream), "seal_batch")
+
+    def open_batch(self, descs, n, arena, status, flags=0, stream=None):
+        self._check(lib().qpp_open_batch(self.handle, _ptr(descs), n, _ptr(arena), _ptr(status), flags, stream),
+                    "open_batch")
+
+    def hp_mask_batch(self, descs, n, arena, masks, stream=None):
+        self._check(lib().qpp_hp_mask_batch(self.handle, _ptr(descs), n, _ptr(arena), _ptr(masks), stream),
+                    "hp_mask_batch")
+
+    # timing on a stream (HIP events)
+    def event(self):
+        e = vp()
+        self._check(lib().qpp_event_create(self.handle, ctypes.byref(e)), "event")
+        return e.value
+
+    def record(self, ev, stream=None):
+        self._check(lib().qpp_event_record(self.handle, ev, stream), "record")
+
+    def new_stream(self):
+        st = vp()
+        self._check(lib().qpp_stream_create(self.handle, ctypes.byref(st)), "stream")
+        return st.value
+
+    def wait(self, stream, ev):
+        self._check(lib().qpp_stream_wait_event(self.handle, stream, ev), "wait_event")
+
+    def host_alloc(self, nbytes):
+        """pinned host memory as a numpy uint8 array (freed with the context)"""
+        p = vp()
+        self._check(lib().qpp_host_alloc(self.handle, int(nbytes), ctypes.byref(p)), "host_alloc")
+        return np.ctypeslib.as_array((ctypes.c_uint8 * int(nbytes)).from_address(p.value))
+
+    def elapsed_ms(self, e0, e1):
+        ms = ctypes.c_float()
+        self._check(lib().qpp_event_elapsed_ms(self.handle, e0, e1, ctypes.byref(ms)), "elapsed")
+        return ms.value
+
+
+def _ptr(x):
+    if x is None:
+        return None
+    if isinstance(x, DeviceBuffer):
+        return x.ptr
+    return int(x)
+
+
+class Key:
+    """One direction's packet key + header key (TLS_*::new -> (Self, HeaderKey))."""
+
+    def __init__(self, ctx, handle):
+        self.ctx, self.handle = ctx, handle
+
+    def free(self):
+        if self.handle:
+            lib().qpp_key_free(self.handle)
+            self.handle = None
+
+    @property
+    def slot(self):
+        return lib().qpp_key_slot(self.handle)
+
+    @property
+    def suite(self):
+        return lib().qpp_key_suite(self.handle)
+
+    def tag_len(self):
+        return lib().qpp_tag_len(self.handle)
+
+    def sample_len(self):
+        return lib().qpp_sample_len(self.handle)
+
+    def aead_confidentiality_limit(self):
+        return lib().qpp_confidentiality_limit(self.handle)
+
+    def aead_integrity_limit(self):
+        return lib().qpp_integrity_limit(self.handle)
+
+    def material(self):
+        kl = KEY_LEN[self.suite]
+        k, iv, hp = (ctypes.c_uint8 * 32)(), (ctypes.c_uint8 * 12)(), (ctypes.c_uint8 * 32)()
+        lib().qpp_key_material(self.handle, k, iv, hp)
+        return bytes(k[:kl]), bytes(iv), bytes(hp[:kl])
+
+    def derive_next_key(self):
+        h = vp()
+        rc = lib().qpp_key_update(self.handle, ctypes.byref(h))
+        if rc != OK:
+            raise QppError(rc, "qpp_key_update")
+        return Key(self.ctx, h.value)
+
+    def encrypt(self, pn, header, payload):
+        buf = ctypes.create_string_buffer(bytes(payload) + bytes(16), len(payload) + 16)
+        rc = lib().qpp_seal(self.handle, pn, _bytes_ptr(header), len(header), buf, len(payload), len(payload) + 16)
+        if rc != OK:
+            raise QppError(rc, "qpp_seal")
+        return buf.raw
+
+    def encrypt_scatter(self, pn, header, inline, extra):
+        io = ctypes.create_string_buffer(bytes(inline), max(len(inline), 1))
+        out = ctypes.create_string_buffer(len(extra) + 16)
+        rc = lib().qpp_seal_scatter(self.handle, pn, _bytes_ptr(header), len(header), io, len(inline),
+                                    _bytes_ptr(extra), len(extra), out)
+        if rc != OK:
+            raise QppError(rc, "qpp_seal_scatter")
+        return io.raw[:len(inline)], out.raw
+
+    def decrypt(self, pn, header, payload):
+        buf = ctypes.create_string_buffer(bytes(payload), max(len(payload), 1))
+        rc = lib().qpp_open(self.handle, pn, _bytes_ptr(header), len(header), buf, len(payload))
+        if rc == DECRYPT_ERROR:
+            raise DecryptError(rc, "qpp_open")
+        if rc != OK:
+            raise QppError(rc, "qpp_open")
+        return buf.raw[:len(payload) - 16]
+
+    def header_protection_mask(self, sample):
+        out = (ctypes.c_uint8 * 5)()
+        rc = lib().qpp_hp_mask(self.handle, _bytes_ptr(sample), len(sample), out)
+        if rc != OK:
+            raise QppError(rc, "qpp_hp_mask")
+        return bytes(out)
+
+
+# ------------------------------------------------------------------ synthetic batches (bench + tests)
+
+def xoshiro_bytes(seed, n):
+    """Deterministic synthetic payload bytes (numpy PCG64 seeded from `seed`)."""
+    return np.random.Generator(np.random.PCG64(seed)).integers(0, 256, size=n, dtype=np.uint8)
+
+
+def make_batch(n, pt_len, key_slots, seed, aad_len=21, pn_len=4, pn_base=0, stride=None, mixed=True):
+    """Packets back to back in an arena: [AAD aad_len | payload pt_len | tag 16] per `stride` bytes.
+
+    AAD = 1-RTT short header 0x43 || DCID(16) || PN(4).  key_idx = splitmix64(i) % len(key_slots)
+    when mixed, else key_slots[0].  Returns (descs, arena).
+    """
+    stride = stride or ((aad_len + pt_len + 16 + 15) // 16) * 16
+    arena = xoshiro_bytes(seed, n * stride)
+    descs = np.zeros(n, dtype=PKT_DTYPE)
+    idx = np.arange(n, dtype=np.uint64)
+    descs["pn"] = (np.uint64(pn_base) + idx) & np.uint64((1 << 62) - 1)
+    descs["off"] = (idx * np.uint64(stride)).astype(np.uint32)
+    descs["aad_len"] = aad_len
+    descs["pt_len"] = pt_len
+    descs["pn_len"] = pn_len
+    slots = np.asarray(key_slots, dtype=np.uint32)
+    if mixed and len(slots) > 1:
+        z = (idx + np.uint64(0x9E3779B97F4A7C15)) * np.uint64(1)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+        descs["key_idx"] = slots[(z % np.uint64(len(slots))).astype(np.int64)]
+    else:
+        descs["key_idx"] = slots[0]
+    if aad_len >= 1:
+        arena.reshape(n, stride)[:, 0] = 0x43
+    return descs, arena

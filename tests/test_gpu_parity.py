@@ -1,0 +1,329 @@
+"""GPU parity: the HIP path (through the C ABI in libqpp.so) against the oracle and the golden vectors.
+
+Bar: bit-exact ciphertext, tag, header-protection mask and status for every packet (integer work).
+Mirrors the reference's tests (quic/s2n-quic-crypto/src/{initial.rs:142-241, retry.rs:55-64,
+one_rtt.rs:79-114}; quic/s2n-quic-core/src/crypto/tls/testing.rs:612-681 seal_open/protect_unprotect)
+and adds batch cases: ragged lengths, mixed keys and suites, tampered tags, full-size round trips.
+"""
+import numpy as np
+import pytest
+
+import _oracle as orc
+import qpp
+from conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+H = bytes.fromhex
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = qpp.Context(0)
+    yield c
+    c.close()
+
+
+# ------------------------------------------------------------------ RFC 9001 Appendix A through the trait mirror
+
+def test_initial_keys_and_a2_seal(ctx, rfc):
+    sealer, opener = ctx.initial_keys(qpp.ENDPOINT_CLIENT, H(rfc["dcid"]))
+    assert sealer.material() == (H(rfc["client"]["key"]), H(rfc["client"]["iv"]), H(rfc["client"]["hp"]))
+    assert opener.material() == (H(rfc["server"]["key"]), H(rfc["server"]["iv"]), H(rfc["server"]["hp"]))
+    a2 = rfc["a2"]
+    payload = H(a2["payload_prefix"]) + bytes(a2["padded_payload_len"] - len(H(a2["payload_prefix"])))
+    header = H(a2["header"])
+    sealed = sealer.encrypt(a2["pn"], header, payload)
+    prot = H(a2["protected_packet"])
+    assert sealed == prot[len(header):]
+    hdr_len = len(header) - a2["pn_len"]
+    sample = sealed[4 - a2["pn_len"]:20 - a2["pn_len"]]
+    assert sample.hex() == a2["sample"]
+    assert sealer.header_protection_mask(sample).hex() == a2["mask"]
+    # the server opens it (rfc_example_server_test)
+    _, server_opener = ctx.initial_keys(qpp.ENDPOINT_SERVER, H(rfc["dcid"]))
+    assert server_opener.decrypt(a2["pn"], header, sealed) == payload
+    for k in (sealer, opener, server_opener):
+        k.free()
+
+
+def test_a3_server_initial(ctx, rfc):
+    sealer, _ = ctx.initial_keys(qpp.ENDPOINT_SERVER, H(rfc["dcid"]))
+    a3 = rfc["a3"]
+    header = H(a3["header"])
+    sealed = sealer.encrypt(a3["pn"], header, H(a3["payload"]))
+    assert sealed == H(a3["protected_packet"])[len(header):]
+    assert sealer.header_protection_mask(H(a3["sample"])).hex() == a3["mask"]
+
+
+def test_a4_retry_tag(ctx, rfc):
+    a4 = rfc["a4"]
+    k = ctx.raw_key(1, H(a4["key"]), H(a4["nonce"]), bytes(16))  # pn 0: nonce == iv
+    assert k.encrypt(0, H(a4["pseudo_packet"]), b"").hex() == a4["tag"]
+    with pytest.raises(qpp.DecryptError):
+        k.decrypt(0, H(a4["pseudo_packet"]), H("00112233445566778899aabbccddeeff"))
+    assert k.decrypt(0, H(a4["pseudo_packet"]), H(a4["tag"])) == b""
+
+
+def test_a5_chacha_and_key_update(ctx, rfc):
+    a5 = rfc["a5"]
+    k = ctx.key(3, H(a5["secret"]))
+    assert k.material() == (H(a5["key"]), H(a5["iv"]), H(a5["hp"]))
+    sealed = k.encrypt(a5["pn"], H(a5["header"]), H(a5["plaintext"]))
+    assert sealed.hex() == a5["ciphertext"]
+    assert k.header_protection_mask(H(a5["sample"])).hex() == a5["mask"]
+    nxt = k.derive_next_key()
+    ref = ctx.key(3, H(a5["ku_secret"]))
+    assert nxt.material()[:2] == ref.material()[:2]
+    assert nxt.material()[2] == k.material()[2]  # HP key is not updated (RFC 9001 §6)
+    assert nxt.encrypt(0, b"", bytes(32)) == ref.encrypt(0, b"", bytes(32))  # test_key_update
+    bad = ctx.key(3, bytes(32)).derive_next_key()
+    assert bad.encrypt(0, b"", bytes(32)) != ref.encrypt(0, b"", bytes(32))
+
+
+def test_limits_and_lengths(ctx):
+    for suite, conf, integ in ((1, 2**23, 2**52), (2, 2**23, 2**52), (3, 2**62, 2**36)):
+        k = ctx.key(suite, bytes(qpp.HASH_LEN[suite]))
+        assert (k.tag_len(), k.sample_len()) == (16, 16)
+        assert (k.aead_confidentiality_limit(), k.aead_integrity_limit()) == (conf, integ)
+    with pytest.raises(qpp.QppError) as e:
+        ctx.key(9, bytes(32))
+    assert e.value.code == qpp.UNSUPPORTED
+
+
+# ------------------------------------------------------------------ golden fixtures through the per-packet API
+
+@pytest.mark.parametrize("name,suite", [("aead_aes128gcm.json", 1), ("aead_aes256gcm.json", 2),
+                                        ("aead_chacha20poly1305.json", 3)])
+def test_aead_fixtures(ctx, name, suite):
+    for c in load_golden(name)["cases"]:
+        k = ctx.raw_key(suite, H(c["key"]), H(c["iv"]), bytes(qpp.KEY_LEN[suite]))
+        sealed = k.encrypt(c["pn"], H(c["aad"]), H(c["pt"]))
+        assert sealed.hex() == c["ct"] + c["tag"], len(H(c["pt"]))
+        assert k.decrypt(c["pn"], H(c["aad"]), sealed) == H(c["pt"])
+        bad = bytearray(sealed)
+        bad[len(bad) // 2] ^= 0x80
+        with pytest.raises(qpp.DecryptError):
+            k.decrypt(c["pn"], H(c["aad"]), bytes(bad))
+        k.free()
+
+
+def test_short_open_is_decrypt_error(ctx):
+    k = ctx.key(1, bytes(32))
+    with pytest.raises(qpp.DecryptError):
+        k.decrypt(1, b"", bytes(15))
+
+
+def test_hp_fixtures(ctx):
+    for c in load_golden("hp_masks.json")["cases"]:
+        k = ctx.raw_key(c["suite"], bytes(qpp.KEY_LEN[c["suite"]]), bytes(12), H(c["hp"]))
+        assert k.header_protection_mask(H(c["sample"])).hex() == c["mask"]
+        k.free()
+
+
+def test_kdf_chains(ctx):
+    for ch in load_golden("kdf_chains.json")["chains"]:
+        k = ctx.key(ch["suite"], H(ch["secret"]))
+        hp0 = H(ch["steps"][0]["hp"])
+        for step in ch["steps"]:
+            key, iv, hp = k.material()
+            assert (key, iv) == (H(step["key"]), H(step["iv"]))
+            assert hp == hp0  # carried over by every update
+            k = k.derive_next_key()
+
+
+def test_seal_scatter(ctx):
+    # seal_in_place_scatter: inline || extra sealed as one message
+    k = ctx.key(2, bytes(range(48)))
+    inline, extra = bytes(range(100)), bytes(range(37))
+    ct_in, ct_extra_tag = k.encrypt_scatter(77, b"\x41hdr", inline, extra)
+    whole = k.encrypt(77, b"\x41hdr", inline + extra)
+    assert ct_in + ct_extra_tag == whole
+
+
+# ------------------------------------------------------------------ batches vs the oracle
+
+def _keys(ctx, specs, seed):
+    rng = np.random.default_rng(seed)
+    keys, orc_keys = [], []
+    for suite in specs:
+        k = ctx.key(suite, rng.integers(0, 256, qpp.HASH_LEN[suite], dtype=np.uint8).tobytes())
+        keys.append(k)
+        kk, iv, hp = k.material()
+        orc_keys.append((suite, kk, iv, hp))
+    return keys, orc.make_keys(orc_keys)
+
+
+def _ragged_batch(n, slots, seed, max_len=1500):
+    rng = np.random.default_rng(seed)
+    pt = rng.integers(0, max_len + 1, n).astype(np.int64)
+    pt[:8] = [0, 1, 15, 16, 17, 31, 32, 33]
+    aad = rng.choice([0, 1, 5, 6, 16, 21, 22, 45], n).astype(np.int64)
+    pn_len = rng.integers(1, 5, n)
+    aad = np.maximum(aad, pn_len)  # the header holds the PN bytes
+    pt = np.maximum(pt, 4 - pn_len + 0)  # sample must fit (encoding.rs:179-186 pads to ensure it)
+    sizes = aad + pt + 16
+    offs = np.concatenate([[0], np.cumsum(sizes + rng.integers(0, 9, n))[:-1]]).astype(np.int64)
+    arena = rng.integers(0, 256, int(offs[-1] + sizes[-1] + 64), dtype=np.uint8)
+    descs = np.zeros(n, dtype=qpp.PKT_DTYPE)
+    descs["pn"] = rng.integers(0, 2**62, n, dtype=np.uint64)
+    descs["key_idx"] = np.asarray(slots, dtype=np.uint32)[rng.integers(0, len(slots), n)]
+    descs["off"] = offs
+    descs["aad_len"] = aad
+    descs["pt_len"] = pt
+    descs["pn_len"] = pn_len
+    return descs, arena
+
+
+def _run_seal(ctx, descs, arena, flags):
+    n = len(descs)
+    d_desc, d_arena = ctx.alloc(descs.nbytes), ctx.alloc(arena.nbytes)
+    d_mask, d_status = ctx.alloc(5 * n), ctx.alloc(n)
+    d_desc.upload(descs)
+    d_arena.upload(arena)
+    ctx.seal_batch(d_desc, n, d_arena, d_mask, d_status, flags)
+    ctx.sync()
+    out = d_arena.download(), d_mask.download(), d_status.download(dtype=np.int8)
+    for b in (d_desc, d_arena, d_mask, d_status):
+        b.free()
+    return out
+
+
+def _run_open(ctx, descs, arena):
+    n = len(descs)
+    d_desc, d_arena, d_status = ctx.alloc(descs.nbytes), ctx.alloc(arena.nbytes), ctx.alloc(n)
+    d_desc.upload(descs)
+    d_arena.upload(arena)
+    ctx.open_batch(d_desc, n, d_arena, d_status)
+    ctx.sync()
+    out = d_arena.download(), d_status.download(dtype=np.int8)
+    for b in (d_desc, d_arena, d_status):
+        b.free()
+    return out
+
+
+def _oracle_keys_for(keys_orc, descs, slots):
+    """oracle keys are indexed 0..K-1; map device slots to oracle indices"""
+    remap = {s: i for i, s in enumerate(slots)}
+    d = descs.copy()
+    d["key_idx"] = [remap[int(s)] for s in descs["key_idx"]]
+    return d
+
+
+@pytest.mark.parametrize("specs", [[1], [2], [3], [1, 1, 2, 3, 3, 2, 1, 3]], ids=["aes128", "aes256", "chacha", "mixed"])
+def test_batch_seal_open_ragged(ctx, specs):
+    keys, okeys = _keys(ctx, specs, seed=len(specs) * 31 + specs[0])
+    slots = [k.slot for k in keys]
+    descs, arena = _ragged_batch(2048, slots, seed=7 + len(specs))
+    flags = qpp.HP_MASK_OUT | qpp.HP_APPLY
+    got_arena, got_masks, got_status = _run_seal(ctx, descs, arena, flags)
+    want_arena = arena.copy()
+    want_masks = orc.seal_batch(okeys, _oracle_keys_for(okeys, descs, slots), want_arena, flags)
+    assert (got_status == 0).all()
+    assert got_masks.tobytes() == want_masks
+    bad = np.nonzero(got_arena != want_arena)[0]
+    assert bad.size == 0, f"first mismatch at arena byte {bad[:8]}"
+
+    # open needs the unprotected header: seal again without HP to get the AAD the receiver uses
+    sealed_arena, _, _ = _run_seal(ctx, descs, arena, 0)
+    tampered = np.zeros(len(descs), bool)
+    tampered[::97] = True
+    ct = sealed_arena.copy()
+    for i in np.nonzero(tampered)[0]:
+        d = descs[i]
+        ct[int(d["off"]) + int(d["aad_len"]) + int(d["pt_len"]) + (i % 16)] ^= 1 << (i % 8)
+    got_pt, st = _run_open(ctx, descs, ct)
+    want_pt = ct.copy()
+    want_st = orc.open_batch(okeys, _oracle_keys_for(okeys, descs, slots), want_pt)
+    assert list(st) == want_st
+    assert (st[tampered] == qpp.DECRYPT_ERROR).all() and (st[~tampered] == 0).all()
+    assert (got_pt == want_pt).all()
+    # round trip: untampered payloads are the original plaintext again
+    for i in np.nonzero(~tampered)[0][:200]:
+        d = descs[i]
+        a, b = int(d["off"]) + int(d["aad_len"]), int(d["off"]) + int(d["aad_len"]) + int(d["pt_len"])
+        assert (got_pt[a:b] == arena[a:b]).all()
+    for k in keys:
+        k.free()
+
+
+def test_jumbo_and_edges(ctx):
+    keys, okeys = _keys(ctx, [1, 2, 3], seed=99)
+    slots = [k.slot for k in keys]
+    lens = [0, 1, 4, 8000, 8000, 1452, 300, 65535 - 100]
+    n = len(lens) * 3
+    descs = np.zeros(n, dtype=qpp.PKT_DTYPE)
+    off = 0
+    for i in range(n):
+        L = lens[i % len(lens)]
+        descs[i] = (2**32 + 7 * i if i % 2 else i, slots[i // len(lens)], off, 21, L, 4, 0, 0)
+        off += 21 + L + 16 + 3
+    arena = np.random.default_rng(5).integers(0, 256, off + 64, dtype=np.uint8)
+    got, _, st = _run_seal(ctx, descs, arena, 0)
+    want = arena.copy()
+    orc.seal_batch(okeys, _oracle_keys_for(okeys, descs, slots), want, 0)
+    assert (st == 0).all() and (got == want).all()
+
+
+def test_hp_mask_batch_receive_side(ctx):
+    keys, okeys = _keys(ctx, [1, 3, 2], seed=3)
+    slots = [k.slot for k in keys]
+    descs, arena = _ragged_batch(512, slots, seed=11)
+    descs["pt_len"] = np.maximum(descs["pt_len"], 20)
+    descs["aad_len"] = np.maximum(descs["aad_len"], 4)
+    descs["off"] = np.arange(512) * 1600
+    arena = np.random.default_rng(2).integers(0, 256, 512 * 1600, dtype=np.uint8)
+    recv = descs.copy()
+    recv["pn_len"] = 0  # receive side: sample at header_len + 4
+    d_desc, d_arena, d_mask = ctx.alloc(recv.nbytes), ctx.alloc(arena.nbytes), ctx.alloc(5 * 512)
+    d_desc.upload(recv)
+    d_arena.upload(arena)
+    ctx.hp_mask_batch(d_desc, 512, d_arena, d_mask)
+    got = d_mask.download().tobytes()
+    for i in range(512):
+        d = recv[i]
+        k = okeys[slots.index(int(d["key_idx"]))]
+        s = int(d["off"]) + int(d["aad_len"]) + 4
+        want = orc.hp_mask(k.suite, bytes(k.hp)[:qpp.KEY_LEN[k.suite]], arena[s:s + 16].tobytes())
+        assert got[5 * i:5 * i + 5] == want
+
+
+@pytest.mark.parametrize("suite", [1, 2, 3])
+def test_full_size_round_trip(ctx, suite):
+    """BASELINE configs 2/3 size (1 Mi x 1200 B): seal -> open round trip restores every payload, every
+    status is OK, and a seeded sample of packets is bit-exact against the oracle."""
+    n, pt_len = 1 << 20, 1200
+    keys, okeys = _keys(ctx, [suite] * (1 if suite == 1 else 64), seed=suite)
+    slots = [k.slot for k in keys]
+    descs, arena = qpp.make_batch(n, pt_len, slots, seed=0x5eed0002, pn_base=(2**32 if suite == 2 else 0))
+    d_desc, d_arena, d_mask, d_status = ctx.alloc(descs.nbytes), ctx.alloc(arena.nbytes), ctx.alloc(5 * n), ctx.alloc(n)
+    d_desc.upload(descs)
+    d_arena.upload(arena)
+    ctx.seal_batch(d_desc, n, d_arena, d_mask, d_status, qpp.HP_MASK_OUT)
+    sealed = d_arena.download()
+    masks = d_mask.download()
+    stride = arena.size // n
+    rng = np.random.default_rng(suite)
+    pick = np.sort(rng.choice(n, 1500, replace=False))
+    sub_descs = descs[pick].copy()
+    sub_arena = np.concatenate([arena[i * stride:(i + 1) * stride] for i in pick])
+    sub_descs["off"] = np.arange(len(pick)) * stride
+    sub_want = sub_arena.copy()
+    want_masks = orc.seal_batch(okeys, _oracle_keys_for(okeys, sub_descs, slots), sub_want, qpp.HP_MASK_OUT)
+    sub_got = np.concatenate([sealed[i * stride:(i + 1) * stride] for i in pick])
+    assert (sub_got == sub_want).all()
+    assert np.concatenate([masks[5 * i:5 * i + 5] for i in pick]).tobytes() == want_masks
+    ctx.open_batch(d_desc, n, d_arena, d_status)
+    st = d_status.download(dtype=np.int8)
+    opened = d_arena.download()
+    assert (st == 0).all()
+    v = opened.reshape(n, stride)
+    a = arena.reshape(n, stride)
+    assert (v[:, 21:21 + pt_len] == a[:, 21:21 + pt_len]).all()
+    # a checksum of checksums over the ciphertext: identical across two runs (determinism)
+    d_arena.upload(arena)
+    ctx.seal_batch(d_desc, n, d_arena, d_mask, d_status, qpp.HP_MASK_OUT)
+    assert (d_arena.download() == sealed).all()
+    for b in (d_desc, d_arena, d_mask, d_status):
+        b.free()
+    for k in keys:
+        k.free()

@@ -21,6 +21,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "s2n-quic_amd"))
 import numpy as np  # noqa: E402
 
+import multigpu  # noqa: E402
 import qpp  # noqa: E402
 
 qpp.lib()  # load the engine (and its HIP runtime) before anything else touches the GPU
@@ -78,38 +79,21 @@ def main():
     ap.add_argument("--mode", default="device", choices=["device", "e2e"])
     ap.add_argument("--cpu-seconds", type=float, default=1.5)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-hp", action="store_true", help="seal without the HP mask (diagnostic)")
     args = ap.parse_args()
 
-    rank = int(os.environ.get("RANK", 0))
-    world = int(os.environ.get("WORLD_SIZE", 1))
-    local_rank = int(os.environ.get("LOCAL_RANK", 0))
-    dist = None
-    if world > 1:
-        import torch
-        import torch.distributed as dist_mod
-
-        dist = dist_mod
-        dist.init_process_group("gloo")  # CPU only: barrier + max over ranks; the data path has no collective
-
-    def barrier():
-        if dist:
-            dist.barrier()
-
-    def max_over_ranks(x):
-        if not dist:
-            return x
-        t = torch.tensor([x], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item())
+    rank, world, local_rank = multigpu.env_rank()
+    ctl = multigpu.Control(world)  # gloo on CPU tensors: barrier + max over ranks only
+    barrier, max_over_ranks = ctl.barrier, ctl.max
 
     suite = SUITES[args.suite]
     ctx = qpp.Context(local_rank)
     rng = np.random.default_rng(0x5eed0000 + 1)
     keys = [ctx.key(suite, rng.integers(0, 256, qpp.HASH_LEN[suite], dtype=np.uint8).tobytes()) for _ in range(args.keys)]
     n, pt, aad = args.packets, args.pt, args.aad
-    descs, arena = qpp.make_batch(n, pt, [k.slot for k in keys], seed=0x5eed0000 + 1 + 7919 * rank, aad_len=aad,
-                                  pn_base=rank * n)
-    flags = qpp.HP_MASK_OUT | (qpp.ONLY_CHACHA if suite == 3 else qpp.ONLY_AES)
+    sh = multigpu.shard(rank, world, n, seed_base=0x5eed0000 + 1)
+    descs, arena = qpp.make_batch(n, pt, [k.slot for k in keys], seed=sh["seed"], aad_len=aad, pn_base=sh["pn_base"])
+    flags = (0 if args.no_hp else qpp.HP_MASK_OUT) | (qpp.ONLY_CHACHA if suite == 3 else qpp.ONLY_AES)
     d_desc, d_mask, d_status = ctx.alloc(descs.nbytes), ctx.alloc(5 * n), ctx.alloc(n)
     d_desc.upload(descs)
     s = ctx.stream

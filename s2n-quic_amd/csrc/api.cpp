@@ -103,7 +103,7 @@ int ensure_plan(qpp_ctx *ctx, uint32_t n) {
     HIP_TRY(ctx, hipMalloc(&p.cursor, sizeof(uint32_t) * kcap));
     HIP_TRY(ctx, hipMalloc(&p.istart, sizeof(uint32_t) * (kcap + 1)));
     HIP_TRY(ctx, hipMalloc(&p.perm, sizeof(uint32_t) * std::max<uint32_t>(ncap, 1)));
-    HIP_TRY(ctx, hipMalloc(&p.work, sizeof(WorkItem) * (plan_max_work(ncap, kcap) + 1)));
+    HIP_TRY(ctx, hipMalloc(&p.work, sizeof(WorkItem) * (plan_max_work(ncap, kcap, kMinPacketsPerItem) + 1)));
     HIP_TRY(ctx, hipMalloc(&p.n_work, sizeof(uint32_t)));
     ctx->plan_n_cap = ncap;
     ctx->plan_key_cap = kcap;
@@ -197,7 +197,7 @@ int run_one(const qpp_key *k, bool seal, uint64_t pn, const uint8_t *header, siz
         HIP_TRY(ctx, hipMemcpyAsync(ctx->plan1.perm, &zero, 4, hipMemcpyHostToDevice, s));
         HIP_TRY(ctx, hipMemcpyAsync(ctx->plan1.work, &w, sizeof w, hipMemcpyHostToDevice, s));
         HIP_TRY(ctx, hipMemcpyAsync(ctx->plan1.n_work, &one, 4, hipMemcpyHostToDevice, s));
-        // grid = plan_max_work(1, key_cap); only work item 0 exists
+        // key_cap = 0: grid = plan_max_work(1, 0, per) = 1; only work item 0 exists
         HIP_TRY(ctx, launch_aes_gcm(seal, ctx->d_keys, ctx->d_desc1, ctx->plan1, 1, 0, ctx->d_stage, ctx->d_mask1,
                                     ctx->d_status1, 0, s));
     } else {
@@ -461,7 +461,7 @@ int qpp_seal_batch(qpp_ctx *ctx, const qpp_pkt *descs, size_t n, uint8_t *arena,
     if (!(flags & QPP_ONLY_CHACHA)) {
         rc = ensure_plan(ctx, (uint32_t)n);
         if (rc) return rc;
-        HIP_TRY(ctx, launch_plan(ctx->d_keys, ctx->key_cap, descs, (uint32_t)n, ctx->plan, s));
+        HIP_TRY(ctx, launch_plan(ctx->d_keys, ctx->key_cap, descs, (uint32_t)n, ctx->plan, aes_packets_per_item(), s));
         HIP_TRY(ctx, launch_aes_gcm(true, ctx->d_keys, descs, ctx->plan, (uint32_t)n, ctx->key_cap, arena, masks, status,
                                     flags, s));
     }
@@ -482,7 +482,7 @@ int qpp_open_batch(qpp_ctx *ctx, const qpp_pkt *descs, size_t n, uint8_t *arena,
     if (!(flags & QPP_ONLY_CHACHA)) {
         rc = ensure_plan(ctx, (uint32_t)n);
         if (rc) return rc;
-        HIP_TRY(ctx, launch_plan(ctx->d_keys, ctx->key_cap, descs, (uint32_t)n, ctx->plan, s));
+        HIP_TRY(ctx, launch_plan(ctx->d_keys, ctx->key_cap, descs, (uint32_t)n, ctx->plan, aes_packets_per_item(), s));
         HIP_TRY(ctx, launch_aes_gcm(false, ctx->d_keys, descs, ctx->plan, (uint32_t)n, ctx->key_cap, arena, nullptr,
                                     status, 0, s));
     }

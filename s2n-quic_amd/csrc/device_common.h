@@ -51,15 +51,24 @@ __device__ __forceinline__ void st_bytes(uint8_t *p, uint4 v, uint32_t r) {
         if (i < r) p[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
 }
 
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // gfx950 v_bitop3_b32: one op for a ^ b ^ c
+}
+__device__ __forceinline__ uint4 xor3(uint4 a, uint4 b, uint4 c) {
+    return make_uint4(xor3(a.x, b.x, c.x), xor3(a.y, b.y, c.y), xor3(a.z, b.z, c.z), xor3(a.w, b.w, c.w));
+}
+
 // ---------------------------------------------------------------- AES with bank-replicated LDS T-tables
+// Column c of a round: T0[s_c.b0] ^ T1[s_c+1.b1] ^ T2[s_c+2.b2] ^ T3[s_c+3.b3] ^ rk, with T2 = rotl16(T0) and
+// T3 = rotl16(T1), so only T0/T1 are stored (64 KiB replicated); per column: 4 lookups + 4 VALU.
 struct AesLds {
     const uint8_t *lds;
     uint32_t laneword;  // byte0 = 4 * (lane % 32), byte2 = 0x01 (64 KiB table base)
 
-    // T0[byte k of w] / T1[byte k of w]
+    // address of T0[byte K of w] (T1 is at +128): ONE v_perm_b32
     template <int K>
     __device__ __forceinline__ uint32_t addr(uint32_t w) const {
-        // v_perm_b32: byte0 <- laneword.b0, byte1 <- w.bK, byte2 <- laneword.b2, byte3 <- 0
+        // byte0 <- laneword.b0, byte1 <- w.bK, byte2 <- laneword.b2, byte3 <- 0
         return __builtin_amdgcn_perm(w, laneword, (0x0cu << 24) | (2u << 16) | ((4u + K) << 8) | 0u);
     }
     template <int K>
@@ -68,31 +77,93 @@ struct AesLds {
     __device__ __forceinline__ uint32_t t1(uint32_t w) const { return *(const uint32_t *)(lds + addr<K>(w) + 128); }
 
     __device__ __forceinline__ uint32_t col(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t k) const {
-        return t0<0>(a) ^ t1<1>(b) ^ rotl16(t0<2>(c) ^ t1<3>(d)) ^ k;
+        return xor3(t0<0>(a), t1<1>(b), k) ^ rotl16(t0<2>(c) ^ t1<3>(d));
     }
     __device__ __forceinline__ uint32_t last(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t k) const {
-        // S[x] = byte1 of T0[x]; = byte2 and byte3 of T1[x]
+        // S[x] = byte1 of T0[x] = byte2/byte3 of T1[x]; lo|hi are disjoint so one xor3 finishes the column
         uint32_t lo = __builtin_amdgcn_perm(t1<1>(b), t0<0>(a), 0x0c0c0601u);
         uint32_t hi = __builtin_amdgcn_perm(t1<3>(d), t0<2>(c), 0x07020c0cu);
-        return (lo | hi) ^ k;
+        return xor3(lo, hi, k);
+    }
+    __device__ __forceinline__ void round(uint32_t (&s)[4], const uint32_t *__restrict__ rk) const {
+        uint32_t u0 = col(s[0], s[1], s[2], s[3], rk[0]);
+        uint32_t u1 = col(s[1], s[2], s[3], s[0], rk[1]);
+        uint32_t u2 = col(s[2], s[3], s[0], s[1], rk[2]);
+        uint32_t u3 = col(s[3], s[0], s[1], s[2], rk[3]);
+        s[0] = u0; s[1] = u1; s[2] = u2; s[3] = u3;
+    }
+    __device__ __forceinline__ uint4 final(const uint32_t (&s)[4], const uint32_t *__restrict__ rk) const {
+        return make_uint4(last(s[0], s[1], s[2], s[3], rk[0]), last(s[1], s[2], s[3], s[0], rk[1]),
+                          last(s[2], s[3], s[0], s[1], rk[2]), last(s[3], s[0], s[1], s[2], rk[3]));
     }
 
+    // Full AES of one block (no caching): HP mask, key setup, page-crossing groups.
     template <int NR>
     __device__ __forceinline__ uint4 encrypt(uint4 in, const uint32_t *__restrict__ rk) const {
-        uint32_t s0 = in.x ^ rk[0], s1 = in.y ^ rk[1], s2 = in.z ^ rk[2], s3 = in.w ^ rk[3];
+        uint32_t s[4] = {in.x ^ rk[0], in.y ^ rk[1], in.z ^ rk[2], in.w ^ rk[3]};
 #pragma unroll
-        for (int r = 1; r < NR; r++) {
-            uint32_t u0 = col(s0, s1, s2, s3, rk[4 * r + 0]);
-            uint32_t u1 = col(s1, s2, s3, s0, rk[4 * r + 1]);
-            uint32_t u2 = col(s2, s3, s0, s1, rk[4 * r + 2]);
-            uint32_t u3 = col(s3, s0, s1, s2, rk[4 * r + 3]);
-            s0 = u0; s1 = u1; s2 = u2; s3 = u3;
-        }
-        return make_uint4(last(s0, s1, s2, s3, rk[4 * NR + 0]), last(s1, s2, s3, s0, rk[4 * NR + 1]),
-                          last(s2, s3, s0, s1, rk[4 * NR + 2]), last(s3, s0, s1, s2, rk[4 * NR + 3]));
+        for (int r = 1; r < NR; r++) round(s, rk + 4 * r);
+        return final(s, rk + 4 * NR);
     }
 };
 
+// Counter-mode round caching.  For CTR blocks nonce || be32(c) only the last byte of the block changes while
+// c stays inside one 256-block page, so after round 1 only column 0 varies (one lookup) and round 2 needs
+// four lookups (one per output column).  `Page` holds the per-packet, per-page constants.
+struct CtrPage {
+    uint32_t k0, k1, k2, k3;  // round-1 output (k0 without the varying T3 term)
+    uint32_t l0, l1, l2, l3;  // round-2 output without the varying terms
+    uint32_t x3;              // rk[3] byte 3 (xored with the counter's low byte)
+    uint32_t page;            // c >> 8 these constants belong to
+
+    __device__ __forceinline__ void build(const AesLds &a, const uint32_t *__restrict__ rk, uint32_t n0, uint32_t n1,
+                                          uint32_t n2, uint32_t pg) {
+        const uint32_t s0 = n0 ^ rk[0], s1 = n1 ^ rk[1], s2 = n2 ^ rk[2], s3 = bswap32(pg << 8) ^ rk[3];
+        k0 = xor3(a.t0<0>(s0), a.t1<1>(s1), rk[4]) ^ rotl16(a.t0<2>(s2));
+        k1 = a.col(s1, s2, s3, s0, rk[5]);
+        k2 = a.col(s2, s3, s0, s1, rk[6]);
+        k3 = a.col(s3, s0, s1, s2, rk[7]);
+        l0 = xor3(a.t1<1>(k1), rk[8], rotl16(a.t0<2>(k2) ^ a.t1<3>(k3)));
+        l1 = xor3(a.t0<0>(k1), a.t1<1>(k2), rk[9]) ^ rotl16(a.t0<2>(k3));
+        l2 = xor3(a.t0<0>(k2), a.t1<1>(k3), rk[10]) ^ rotl16(a.t1<3>(k1));
+        l3 = xor3(a.t0<0>(k3), rk[11], rotl16(a.t0<2>(k1) ^ a.t1<3>(k2)));
+        x3 = rk[3] >> 24;
+        page = pg;
+    }
+    // state after rounds 1 and 2 for counter c (same page)
+    __device__ __forceinline__ void two_rounds(const AesLds &a, uint32_t c, uint32_t (&v)[4]) const {
+        const uint32_t x = (c & 0xffu) ^ x3;
+        const uint32_t u0 = k0 ^ rotl16(a.t1<0>(x));  // T3[x]
+        v[0] = l0 ^ a.t0<0>(u0);
+        v[1] = l1 ^ rotl16(a.t1<3>(u0));              // T3[u0.b3]
+        v[2] = l2 ^ rotl16(a.t0<2>(u0));              // T2[u0.b2]
+        v[3] = l3 ^ a.t1<1>(u0);                      // T1[u0.b1]
+    }
+};
+
+// NB counter blocks c, c+1, ... (all inside page.page) -> NB keystream blocks, lookups of all NB blocks
+// interleaved round by round for ILP.
+template <int NR, int NB>
+__device__ __forceinline__ void ctr_keystream(const AesLds &a, const CtrPage &pg, const uint32_t *__restrict__ rk,
+                                              uint32_t c, uint4 (&ks)[NB]) {
+    uint32_t s[NB][4];
+#pragma unroll
+    for (int j = 0; j < NB; j++) pg.two_rounds(a, c + j, s[j]);
+#pragma unroll
+    for (int r = 3; r < NR; r++)
+#pragma unroll
+        for (int j = 0; j < NB; j++) a.round(s[j], rk + 4 * r);
+#pragma unroll
+    for (int j = 0; j < NB; j++) ks[j] = a.final(s[j], rk + 4 * NR);
+}
+
+// Same without caching (group straddles a page boundary; rare).
+template <int NR, int NB>
+__device__ __forceinline__ void ctr_keystream_full(const AesLds &a, const uint32_t *__restrict__ rk, uint32_t n0,
+                                                   uint32_t n1, uint32_t n2, uint32_t c, uint4 (&ks)[NB]) {
+#pragma unroll
+    for (int j = 0; j < NB; j++) ks[j] = a.encrypt<NR>(make_uint4(n0, n1, n2, bswap32(c + j)), rk);
+}
 
 // AES T0/T1 bank-replicated tables for the AesLds view: dword d -> row x = d >> 6, slot = d & 63
 // (slots 32..63 hold T1 = rotl8 T0).  No barrier inside.

@@ -2,7 +2,7 @@
 // (its GHASH tables are per key and live in LDS).  Three small launches, all device-side, so a batch
 // whose descriptors are already in HBM never round-trips to the host:
 //   1. plan_hist   : packets per key (LDS-privatised counts, one global add per touched key per block)
-//   2. plan_scan   : one workgroup: key offsets, work list {key, begin, count<=1024, rounds}, n_work
+//   2. plan_scan   : one workgroup: key offsets, work list {key, begin, count<=per, rounds}, n_work
 //   3. plan_scatter: perm[] = packet indices grouped by key (LDS ranks + one global reservation per key)
 // ChaCha20-Poly1305 packets are skipped (their kernel needs no grouping).
 // The reference has no batching at all (Key::encrypt is per packet); this is the
@@ -47,7 +47,7 @@ __global__ __launch_bounds__(kPlanBlock) void plan_hist(const DevKey *__restrict
 __global__ __launch_bounds__(kPlanBlock) void plan_scan(const DevKey *__restrict__ keys, uint32_t key_cap,
                                                        const uint32_t *__restrict__ counts, uint32_t *__restrict__ cursor,
                                                        uint32_t *__restrict__ istart_g, WorkItem *__restrict__ work,
-                                                       uint32_t *__restrict__ n_work) {
+                                                       uint32_t *__restrict__ n_work, uint32_t per) {
     __shared__ uint32_t sc[kPlanBlock], si[kPlanBlock];
     __shared__ uint32_t istart_l[kMaxPlanKeys + 1];
     __shared__ uint32_t carry_c, carry_i;
@@ -58,7 +58,7 @@ __global__ __launch_bounds__(kPlanBlock) void plan_scan(const DevKey *__restrict
     for (uint32_t base = 0; base < key_cap; base += kPlanBlock) {
         const uint32_t k = base + threadIdx.x;
         const uint32_t c = k < key_cap ? counts[k] : 0;
-        const uint32_t items = (c + kPacketsPerGroup - 1) / kPacketsPerGroup;
+        const uint32_t items = (c + per - 1) / per;
         sc[threadIdx.x] = c;
         si[threadIdx.x] = items;
         __syncthreads();
@@ -88,10 +88,9 @@ __global__ __launch_bounds__(kPlanBlock) void plan_scan(const DevKey *__restrict
             if (istart[mid] <= w) lo = mid; else hi = mid;
         }
         const uint32_t i = w - istart[lo];
-        const uint32_t left = counts[lo] - i * kPacketsPerGroup;
+        const uint32_t left = counts[lo] - i * per;
         // cursor[] still holds the key's first perm index: plan_scatter runs after this kernel
-        work[w] = WorkItem{lo, cursor[lo] + i * kPacketsPerGroup,
-                           left < (uint32_t)kPacketsPerGroup ? left : (uint32_t)kPacketsPerGroup, keys[lo].nr};
+        work[w] = WorkItem{lo, cursor[lo] + i * per, left < per ? left : per, keys[lo].nr};
     }
 }
 
@@ -123,20 +122,20 @@ __global__ __launch_bounds__(kPlanBlock) void plan_scatter(const DevKey *__restr
 
 }  // namespace
 
-uint32_t plan_max_work(uint32_t n, uint32_t key_cap) {
-    const uint32_t by_packets = (n + kPacketsPerGroup - 1) / kPacketsPerGroup;
+uint32_t plan_max_work(uint32_t n, uint32_t key_cap, uint32_t per) {
+    const uint32_t by_packets = (n + per - 1) / per;
     const uint32_t by_keys = key_cap < n ? key_cap : n;
     return by_packets + by_keys;
 }
 
 hipError_t launch_plan(const DevKey *keys, uint32_t key_cap, const qpp_pkt *descs, uint32_t n, PlanBuffers pb,
-                       hipStream_t s) {
+                       uint32_t per, hipStream_t s) {
     hipError_t e = hipMemsetAsync(pb.counts, 0, sizeof(uint32_t) * key_cap, s);
     if (e != hipSuccess) return e;
     const dim3 grid((n + kPlanBlock - 1) / kPlanBlock);
     hipLaunchKernelGGL(plan_hist, grid, dim3(kPlanBlock), 0, s, keys, key_cap, descs, n, pb.counts);
     hipLaunchKernelGGL(plan_scan, dim3(1), dim3(kPlanBlock), 0, s, keys, key_cap, pb.counts, pb.cursor, pb.istart, pb.work,
-                       pb.n_work);
+                       pb.n_work, per);
     hipLaunchKernelGGL(plan_scatter, grid, dim3(kPlanBlock), 0, s, keys, key_cap, descs, n, pb.cursor, pb.perm);
     return hipGetLastError();
 }

@@ -65,11 +65,12 @@ static_assert(sizeof(DevKey) == 2576, "DevKey layout");
 struct WorkItem {
     uint32_t key;    // key slot
     uint32_t begin;  // first index into perm[]
-    uint32_t count;  // packets (<= kPacketsPerGroup)
+    uint32_t count;  // packets (<= the variant's packets per item)
     uint32_t nr;     // AES rounds for this key
 };
 
-constexpr int kPacketsPerGroup = 1024;  // one packet per lane, 16 waves per workgroup
+constexpr int kMinPacketsPerItem = 256;  // smallest AES work item (sizes plan scratch)
+constexpr int kDefaultAesVariant = 0;  // see aes_gcm.hip launch_variant
 constexpr int kMaxPlanKeys = 8192;      // keys binned in LDS by the plan kernels (larger tables: global bins)
 
 // ---------------------------------------------------------------- launchers (aes_gcm.hip, chacha.hip, plan.hip)
@@ -78,14 +79,15 @@ struct PlanBuffers {
     uint32_t *cursor;   // [key_cap] scatter cursors
     uint32_t *istart;   // [key_cap + 1] first work item per key (used when key_cap > kMaxPlanKeys)
     uint32_t *perm;     // [n_cap] packet indices grouped by key
-    WorkItem *work;     // [n_cap / kPacketsPerGroup + key_cap + 1]
+    WorkItem *work;     // [n_cap / kMinPacketsPerItem + key_cap + 1]
     uint32_t *n_work;   // [1]
 };
 
 hipError_t launch_key_setup(DevKey *keys, uint32_t first, uint32_t count, hipStream_t s);
 hipError_t launch_plan(const DevKey *keys, uint32_t key_cap, const qpp_pkt *descs, uint32_t n, PlanBuffers pb,
-                       hipStream_t s);
-uint32_t plan_max_work(uint32_t n, uint32_t key_cap);
+                       uint32_t per, hipStream_t s);
+uint32_t plan_max_work(uint32_t n, uint32_t key_cap, uint32_t per);
+uint32_t aes_packets_per_item();  // work-item size of the selected AES-GCM kernel variant
 hipError_t launch_aes_gcm(bool seal, const DevKey *keys, const qpp_pkt *descs, const PlanBuffers &pb, uint32_t n,
                           uint32_t key_cap, uint8_t *arena, uint8_t *masks, int8_t *status, uint32_t flags,
                           hipStream_t s);

@@ -16,7 +16,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libqpp.so")
+LIB_PATH = os.environ.get("QPP_LIB") or os.path.join(HERE, "libqpp.so")  # QPP_LIB: A/B builds
 
 SUITE_AES_128_GCM = 1
 SUITE_AES_256_GCM = 2

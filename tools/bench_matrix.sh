@@ -1,0 +1,16 @@
+#!/bin/bash
+# BASELINE.json configs on one GPU: each line is one bench.py JSON line (device-resident unless --mode e2e).
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+tag=${1:-matrix}; out=gpurun_out/$tag; mkdir -p $out
+run() { name=$1; shift; timeout -k 10 240 python bench.py --steps 5 --warmup 2 --no-cpu "$@" > $out/$name.json 2> $out/$name.err || { echo "FAIL $name"; tail -5 $out/$name.err; return 1; }; python -c "import json;d=json.load(open('$out/$name.json'));print('$name', d['value'], d.get('unit'), d.get('ms_per_step'), d.get('roofline',{}).get('frac'))"; }
+run c2_aes128_1key && \
+run c3_aes256_64keys --suite aes256gcm --keys 64 && \
+run c3_chacha_64keys --suite chacha20poly1305 --keys 64 && \
+run c4_aes128_pt300 --pt 300 --packets 4194304 && \
+run c4_aes128_pt1452 --pt 1452 && \
+run c4_aes128_pt8000 --pt 8000 --packets 131072 && \
+run c5_aes128_4ki_keys --keys 4096 --packets 2097152 && \
+run e2e_aes128 --mode e2e --steps 3 && \
+run e2e_c5_4ki_keys --mode e2e --keys 4096 --packets 2097152 --steps 3

@@ -80,6 +80,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=1.5)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-hp", action="store_true", help="seal without the HP mask (diagnostic)")
+    ap.add_argument("--no-check", action="store_true", help="skip the warmup open-status check (diagnostic builds)")
     args = ap.parse_args()
 
     rank, world, local_rank = multigpu.env_rank()
@@ -119,7 +120,7 @@ def main():
         step()
     ctx.sync(s)
     st = d_status.download(dtype=np.int8)
-    if not (st == 0).all():
+    if not args.no_check and not (st == 0).all():
         raise SystemExit(f"rank {rank}: {int((st != 0).sum())} packets failed to open during warmup")
 
     evs = [(ctx.event(), ctx.event(), ctx.event()) for _ in range(args.steps)]

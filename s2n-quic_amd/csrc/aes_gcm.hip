@@ -48,128 +48,6 @@ struct GhashLds {
     }
 };
 
-// ---------------------------------------------------------------- phased group: AES-CTR x NB + GHASH, LDS-batched
-// hipcc left to itself keeps only 2-4 LDS reads in flight per wave (it trades latency for registers), so the
-// group is written as explicit phases: every lookup of one AES round for all NB blocks, plus the 16 lookups of
-// one GHASH step, is issued before a scheduling barrier, and the xors follow it.  One phase per AES round; the
-// NB GHASH steps of the previous group ride in the first NB phases.
-__device__ __forceinline__ void gh_load(const GhashLds &gh, uint4 z, uint4 (&m)[16]) {
-    m[0] = gh.tj<0>(z.x);   m[1] = gh.tj<1>(z.x);   m[2] = gh.tj<2>(z.x);   m[3] = gh.tj<3>(z.x);
-    m[4] = gh.tj<4>(z.y);   m[5] = gh.tj<5>(z.y);   m[6] = gh.tj<6>(z.y);   m[7] = gh.tj<7>(z.y);
-    m[8] = gh.tj<8>(z.z);   m[9] = gh.tj<9>(z.z);   m[10] = gh.tj<10>(z.z); m[11] = gh.tj<11>(z.z);
-    m[12] = gh.tj<12>(z.w); m[13] = gh.tj<13>(z.w); m[14] = gh.tj<14>(z.w); m[15] = gh.tj<15>(z.w);
-}
-__device__ __forceinline__ uint4 gh_reduce(const uint4 (&m)[16], uint4 c) {
-    const uint4 a = xor3(m[0], m[1], m[2]), b = xor3(m[3], m[4], m[5]), d = xor3(m[6], m[7], m[8]);
-    const uint4 e = xor3(m[9], m[10], m[11]), f = xor3(m[12], m[13], m[14]);
-    return xor3(xor3(a, b, d), xor3(e, f, m[15]), c);
-}
-__device__ __forceinline__ void round_load(const AesLds &a, const uint32_t (&s)[4], uint32_t (&t)[16]) {
-#pragma unroll
-    for (int c = 0; c < 4; c++) {
-        t[4 * c + 0] = a.t0<0>(s[c]);
-        t[4 * c + 1] = a.t1<1>(s[(c + 1) & 3]);
-        t[4 * c + 2] = a.t0<2>(s[(c + 2) & 3]);
-        t[4 * c + 3] = a.t1<3>(s[(c + 3) & 3]);
-    }
-}
-__device__ __forceinline__ void round_mix(const uint32_t (&t)[16], const uint32_t *__restrict__ rk, uint32_t (&s)[4]) {
-#pragma unroll
-    for (int c = 0; c < 4; c++) s[c] = xor3(t[4 * c], t[4 * c + 1], rk[c]) ^ rotl16(t[4 * c + 2] ^ t[4 * c + 3]);
-}
-__device__ __forceinline__ uint4 round_final(const uint32_t (&t)[16], const uint32_t *__restrict__ rk) {
-    uint32_t o[4];
-#pragma unroll
-    for (int c = 0; c < 4; c++) {
-        const uint32_t lo = __builtin_amdgcn_perm(t[4 * c + 1], t[4 * c], 0x0c0c0601u);
-        const uint32_t hi = __builtin_amdgcn_perm(t[4 * c + 3], t[4 * c + 2], 0x07020c0cu);
-        o[c] = xor3(lo, hi, rk[c]);
-    }
-    return make_uint4(o[0], o[1], o[2], o[3]);
-}
-#define QPP_PHASE_BARRIER() __builtin_amdgcn_sched_barrier(0)
-
-// Keystream of NB counter blocks c..c+NB-1 into ks[]; if GH, also absorbs cb[0..NB-1] into the GHASH chain z.
-template <int NR, int NB, bool CACHED, bool GH>
-__device__ __forceinline__ void group_phased(const AesLds &a, const GhashLds &gh, const CtrPage &pg,
-                                             const uint32_t *__restrict__ rk, uint32_t n0, uint32_t n1, uint32_t n2,
-                                             uint32_t c, uint4 (&ks)[NB], uint4 &z, const uint4 (&cb)[NB]) {
-    uint32_t s[NB][4];
-    uint32_t t[NB][16];
-    uint4 gm[16];
-    int phase = 0;  // GHASH step done in this phase (compile-time after unrolling)
-    if constexpr (CACHED) {
-        // phase 1: the one varying lookup of round 1 (T3[x], x = counter byte ^ rk)
-        uint32_t tv[NB];
-#pragma unroll
-        for (int j = 0; j < NB; j++) tv[j] = a.t1<0>(((c + j) & 0xffu) ^ pg.x3);
-        if (GH) gh_load(gh, z, gm);
-        QPP_PHASE_BARRIER();
-        uint32_t u0[NB];
-#pragma unroll
-        for (int j = 0; j < NB; j++) u0[j] = pg.k0 ^ rotl16(tv[j]);
-        if (GH) z = gh_reduce(gm, cb[0]);
-        phase++;
-        // phase 2: four lookups of round 2
-#pragma unroll
-        for (int j = 0; j < NB; j++) {
-            t[j][0] = a.t0<0>(u0[j]);
-            t[j][1] = a.t1<3>(u0[j]);
-            t[j][2] = a.t0<2>(u0[j]);
-            t[j][3] = a.t1<1>(u0[j]);
-        }
-        if (GH && NB > 1) gh_load(gh, z, gm);
-        QPP_PHASE_BARRIER();
-#pragma unroll
-        for (int j = 0; j < NB; j++) {
-            s[j][0] = pg.l0 ^ t[j][0];
-            s[j][1] = pg.l1 ^ rotl16(t[j][1]);
-            s[j][2] = pg.l2 ^ rotl16(t[j][2]);
-            s[j][3] = pg.l3 ^ t[j][3];
-        }
-        if (GH && NB > 1) z = gh_reduce(gm, cb[NB > 1 ? 1 : 0]);
-        phase++;
-    } else {
-#pragma unroll
-        for (int j = 0; j < NB; j++) {
-            s[j][0] = n0 ^ rk[0]; s[j][1] = n1 ^ rk[1]; s[j][2] = n2 ^ rk[2]; s[j][3] = bswap32(c + j) ^ rk[3];
-        }
-#pragma unroll
-        for (int r = 1; r <= 2; r++) {
-#pragma unroll
-            for (int j = 0; j < NB; j++) round_load(a, s[j], t[j]);
-            if (GH && phase < NB) gh_load(gh, z, gm);
-            QPP_PHASE_BARRIER();
-#pragma unroll
-            for (int j = 0; j < NB; j++) round_mix(t[j], rk + 4 * r, s[j]);
-            if (GH && phase < NB) z = gh_reduce(gm, cb[phase < NB ? phase : 0]);
-            phase++;
-        }
-    }
-#pragma unroll
-    for (int r = 3; r < NR; r++) {
-#pragma unroll
-        for (int j = 0; j < NB; j++) round_load(a, s[j], t[j]);
-        if (GH && phase < NB) gh_load(gh, z, gm);
-        QPP_PHASE_BARRIER();
-#pragma unroll
-        for (int j = 0; j < NB; j++) round_mix(t[j], rk + 4 * r, s[j]);
-        if (GH && phase < NB) z = gh_reduce(gm, cb[phase < NB ? phase : 0]);
-        phase++;
-    }
-#pragma unroll
-    for (int j = 0; j < NB; j++) round_load(a, s[j], t[j]);
-    if (GH && phase < NB) gh_load(gh, z, gm);
-    QPP_PHASE_BARRIER();
-#pragma unroll
-    for (int j = 0; j < NB; j++) ks[j] = round_final(t[j], rk + 4 * NR);
-    if (GH && phase < NB) z = gh_reduce(gm, cb[phase < NB ? phase : 0]);
-    phase++;
-#pragma unroll
-    for (int j = 0; j < NB; j++)
-        if (GH && j >= phase) z = gh.mulx(z, cb[j]);  // NB > NR: leftover steps
-}
-
 // Build both table sets for one key.  All 1024 threads take part; ends with a barrier.
 __device__ void build_tables(uint8_t *lds, const DevKey *__restrict__ key) {
     const uint32_t tid = threadIdx.x, nthr = blockDim.x;
@@ -212,17 +90,20 @@ __device__ __forceinline__ PacketView load_packet(const qpp_pkt &d, const DevKey
 }
 
 // Header protection mask from the 16-byte sample (first 5 bytes of AES_hp(sample)).  The HP round keys are read
-// here through a volatile pointer so the compiler cannot hoist them into SGPRs for the whole kernel: they are
-// used once per packet, and hoisting them spills the packet round keys (measured: 36 SGPR spills, slower seal).
+// here, once per packet, into VGPRs: hoisted into SGPRs for the whole kernel they pushed the packet round keys out
+// of SGPRs (measured: 36 SGPR spills and per-iteration round-key reloads, a slower seal).
 template <int HNR>
 __device__ __forceinline__ void hp_finish(const AesLds &aes, const uint32_t *hp_rk_g, uint4 sample,
                                           uint8_t *base, uint32_t hdr_len, uint32_t pn_len, uint8_t *mask_out,
                                           uint32_t flags) {
+    // launder the pointer through a VGPR: the loads below cannot be hoisted or kept in SGPRs
+    uint64_t a = (uint64_t)hp_rk_g;
+    asm volatile("" : "+v"(a));
+    const uint4 *src = (const uint4 *)a;
     uint32_t hp_rk[4 * (HNR + 1)];
-    const volatile uint4 *src = (const volatile uint4 *)hp_rk_g;
 #pragma unroll
     for (int i = 0; i < HNR + 1; i++) {
-        const uint4 v = make_uint4(src[i].x, src[i].y, src[i].z, src[i].w);
+        const uint4 v = src[i];
         hp_rk[4 * i] = v.x; hp_rk[4 * i + 1] = v.y; hp_rk[4 * i + 2] = v.z; hp_rk[4 * i + 3] = v.w;
     }
     uint4 m = aes.encrypt<HNR>(sample, hp_rk);
@@ -251,123 +132,87 @@ __device__ __forceinline__ uint4 ghash_aad_z(const GhashLds &gh, const uint8_t *
     return z;
 }
 
-// One packet per lane.  Blocks are processed NB at a time: the keystream of group g+1 is computed in the same
-// basic block as the GHASH chain of group g, so the two independent dependency chains overlap.
-template <int NR, int NB, bool SEAL, bool PHASED>
+// One packet per lane.  Counter blocks are grouped [NB*g, NB*g + NB) with NB | 256, so a group never crosses a
+// 256-block page (CtrPage constants hold for the whole group) and the packet runs through ONE loop body:
+//   counter 0: unused (its keystream is discarded), counter 1: J0 -> E_K(J0) masks the tag,
+//   counter b + 2: data block b.
+// The GHASH steps of group g-1 are issued in the same basic block as the keystream of group g, so the two
+// independent dependency chains overlap.
+template <int NR, int NB, bool SEAL>
 __device__ __forceinline__ void process_packet(const AesLds &aes, const GhashLds &gh, const DevKey *__restrict__ key,
                                                const qpp_pkt &d, uint32_t pkt_index, uint8_t *arena, uint8_t *masks,
                                                int8_t *status, uint32_t flags) {
+    static_assert(NB >= 2 && (256 % NB) == 0, "NB must divide 256 (and hold counter 1)");
     const uint32_t *__restrict__ rk = key->rk;
     PacketView p = load_packet(d, key, arena);
     uint8_t *pay = p.base + p.aad_len;
     CtrPage pg;
     pg.build(aes, rk, p.n0, p.n1, p.n2, 0);
-    // E_K(J0), J0 = nonce || 1 (page 0)
-    uint4 ek0;
-    {
-        uint32_t s[4];
-        pg.two_rounds(aes, 1, s);
-#pragma unroll
-        for (int r = 3; r < NR; r++) aes.round(s, rk + 4 * r);
-        ek0 = aes.final(s, rk + 4 * NR);
-    }
-    // GHASH state Z = Y ^ (next block), so Y_next * H ^ C folds into one mulx.  Z starts at 0: a leading
-    // zero block does not change GHASH, so every block (AAD included) is absorbed with the same step.
     uint4 z = ghash_aad_z(gh, p.base, p.aad_len);
 
-    const uint32_t nfull = p.len >> 4, rem = p.len & 15;
-    const uint32_t ngroups = nfull / NB;
-    uint4 ks[NB], in[NB];
-    const uint32_t ctr = 2;
-    // group 0: loads stay inside payload||tag (a block start o is readable for 16 bytes iff o <= len)
-#pragma unroll
-    for (int j = 0; j < NB; j++) in[j] = ld16(16u * j <= p.len ? pay + 16 * j : pay);
-    {
-        uint4 none[NB];
-        group_phased<NR, NB, true, false>(aes, gh, pg, rk, p.n0, p.n1, p.n2, ctr, ks, z, none);
-    }
-    // first two ciphertext blocks for the HP sample (used only when len >= 32, i.e. both are full blocks)
-    uint4 c0 = SEAL ? in[0] ^ ks[0] : in[0];
-    uint4 c1 = NB > 1 ? (SEAL ? in[NB > 1 ? 1 : 0] ^ ks[NB > 1 ? 1 : 0] : in[NB > 1 ? 1 : 0]) : c0;
-    for (uint32_t g = 0; g < ngroups; g++) {
-        uint4 cblk[NB];
-#pragma unroll
-        for (int j = 0; j < NB; j++) {
-            const uint4 out = in[j] ^ ks[j];
-            st16(pay + 16 * (NB * g + j), out);
-            cblk[j] = SEAL ? out : in[j];
-        }
-        // next group's input blocks and keystream (also serve the tail after the last full group)
-        const uint32_t nb = NB * (g + 1);
-#pragma unroll
-        for (int j = 0; j < NB; j++) {
-            const uint32_t o = 16 * (nb + j);
-            in[j] = ld16(o <= p.len ? pay + o : pay);
-        }
-        const uint32_t c = ctr + nb;
-        if (PHASED) {
-            // keystream of the next group with this group's GHASH steps interleaved phase by phase
-            if (((c + NB - 1) >> 8) != (c >> 8)) {
-                group_phased<NR, NB, false, true>(aes, gh, pg, rk, p.n0, p.n1, p.n2, c, ks, z, cblk);
-            } else {
-                if ((c >> 8) != pg.page) pg.build(aes, rk, p.n0, p.n1, p.n2, c >> 8);
-                group_phased<NR, NB, true, true>(aes, gh, pg, rk, p.n0, p.n1, p.n2, c, ks, z, cblk);
-            }
-        } else {
-            // keystream of the next group, then this group's GHASH chain; the compiler interleaves the two
-            if (((c + NB - 1) >> 8) != (c >> 8)) {
-                ctr_keystream_full<NR, NB>(aes, rk, p.n0, p.n1, p.n2, c, ks);
-            } else {
-                if ((c >> 8) != pg.page) pg.build(aes, rk, p.n0, p.n1, p.n2, c >> 8);
-                ctr_keystream<NR, NB>(aes, pg, rk, c, ks);
-            }
-#pragma unroll
-            for (int j = 0; j < NB; j++) z = gh.mulx(z, cblk[j]);
-        }
-    }
-    // tail: up to NB-1 full blocks and one partial block; their keystream is already in ks[]
-    const uint32_t done = NB * ngroups;
+    const int nfull = (int)(p.len >> 4), rem = (int)(p.len & 15);
+    const int nblk = nfull + (rem ? 1 : 0);
+    const int ngroups = (nblk + 2 + NB - 1) / NB;
+    uint4 ks[NB], in[NB], cprev[NB], ek0 = make_uint4(0, 0, 0, 0);
+    int bprev = -NB;  // first block index of the previous group (for its GHASH validity)
+    // group 0 inputs: slots 0, 1 are counters 0 and 1 (no data)
 #pragma unroll
     for (int j = 0; j < NB; j++) {
-        const uint32_t b = done + j;
-        if (b < nfull) {
+        const int b = j - 2;
+        in[j] = ld16(b >= 0 && 16 * b <= (int)p.len ? pay + 16 * b : pay);
+    }
+    for (int g = 0; g < ngroups; g++) {
+        const uint32_t c = (uint32_t)(NB * g);
+        if ((c >> 8) != pg.page) pg.build(aes, rk, p.n0, p.n1, p.n2, c >> 8);
+        ctr_keystream<NR, NB>(aes, pg, rk, c, ks);
+        // GHASH of the previous group (independent of the keystream just issued)
+#pragma unroll
+        for (int j = 0; j < NB; j++)
+            if (bprev + j >= 0 && bprev + j < nblk) z = gh.mulx(z, cprev[j]);
+        if (g == 0) ek0 = ks[1];
+        const int b0 = NB * g - 2;  // data block of slot 0
+#pragma unroll
+        for (int j = 0; j < NB; j++) {
+            const int b = b0 + j;
             const uint4 out = in[j] ^ ks[j];
-            st16(pay + 16 * b, out);
-            z = gh.mulx(z, SEAL ? out : in[j]);
-        } else if (b == nfull && rem) {
-            const uint4 out = keep_bytes(in[j] ^ ks[j], rem);
-            st_bytes(pay + 16 * b, out, rem);
-            z = gh.mulx(z, SEAL ? out : keep_bytes(in[j], rem));
+            if (b >= 0 && b < nfull) {
+                st16(pay + 16 * b, out);
+                cprev[j] = SEAL ? out : in[j];
+            } else if (b == nfull && rem) {
+                const uint4 o = keep_bytes(out, rem);
+                st_bytes(pay + 16 * b, o, rem);
+                cprev[j] = SEAL ? o : keep_bytes(in[j], rem);
+            }
+        }
+        bprev = b0;
+        // next group's input blocks (clamped inside payload||tag)
+#pragma unroll
+        for (int j = 0; j < NB; j++) {
+            const int b = b0 + NB + j;
+            in[j] = ld16(16 * b <= (int)p.len ? pay + 16 * b : pay);
         }
     }
-    if (NB == 1 && p.len >= 32) c1 = ld16(pay + 16);  // NB == 1 has no second block in registers
-    // length block: be64(aad bits) || be64(payload bits); then the final multiply
+#pragma unroll
+    for (int j = 0; j < NB; j++)
+        if (bprev + j >= 0 && bprev + j < nblk) z = gh.mulx(z, cprev[j]);
+    // length block: be64(aad bits) || be64(payload bits); tag = Y * H ^ E_K(J0)
     z = gh.mulx(z, make_uint4(0, bswap32(p.aad_len * 8), 0, bswap32(p.len * 8)));
-    const uint4 tag = gh.mulx(z, ek0);  // Y * H ^ E_K(J0)
+    const uint4 tag = gh.mulx(z, ek0);
 
     if (SEAL) {
         st16(pay + p.len, tag);
         int8_t st = QPP_OK;
         if (flags & (QPP_HP_MASK_OUT | QPP_HP_APPLY)) {
-            // sample = ciphertext||tag bytes [4 - pn_len, 20 - pn_len)  (payload.rs:151-169)
+            // sample = ciphertext||tag bytes [4 - pn_len, 20 - pn_len)  (payload.rs:151-169), read back: the lane
+            // wrote those bytes itself (same-lane store -> load ordering)
             const uint32_t s = 4 - p.pn_len;
             if (p.pn_len < 1 || p.pn_len > 4 || p.len < s) {
                 st = QPP_DECODE_ERROR;
             } else {
-                uint4 smp;
-                if (p.len >= 32) {
-                    smp.x = __builtin_amdgcn_alignbyte(c0.y, c0.x, s);
-                    smp.y = __builtin_amdgcn_alignbyte(c0.z, c0.y, s);
-                    smp.z = __builtin_amdgcn_alignbyte(c0.w, c0.z, s);
-                    smp.w = __builtin_amdgcn_alignbyte(c1.x, c0.w, s);
-                } else {
-                    smp = ld16(pay + s);  // short payload: sample reaches into the tag just stored
-                }
+                const uint4 smp = ld16(pay + s);
                 const uint32_t hdr_len = p.aad_len - p.pn_len;
-                if (key->hp_nr == 10)
-                    hp_finish<10>(aes, key->hp_rk, smp, p.base, hdr_len, p.pn_len, masks + 5 * (size_t)pkt_index, flags);
-                else
-                    hp_finish<14>(aes, key->hp_rk, smp, p.base, hdr_len, p.pn_len, masks + 5 * (size_t)pkt_index, flags);
+                hp_finish<NR == 10 ? 10 : 14>(aes, key->hp_rk, smp, p.base, hdr_len, p.pn_len,
+                                              masks + 5 * (size_t)pkt_index, flags);
             }
         }
         if (status) status[pkt_index] = st;
@@ -377,14 +222,14 @@ __device__ __forceinline__ void process_packet(const AesLds &aes, const GhashLds
         const bool ok = (diff.x | diff.y | diff.z | diff.w) == 0;  // all 16 bytes compared, no early exit
         if (!ok) {
             // never release unauthenticated plaintext
-            for (uint32_t b = 0; b < nfull; b++) st16(pay + 16 * b, make_uint4(0, 0, 0, 0));
+            for (int b = 0; b < nfull; b++) st16(pay + 16 * b, make_uint4(0, 0, 0, 0));
             if (rem) st_bytes(pay + 16 * nfull, make_uint4(0, 0, 0, 0), rem);
         }
         status[pkt_index] = ok ? QPP_OK : QPP_DECRYPT_ERROR;
     }
 }
 
-template <bool SEAL, int NB, int WG, bool PHASED>
+template <bool SEAL, int NB, int WG, int NR>
 __global__ __launch_bounds__(WG) void aes_gcm_kernel(const DevKey *__restrict__ keys, const qpp_pkt *__restrict__ descs,
                                                     const uint32_t *__restrict__ perm, const WorkItem *__restrict__ work,
                                                     const uint32_t *__restrict__ n_work, uint8_t *__restrict__ arena,
@@ -396,6 +241,7 @@ __global__ __launch_bounds__(WG) void aes_gcm_kernel(const DevKey *__restrict__ 
 #endif
     if (blockIdx.x >= *n_work) return;  // uniform: grid is sized for the worst case
     const WorkItem w = work[blockIdx.x];
+    if (w.nr != NR) return;  // AES-128 and AES-256 work items are served by separate launches (SGPR budget)
     const DevKey *__restrict__ key = keys + w.key;
     build_tables(lds, key);
     const AesLds aes = make_aes(lds);
@@ -403,10 +249,7 @@ __global__ __launch_bounds__(WG) void aes_gcm_kernel(const DevKey *__restrict__ 
     for (uint32_t t = threadIdx.x; t < w.count; t += WG) {  // WG < 1024: several passes over the work item
         const uint32_t pi = perm[w.begin + t];
         const qpp_pkt d = descs[pi];
-        if (w.nr == 10)
-            process_packet<10, NB, SEAL, PHASED>(aes, gh, key, d, pi, arena, masks, status, flags);
-        else
-            process_packet<14, NB, SEAL, PHASED>(aes, gh, key, d, pi, arena, masks, status, flags);
+        process_packet<NR, NB, SEAL>(aes, gh, key, d, pi, arena, masks, status, flags);
     }
 }
 
@@ -473,27 +316,22 @@ constexpr uint32_t kDynLds = kLdsBytes;
 // selects one (tuning knob).  One workgroup per CU (130 KiB LDS), so WG = waves per CU x 64.
 struct Variant {
     int nb, wg, per;
-    bool phased;
 };
-constexpr Variant kVariants[] = {{6, 512, 1024, false}, {4, 512, 1024, false}, {4, 512, 1024, true},
-                                 {2, 512, 1024, true},  {2, 1024, 1024, false}, {8, 512, 1024, false},
-                                 {4, 512, 512, false}};
+constexpr Variant kVariants[] = {{4, 512, 1024}, {8, 512, 1024}, {2, 1024, 1024}, {4, 512, 512}, {2, 512, 1024}};
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
-template <bool SEAL>
+template <bool SEAL, int NR>
 void launch_variant(int v, dim3 grid, hipStream_t s, const DevKey *keys, const qpp_pkt *descs, const PlanBuffers &pb,
                     uint8_t *arena, uint8_t *masks, int8_t *status, uint32_t flags) {
-#define QPP_AES_LAUNCH(NB, WG, PH)                                                                                 \
-    hipLaunchKernelGGL((aes_gcm_kernel<SEAL, NB, WG, PH>), grid, dim3(WG), kDynLds, s, keys, descs, pb.perm,     \
+#define QPP_AES_LAUNCH(NB, WG)                                                                                    \
+    hipLaunchKernelGGL((aes_gcm_kernel<SEAL, NB, WG, NR>), grid, dim3(WG), kDynLds, s, keys, descs, pb.perm,     \
                        pb.work, pb.n_work, arena, masks, status, flags)
     switch (v) {
-        case 0: QPP_AES_LAUNCH(6, 512, false); break;
-        case 1: QPP_AES_LAUNCH(4, 512, false); break;
-        case 2: QPP_AES_LAUNCH(4, 512, true); break;
-        case 3: QPP_AES_LAUNCH(2, 512, true); break;
-        case 4: QPP_AES_LAUNCH(2, 1024, false); break;
-        case 5: QPP_AES_LAUNCH(8, 512, false); break;
-        default: QPP_AES_LAUNCH(4, 512, false); break;
+        case 0: QPP_AES_LAUNCH(4, 512); break;
+        case 1: QPP_AES_LAUNCH(8, 512); break;
+        case 2: QPP_AES_LAUNCH(2, 1024); break;
+        case 3: QPP_AES_LAUNCH(4, 512); break;
+        default: QPP_AES_LAUNCH(2, 512); break;
     }
 #undef QPP_AES_LAUNCH
 }
@@ -512,13 +350,18 @@ uint32_t aes_packets_per_item() { return (uint32_t)kVariants[aes_variant()].per;
 
 hipError_t launch_aes_gcm(bool seal, const DevKey *keys, const qpp_pkt *descs, const PlanBuffers &pb, uint32_t n,
                           uint32_t key_cap, uint8_t *arena, uint8_t *masks, int8_t *status, uint32_t flags,
-                          hipStream_t s) {
+                          uint32_t suites, hipStream_t s) {
     if (!n) return hipSuccess;
     const dim3 grid(plan_max_work(n, key_cap, aes_packets_per_item()));
-    if (seal)
-        launch_variant<true>(aes_variant(), grid, s, keys, descs, pb, arena, masks, status, flags);
-    else
-        launch_variant<false>(aes_variant(), grid, s, keys, descs, pb, arena, masks, status, flags);
+    const int v = aes_variant();
+    if (suites & (1u << QPP_SUITE_TLS_AES_128_GCM_SHA256)) {
+        if (seal) launch_variant<true, 10>(v, grid, s, keys, descs, pb, arena, masks, status, flags);
+        else launch_variant<false, 10>(v, grid, s, keys, descs, pb, arena, masks, status, flags);
+    }
+    if (suites & (1u << QPP_SUITE_TLS_AES_256_GCM_SHA384)) {
+        if (seal) launch_variant<true, 14>(v, grid, s, keys, descs, pb, arena, masks, status, flags);
+        else launch_variant<false, 14>(v, grid, s, keys, descs, pb, arena, masks, status, flags);
+    }
     return hipGetLastError();
 }
 

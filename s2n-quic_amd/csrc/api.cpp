@@ -20,6 +20,7 @@ struct qpp_ctx {
     uint32_t key_cap = 0;
     std::vector<DevKey> h_keys;
     std::vector<uint32_t> free_slots;
+    uint32_t live_by_suite[4] = {0, 0, 0, 0};  // live keys per suite: which kernels a batch can need
     uint32_t next_slot = 0;
     uint32_t dirty_lo = UINT32_MAX, dirty_hi = 0;
     // plan scratch
@@ -153,6 +154,7 @@ int install(qpp_key *k) {
     }
     ctx->dirty_lo = std::min(ctx->dirty_lo, k->slot);
     ctx->dirty_hi = std::max(ctx->dirty_hi, k->slot + 1);
+    ctx->live_by_suite[k->suite]++;
     return QPP_OK;
 }
 
@@ -164,6 +166,13 @@ void derive(qpp_key *k) {
 }
 
 bool is_aes(int suite) { return suite != QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256; }
+
+uint32_t suite_mask(const qpp_ctx *ctx) {
+    uint32_t m = 0;
+    for (int s = 1; s <= 3; s++)
+        if (ctx->live_by_suite[s]) m |= 1u << s;
+    return m;
+}
 
 // One packet through the batch kernels: stage = [pad4 | header | payload | tag].
 int run_one(const qpp_key *k, bool seal, uint64_t pn, const uint8_t *header, size_t header_len, const uint8_t *payload,
@@ -199,7 +208,7 @@ int run_one(const qpp_key *k, bool seal, uint64_t pn, const uint8_t *header, siz
         HIP_TRY(ctx, hipMemcpyAsync(ctx->plan1.n_work, &one, 4, hipMemcpyHostToDevice, s));
         // key_cap = 0: grid = plan_max_work(1, 0, per) = 1; only work item 0 exists
         HIP_TRY(ctx, launch_aes_gcm(seal, ctx->d_keys, ctx->d_desc1, ctx->plan1, 1, 0, ctx->d_stage, ctx->d_mask1,
-                                    ctx->d_status1, 0, s));
+                                    ctx->d_status1, 0, 1u << k->suite, s));
     } else {
         HIP_TRY(ctx, launch_chacha(seal, ctx->d_keys, ctx->d_desc1, 1, ctx->d_stage, ctx->d_mask1, ctx->d_status1, 0, s));
     }
@@ -336,6 +345,7 @@ void qpp_key_free(qpp_key *key) {
     qpp_ctx *ctx = key->ctx;
     if (ctx && key->slot < ctx->key_cap && ctx->h_keys[key->slot].live) {
         hipSetDevice(ctx->device);
+        ctx->live_by_suite[key->suite]--;
         secure_zero(&ctx->h_keys[key->slot], sizeof(DevKey));
         hipMemset(ctx->d_keys + key->slot, 0, sizeof(DevKey));  // synchronous: zeroize the device copy
         ctx->free_slots.push_back(key->slot);
@@ -463,7 +473,7 @@ int qpp_seal_batch(qpp_ctx *ctx, const qpp_pkt *descs, size_t n, uint8_t *arena,
         if (rc) return rc;
         HIP_TRY(ctx, launch_plan(ctx->d_keys, ctx->key_cap, descs, (uint32_t)n, ctx->plan, aes_packets_per_item(), s));
         HIP_TRY(ctx, launch_aes_gcm(true, ctx->d_keys, descs, ctx->plan, (uint32_t)n, ctx->key_cap, arena, masks, status,
-                                    flags, s));
+                                    flags, suite_mask(ctx), s));
     }
     if (!(flags & QPP_ONLY_AES))
         HIP_TRY(ctx, launch_chacha(true, ctx->d_keys, descs, (uint32_t)n, arena, masks, status, flags, s));
@@ -484,7 +494,7 @@ int qpp_open_batch(qpp_ctx *ctx, const qpp_pkt *descs, size_t n, uint8_t *arena,
         if (rc) return rc;
         HIP_TRY(ctx, launch_plan(ctx->d_keys, ctx->key_cap, descs, (uint32_t)n, ctx->plan, aes_packets_per_item(), s));
         HIP_TRY(ctx, launch_aes_gcm(false, ctx->d_keys, descs, ctx->plan, (uint32_t)n, ctx->key_cap, arena, nullptr,
-                                    status, 0, s));
+                                    status, 0, suite_mask(ctx), s));
     }
     if (!(flags & QPP_ONLY_AES))
         HIP_TRY(ctx, launch_chacha(false, ctx->d_keys, descs, (uint32_t)n, arena, nullptr, status, 0, s));

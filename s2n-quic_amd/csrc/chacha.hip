@@ -125,6 +125,8 @@ __device__ __forceinline__ void apply_mask(uint8_t *base, uint32_t hdr_len, uint
     }
 }
 
+// One lane per packet, software-pipelined over 64-byte chunks: the keystream of chunk g+1 is computed in the same
+// basic block as the Poly1305 steps of chunk g (independent chains), and chunk g+1's input is loaded one chunk ahead.
 template <bool SEAL>
 __global__ __launch_bounds__(256) void chacha_kernel(const DevKey *__restrict__ keys, const qpp_pkt *__restrict__ descs,
                                                     uint32_t n, uint8_t *__restrict__ arena, uint8_t *masks,
@@ -153,29 +155,47 @@ __global__ __launch_bounds__(256) void chacha_kernel(const DevKey *__restrict__ 
         if (aad_len - off < 16) a = keep_bytes(a, aad_len - off);
         mac.block(a);
     }
-    uint4 c0 = make_uint4(0, 0, 0, 0), c1 = c0;
-    for (uint32_t off = 0, ctr = 1; off < len; off += 64, ctr++) {
-        chacha_block(k, ctr, n0, n1, n2, ks);
+    // inputs of chunk c (4 blocks, each clamped inside payload||tag)
+    auto load_chunk = [&](uint32_t c, uint4 (&in)[4]) {
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-            const uint32_t o = off + 16 * q;
-            if (o < len) {
-                uint4 in = ld16(pay + o);  // in bounds: payload||tag
-                uint4 out = in ^ make_uint4(ks[4 * q], ks[4 * q + 1], ks[4 * q + 2], ks[4 * q + 3]);
-                const uint32_t r = len - o;
-                uint4 c;
-                if (r >= 16) {
-                    st16(pay + o, out);
-                    c = SEAL ? out : in;
-                } else {
-                    out = keep_bytes(out, r);
-                    st_bytes(pay + o, out, r);
-                    c = SEAL ? out : keep_bytes(in, r);
-                }
-                if (o == 0) c0 = c;
-                if (o == 16) c1 = c;
-                mac.block(c);
+            const uint32_t o = 64 * c + 16 * q;
+            in[q] = ld16(o <= len ? pay + o : pay);
+        }
+    };
+    const uint32_t nchunks = len / 64;  // full 64-byte chunks
+    uint4 in[4], cb[4];
+    load_chunk(0, in);
+    chacha_block(k, 1, n0, n1, n2, ks);
+    for (uint32_t c = 0; c < nchunks; c++) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint4 out = in[q] ^ make_uint4(ks[4 * q], ks[4 * q + 1], ks[4 * q + 2], ks[4 * q + 3]);
+            st16(pay + 64 * c + 16 * q, out);
+            cb[q] = SEAL ? out : in[q];
+        }
+        load_chunk(c + 1, in);
+        chacha_block(k, c + 2, n0, n1, n2, ks);  // next chunk (or the tail) ...
+#pragma unroll
+        for (int q = 0; q < 4; q++) mac.block(cb[q]);  // ... beside this chunk's MAC
+    }
+    // tail: < 64 bytes, keystream already in ks[]
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const uint32_t o = 64 * nchunks + 16 * q;
+        if (o < len) {
+            uint4 out = in[q] ^ make_uint4(ks[4 * q], ks[4 * q + 1], ks[4 * q + 2], ks[4 * q + 3]);
+            const uint32_t r = len - o;
+            uint4 c;
+            if (r >= 16) {
+                st16(pay + o, out);
+                c = SEAL ? out : in[q];
+            } else {
+                out = keep_bytes(out, r);
+                st_bytes(pay + o, out, r);
+                c = SEAL ? out : keep_bytes(in[q], r);
             }
+            mac.block(c);
         }
     }
     mac.block(make_uint4(aad_len, 0, len, 0));  // le64(aad_len) || le64(ct_len)
@@ -189,15 +209,7 @@ __global__ __launch_bounds__(256) void chacha_kernel(const DevKey *__restrict__ 
             if (d.pn_len < 1 || d.pn_len > 4 || len < s) {
                 st = QPP_DECODE_ERROR;
             } else {
-                uint4 smp;
-                if (len >= 32) {
-                    smp.x = __builtin_amdgcn_alignbyte(c0.y, c0.x, s);
-                    smp.y = __builtin_amdgcn_alignbyte(c0.z, c0.y, s);
-                    smp.z = __builtin_amdgcn_alignbyte(c0.w, c0.z, s);
-                    smp.w = __builtin_amdgcn_alignbyte(c1.x, c0.w, s);
-                } else {
-                    smp = ld16(pay + s);
-                }
+                const uint4 smp = ld16(pay + s);  // this lane's own ciphertext||tag bytes
                 uint32_t hk[8];
 #pragma unroll
                 for (int i = 0; i < 8; i++) hk[i] = key->hp_rk[i];

@@ -157,14 +157,6 @@ __device__ __forceinline__ void ctr_keystream(const AesLds &a, const CtrPage &pg
     for (int j = 0; j < NB; j++) ks[j] = a.final(s[j], rk + 4 * NR);
 }
 
-// Same without caching (group straddles a page boundary; rare).
-template <int NR, int NB>
-__device__ __forceinline__ void ctr_keystream_full(const AesLds &a, const uint32_t *__restrict__ rk, uint32_t n0,
-                                                   uint32_t n1, uint32_t n2, uint32_t c, uint4 (&ks)[NB]) {
-#pragma unroll
-    for (int j = 0; j < NB; j++) ks[j] = a.encrypt<NR>(make_uint4(n0, n1, n2, bswap32(c + j)), rk);
-}
-
 // AES T0/T1 bank-replicated tables for the AesLds view: dword d -> row x = d >> 6, slot = d & 63
 // (slots 32..63 hold T1 = rotl8 T0).  No barrier inside.
 __device__ __forceinline__ void build_aes_tables(uint8_t *lds) {

@@ -88,9 +88,10 @@ hipError_t launch_plan(const DevKey *keys, uint32_t key_cap, const qpp_pkt *desc
                        uint32_t per, hipStream_t s);
 uint32_t plan_max_work(uint32_t n, uint32_t key_cap, uint32_t per);
 uint32_t aes_packets_per_item();  // work-item size of the selected AES-GCM kernel variant
+// suites: bit (1 << suite) for every suite with a live key in the context (launches only what can occur)
 hipError_t launch_aes_gcm(bool seal, const DevKey *keys, const qpp_pkt *descs, const PlanBuffers &pb, uint32_t n,
                           uint32_t key_cap, uint8_t *arena, uint8_t *masks, int8_t *status, uint32_t flags,
-                          hipStream_t s);
+                          uint32_t suites, hipStream_t s);
 hipError_t launch_chacha(bool seal, const DevKey *keys, const qpp_pkt *descs, uint32_t n, uint8_t *arena,
                          uint8_t *masks, int8_t *status, uint32_t flags, hipStream_t s);
 hipError_t launch_hp_mask(const DevKey *keys, const qpp_pkt *descs, uint32_t n, const uint8_t *arena,

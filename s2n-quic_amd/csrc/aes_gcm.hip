@@ -25,47 +25,83 @@ namespace {
 using namespace dev;
 
 // ---------------------------------------------------------------- GHASH: Y <- Y * H via 16 byte tables in LDS
-// X * H = xor_j T_j[x_j] (GF(2)-linear in X).  The running value is kept as Z = Y ^ C_next so that the
-// xor with the next block folds into the last xor3 of the table reduction.
-struct GhashLds {
-    const uint8_t *lds;
-    template <int J>
-    __device__ __forceinline__ uint4 tj(uint32_t w) const {
-        constexpr int kShift = 8 * (J & 3);
-        uint32_t off = ((w >> kShift) & 0xffu) << 4;
-        return *(const uint4 *)(lds + kLdsGhash + J * 4096 + off);
+// X * H = xor_j T_j[x_j] (GF(2)-linear in X), T_j[x] = (x at byte j) * H.  The running value is kept as
+// Z = Y ^ C_next so that the xor with the next block folds into the last xor3 of the table reduction.
+//
+// Conflict-free layout: T_j[x] lives at x * 256 + j * 16, so a 256-byte row holds the 16 tables' entries for
+// one byte value and table j always sits in bank quad j.  A ds_read_b128 serves 16 lanes per LDS cycle; if
+// those lanes all read the SAME table j with random x they pile onto one bank quad (with the old j * 4096 +
+// x * 16 layout they spread randomly: ~3x cycles, 27 % of all LDS cycles were bank conflicts).  So every lane
+// walks the 16 byte positions in its own order: lane r = lane % 16 = 4 q + b reads, at step (k, i), byte
+// j(k, i) = 4 ((k + q) & 3) + ((i + b) & 3).  Within each 16-lane group of ds_read_b128 ({0-3,12-15,20-27},
+// {4-11,16-19,28-31}, and the same + 32) the lanes have distinct r, hence distinct j: one LDS cycle per group.
+// The word part of that order is a rotation of Z's words by q (W[k] = Z.w[(k + q) & 3], two v_cndmask levels),
+// the byte part a per-lane v_perm selector; the address (x << 8 | j << 4) is that one v_perm.
+struct Ghash {
+    uint32_t lc[4];   // byte i of lc[k] = 16 * j(k, i)
+    uint32_t sel[4];  // v_perm selector of step i: byte0 <- lc[k].b_i, byte1 <- W[k].b_((i+b)&3), bytes 2,3 <- 0
+    bool q1, q2;      // word rotation by q = q1 + 2 q2
+
+    __device__ __forceinline__ static Ghash make() {
+        Ghash g;
+        const uint32_t r = threadIdx.x & 15u, q = r >> 2, b = r & 3u;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            uint32_t v = 0;
+#pragma unroll
+            for (int i = 0; i < 4; i++) v |= ((4u * ((k + q) & 3u) + ((i + b) & 3u)) << 4) << (8 * i);
+            g.lc[k] = v;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; i++) g.sel[i] = 0x0c0c0000u | ((4u + ((i + b) & 3u)) << 8) | (uint32_t)i;
+        g.q1 = q & 1u;
+        g.q2 = (q >> 1) & 1u;
+        return g;
     }
-    // returns z * H ^ c
-    __device__ __forceinline__ uint4 mulx(uint4 z, uint4 c) const {
-        uint4 a = xor3(tj<0>(z.x), tj<1>(z.x), tj<2>(z.x));
-        uint4 b = xor3(tj<3>(z.x), tj<4>(z.y), tj<5>(z.y));
-        uint4 d = xor3(tj<6>(z.y), tj<7>(z.y), tj<8>(z.z));
-        uint4 e = xor3(tj<9>(z.z), tj<10>(z.z), tj<11>(z.z));
-        uint4 f = xor3(tj<12>(z.w), tj<13>(z.w), tj<14>(z.w));
-        uint4 g = xor3(a, b, d);
-        uint4 h = xor3(e, f, tj<15>(z.w));
+    // W = Z with its words rotated by q
+    __device__ __forceinline__ uint4 rot(uint4 z) const {
+        const uint4 a = q1 ? make_uint4(z.y, z.z, z.w, z.x) : z;
+        return q2 ? make_uint4(a.z, a.w, a.x, a.y) : a;
+    }
+    template <int K, int I>
+    __device__ __forceinline__ uint4 look(const uint4 &w) const {
+        const uint32_t wk = K == 0 ? w.x : K == 1 ? w.y : K == 2 ? w.z : w.w;
+        return lds_ld128(kLdsGhash + __builtin_amdgcn_perm(wk, lc[K], sel[I]));
+    }
+    // (Z * H) ^ c in natural word order, from W = rot(Z)
+    __device__ __forceinline__ uint4 prod(const uint4 &w, uint4 c) const {
+        const uint4 a = xor3(look<0, 0>(w), look<0, 1>(w), look<0, 2>(w));
+        const uint4 b = xor3(look<0, 3>(w), look<1, 0>(w), look<1, 1>(w));
+        const uint4 d = xor3(look<1, 2>(w), look<1, 3>(w), look<2, 0>(w));
+        const uint4 e = xor3(look<2, 1>(w), look<2, 2>(w), look<2, 3>(w));
+        const uint4 f = xor3(look<3, 0>(w), look<3, 1>(w), look<3, 2>(w));
+        const uint4 g = xor3(a, b, d);
+        const uint4 h = xor3(e, f, look<3, 3>(w));
         return xor3(g, h, c);
     }
+    // one chain step: W' = rot(Z * H ^ c)
+    __device__ __forceinline__ uint4 mulx(const uint4 &w, uint4 c) const { return rot(prod(w, c)); }
 };
 
-// Build both table sets for one key.  All 1024 threads take part; ends with a barrier.
-__device__ void build_tables(uint8_t *lds, const DevKey *__restrict__ key) {
+// Build both table sets for one key.  All threads take part; ends with a barrier.
+__device__ void build_tables(const DevKey *__restrict__ key) {
     const uint32_t tid = threadIdx.x, nthr = blockDim.x;
     // V powers -> LDS
     for (uint32_t i = tid; i < 128; i += nthr) {
         const uint32_t *v = key->V[i];
-        *(uint4 *)(lds + kLdsV + 16 * i) = make_uint4(v[0], v[1], v[2], v[3]);
+        lds_st128(kLdsV + 16 * i, make_uint4(v[0], v[1], v[2], v[3]));
     }
-    build_aes_tables(lds);
+    build_aes_tables(kLdsAes);
     __syncthreads();
-    // GHASH tables: entry e = 256 j + x; T_j[x] = xor of V[8j+i] over set bits (bit 7-i) of x
+    // GHASH tables: entry e = 16 x + j (consecutive threads fill one row); T_j[x] = xor of V[8j+i] over the set
+    // bits (bit 7-i) of x
     for (uint32_t e = tid; e < 4096; e += nthr) {
-        uint32_t j = e >> 8, x = e & 255;
+        const uint32_t j = e & 15, x = e >> 4;
         uint4 acc = make_uint4(0, 0, 0, 0);
 #pragma unroll
         for (int i = 0; i < 8; i++)
-            if ((x >> (7 - i)) & 1) acc = acc ^ *(const uint4 *)(lds + kLdsV + 16 * (8 * j + i));
-        *(uint4 *)(lds + kLdsGhash + 16 * e) = acc;
+            if ((x >> (7 - i)) & 1) acc = acc ^ lds_ld128(kLdsV + 16 * (8 * j + i));
+        lds_st128(kLdsGhash + 256 * x + 16 * j, acc);
     }
     __syncthreads();
 }
@@ -120,63 +156,135 @@ __device__ __forceinline__ void hp_finish(const AesLds &aes, const uint32_t *hp_
     }
 }
 
-// GHASH over the AAD (zero-padded to 16 bytes), as the pending Z of the chain.
-__device__ __forceinline__ uint4 ghash_aad_z(const GhashLds &gh, const uint8_t *aad, uint32_t aad_len) {
-    uint4 z = make_uint4(0, 0, 0, 0);
+// GHASH over the AAD (zero-padded to 16 bytes), as the pending (rotated) Z of the chain.
+__device__ __forceinline__ uint4 ghash_aad_w(const Ghash &gh, const uint8_t *aad, uint32_t aad_len) {
+    uint4 w = make_uint4(0, 0, 0, 0);
     for (uint32_t off = 0; off < aad_len; off += 16) {
         uint4 a = ld16(aad + off);
         uint32_t r = aad_len - off;
         if (r < 16) a = keep_bytes(a, r);
-        z = gh.mulx(z, a);
+        w = off ? gh.mulx(w, a) : gh.rot(a);  // Y_0 = 0: the first Z is the block itself
     }
-    return z;
+    return w;
 }
 
-// One packet per lane.  Counter blocks are grouped [NB*g, NB*g + NB) with NB | 256, so a group never crosses a
-// 256-block page (CtrPage constants hold for the whole group) and the packet runs through ONE loop body:
+// Coalesced payload I/O through a per-wave LDS staging area.  A lane-per-packet load touches 64 scattered lines
+// per wave instruction (packets are ~1.2 KB apart) and thrashes L1 (measured: with the payload I/O confined to an
+// L1-resident window the seal ran 1.9 -> 1.5 ms at NB = 4, and 3.1 -> 1.2 ms at NB = 2 / 1024 threads).  So each
+// group's NB x 16 B per packet is moved cooperatively: in wave instruction i, the NB lanes of a lane-group of NB
+// load the NB chunks of ONE packet (p = PPI i + lane / NB, 64 B contiguous at NB = 4), write them to LDS at slot
+// 64 i + lane, and every lane then reads its own packet's NB blocks back.  Outputs go the other way.  The chunk a
+// lane moves is rotated by p / ROT so that the owner's reads (slot(p, k) = 64 (p / PPI) + NB (p % PPI) +
+// ((k + p / ROT) % NB)) hit 16 distinct bank quads per ds_read_b128 lane group (conflict-free).
+template <int NB>
+struct Stage {
+    static constexpr uint32_t PPI = 64 / NB, ROT = 16 / NB;
+    uint32_t base;  // this wave's 64 * NB * 16 byte region
+    uint32_t lane;
+    __device__ __forceinline__ uint32_t own(uint32_t k) const {  // LDS address of my packet's chunk k
+        return base + 16u * (64u * (lane / PPI) + NB * (lane % PPI) + ((k + lane / ROT) % NB));
+    }
+    __device__ __forceinline__ uint32_t coop(int i) const { return base + 16u * (64u * i + lane); }
+    __device__ __forceinline__ uint32_t coop_src(int i) const { return PPI * i + lane / NB; }  // packet lane
+    __device__ __forceinline__ uint32_t coop_chunk(int i) const {
+        const uint32_t p = coop_src(i);
+        return ((lane % NB) + NB - (p / ROT) % NB) % NB;
+    }
+};
+
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
+    return v;
+}
+__device__ __forceinline__ void wave_lds_sync() {
+    // the wave's own LDS traffic is in order; this keeps the compiler from moving LDS accesses across the exchange
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// One packet per lane (has = false: the lane only helps with the wave's cooperative I/O).  Counter blocks are
+// grouped [NB*g, NB*g + NB) with NB | 256, so a group never crosses a 256-block page (CtrPage constants hold for
+// the whole group) and the packet runs through ONE loop body:
 //   counter 0: unused (its keystream is discarded), counter 1: J0 -> E_K(J0) masks the tag,
 //   counter b + 2: data block b.
 // The GHASH steps of group g-1 are issued in the same basic block as the keystream of group g, so the two
 // independent dependency chains overlap.
 template <int NR, int NB, bool SEAL>
-__device__ __forceinline__ void process_packet(const AesLds &aes, const GhashLds &gh, const DevKey *__restrict__ key,
-                                               const qpp_pkt &d, uint32_t pkt_index, uint8_t *arena, uint8_t *masks,
-                                               int8_t *status, uint32_t flags) {
+__device__ __forceinline__ void process_packet(const AesLds &aes, const Ghash &gh, const Stage<NB> &st,
+                                               const DevKey *__restrict__ key, const uint32_t *__restrict__ rk,
+                                               bool has, const qpp_pkt &d, uint32_t pkt_index, uint8_t *arena,
+                                               uint8_t *masks, int8_t *status, uint32_t flags) {
     static_assert(NB >= 2 && (256 % NB) == 0, "NB must divide 256 (and hold counter 1)");
-    const uint32_t *__restrict__ rk = key->rk;
     PacketView p = load_packet(d, key, arena);
+    if (!has) p.len = 0;
     uint8_t *pay = p.base + p.aad_len;
     CtrPage pg;
     pg.build(aes, rk, p.n0, p.n1, p.n2, 0);
-    uint4 z = ghash_aad_z(gh, p.base, p.aad_len);
+    uint4 z = has ? ghash_aad_w(gh, p.base, p.aad_len) : make_uint4(0, 0, 0, 0);  // rotated running value
 
     const int nfull = (int)(p.len >> 4), rem = (int)(p.len & 15);
     const int nblk = nfull + (rem ? 1 : 0);
-    const int ngroups = (nblk + 2 + NB - 1) / NB;
-    uint4 ks[NB], in[NB], cprev[NB], ek0 = make_uint4(0, 0, 0, 0);
-    int bprev = -NB;  // first block index of the previous group (for its GHASH validity)
-    // group 0 inputs: slots 0, 1 are counters 0 and 1 (no data)
+    const int ngroups = has ? (nblk + 2 + NB - 1) / NB : 0;
+    const int G = (int)wave_max((uint32_t)ngroups);  // the wave runs the longest packet's groups
+
+    // cooperative roles: payload offset and length of the packet whose chunk this lane moves in instruction i
+    uint32_t co_off[NB], co_len[NB], co_k[NB];
+    const uint32_t my_off = (uint32_t)(pay - arena);
 #pragma unroll
-    for (int j = 0; j < NB; j++) {
-        const int b = j - 2;
-        in[j] = ld16(b >= 0 && 16 * b <= (int)p.len ? pay + 16 * b : pay);
+    for (int i = 0; i < NB; i++) {
+        co_off[i] = (uint32_t)__shfl((int)my_off, (int)st.coop_src(i), 64);
+        co_len[i] = (uint32_t)__shfl((int)p.len, (int)st.coop_src(i), 64);
+        co_k[i] = st.coop_chunk(i);
     }
-    for (int g = 0; g < ngroups; g++) {
+    // chunk of block b = NB g - 2 + k, clamped inside payload||tag (its value is unused when out of range)
+    auto co_load = [&](int g, uint4 (&v)[NB]) {
+#pragma unroll
+        for (int i = 0; i < NB; i++) {
+            const int b = NB * g - 2 + (int)co_k[i];
+            const bool ok = b >= 0 && 16 * b <= (int)co_len[i];
+            v[i] = ld16(arena + co_off[i] + (ok ? 16u * (uint32_t)b : 0u));
+        }
+    };
+
+    uint4 ks[NB], cin[NB], cprev[NB], ek0 = make_uint4(0, 0, 0, 0);
+    int bprev = -NB;  // first block index of the previous group (for its GHASH validity)
+    co_load(0, cin);
+    for (int g = 0; g < G; g++) {
+        // this group's inputs: coalesced chunks -> LDS -> my packet's blocks
+#pragma unroll
+        for (int i = 0; i < NB; i++) lds_st128(st.coop(i), cin[i]);
+        wave_lds_sync();
+        uint4 in[NB];
+#pragma unroll
+        for (int j = 0; j < NB; j++) in[j] = lds_ld128(st.own(j));
+        co_load(g + 1, cin);  // prefetch the next group (latency hidden by this group's AES)
+
         const uint32_t c = (uint32_t)(NB * g);
         if ((c >> 8) != pg.page) pg.build(aes, rk, p.n0, p.n1, p.n2, c >> 8);
+#ifdef QPP_DIAG_NOAES
+#pragma unroll
+        for (int j = 0; j < NB; j++) ks[j] = make_uint4(c + j, pg.k0, pg.l0, 0);
+#else
         ctr_keystream<NR, NB>(aes, pg, rk, c, ks);
+#endif
         // GHASH of the previous group (independent of the keystream just issued)
 #pragma unroll
         for (int j = 0; j < NB; j++)
+#ifdef QPP_DIAG_NOGHASH
+            if (bprev + j >= 0 && bprev + j < nblk) z = z ^ cprev[j];
+#else
             if (bprev + j >= 0 && bprev + j < nblk) z = gh.mulx(z, cprev[j]);
+#endif
         if (g == 0) ek0 = ks[1];
         const int b0 = NB * g - 2;  // data block of slot 0
 #pragma unroll
         for (int j = 0; j < NB; j++) {
             const int b = b0 + j;
             const uint4 out = in[j] ^ ks[j];
+            lds_st128(st.own(j), out);  // full blocks leave through the cooperative store below
             if (b >= 0 && b < nfull) {
-                st16(pay + 16 * b, out);
                 cprev[j] = SEAL ? out : in[j];
             } else if (b == nfull && rem) {
                 const uint4 o = keep_bytes(out, rem);
@@ -185,19 +293,22 @@ __device__ __forceinline__ void process_packet(const AesLds &aes, const GhashLds
             }
         }
         bprev = b0;
-        // next group's input blocks (clamped inside payload||tag)
+        wave_lds_sync();
 #pragma unroll
-        for (int j = 0; j < NB; j++) {
-            const int b = b0 + NB + j;
-            in[j] = ld16(16 * b <= (int)p.len ? pay + 16 * b : pay);
+        for (int i = 0; i < NB; i++) {
+            const uint4 v = lds_ld128(st.coop(i));
+            const int b = b0 + (int)co_k[i];
+            if (b >= 0 && b < (int)(co_len[i] >> 4)) st16(arena + co_off[i] + 16u * (uint32_t)b, v);
         }
+        wave_lds_sync();  // the next group's staging writes come after these reads
     }
 #pragma unroll
     for (int j = 0; j < NB; j++)
         if (bprev + j >= 0 && bprev + j < nblk) z = gh.mulx(z, cprev[j]);
+    if (!has) return;
     // length block: be64(aad bits) || be64(payload bits); tag = Y * H ^ E_K(J0)
     z = gh.mulx(z, make_uint4(0, bswap32(p.aad_len * 8), 0, bswap32(p.len * 8)));
-    const uint4 tag = gh.mulx(z, ek0);
+    const uint4 tag = gh.prod(z, ek0);
 
     if (SEAL) {
         st16(pay + p.len, tag);
@@ -234,22 +345,27 @@ __global__ __launch_bounds__(WG) void aes_gcm_kernel(const DevKey *__restrict__ 
                                                     const uint32_t *__restrict__ perm, const WorkItem *__restrict__ work,
                                                     const uint32_t *__restrict__ n_work, uint8_t *__restrict__ arena,
                                                     uint8_t *masks, int8_t *status, uint32_t flags) {
-#ifdef QPP_STATIC_LDS
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
-#else
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];  // measured faster than static (seal), see DESIGN
-#endif
+    // dynamic LDS (tables + this variant's staging, reserved by the launch), addressed by offset (lds_ld32 / lds_ld128)
     if (blockIdx.x >= *n_work) return;  // uniform: grid is sized for the worst case
     const WorkItem w = work[blockIdx.x];
     if (w.nr != NR) return;  // AES-128 and AES-256 work items are served by separate launches (SGPR budget)
     const DevKey *__restrict__ key = keys + w.key;
-    build_tables(lds, key);
-    const AesLds aes = make_aes(lds);
-    const GhashLds gh{lds};
-    for (uint32_t t = threadIdx.x; t < w.count; t += WG) {  // WG < 1024: several passes over the work item
-        const uint32_t pi = perm[w.begin + t];
-        const qpp_pkt d = descs[pi];
-        process_packet<NR, NB, SEAL>(aes, gh, key, d, pi, arena, masks, status, flags);
+    build_tables(key);
+    const AesLds aes = make_aes(kLdsAes);
+    const Ghash gh = Ghash::make();
+    // packet round keys in SGPRs for the whole work item (uniform: one key per workgroup)
+    uint32_t rk[4 * (NR + 1)];
+#pragma unroll
+    for (int i = 0; i < 4 * (NR + 1); i++) rk[i] = __builtin_amdgcn_readfirstlane(key->rk[i]);
+    Stage<NB> st;
+    st.lane = threadIdx.x & 63u;
+    st.base = kLdsStage + (threadIdx.x >> 6) * (64u * 16u * NB);
+    for (uint32_t t0 = 0; t0 < w.count; t0 += WG) {  // WG < 1024: several passes over the work item
+        const uint32_t t = t0 + threadIdx.x;
+        const bool has = t < w.count;
+        const uint32_t pi = has ? perm[w.begin + t] : 0;
+        const qpp_pkt d = descs[pi];  // (any valid descriptor for helper lanes)
+        process_packet<NR, NB, SEAL>(aes, gh, st, key, rk, has, d, pi, arena, masks, status, flags);
     }
 }
 
@@ -307,31 +423,28 @@ hipError_t launch_key_setup(DevKey *keys, uint32_t first, uint32_t count, hipStr
 }
 
 namespace {
-#ifdef QPP_STATIC_LDS
-constexpr uint32_t kDynLds = 0;
-#else
-constexpr uint32_t kDynLds = kLdsBytes;
-#endif
 // (blocks per lane-iteration NB, workgroup size WG, packets per work item PER) variants; QPP_AES_VARIANT=<index>
-// selects one (tuning knob).  One workgroup per CU (130 KiB LDS), so WG = waves per CU x 64.
+// selects one (tuning knob).  One workgroup per CU (tables + staging fill the 160 KiB LDS), so
+// WG = waves per CU x 64.
 struct Variant {
     int nb, wg, per;
 };
-constexpr Variant kVariants[] = {{4, 512, 1024}, {8, 512, 1024}, {2, 1024, 1024}, {4, 512, 512}, {2, 512, 1024}};
+constexpr Variant kVariants[] = {{4, 512, 1024}, {2, 1024, 1024}, {2, 512, 1024}, {4, 256, 1024}};
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
+constexpr uint32_t lds_bytes(int nb, int wg) { return kLdsStage + (uint32_t)(wg / 64) * 1024u * (uint32_t)nb; }
 
 template <bool SEAL, int NR>
 void launch_variant(int v, dim3 grid, hipStream_t s, const DevKey *keys, const qpp_pkt *descs, const PlanBuffers &pb,
                     uint8_t *arena, uint8_t *masks, int8_t *status, uint32_t flags) {
 #define QPP_AES_LAUNCH(NB, WG)                                                                                    \
-    hipLaunchKernelGGL((aes_gcm_kernel<SEAL, NB, WG, NR>), grid, dim3(WG), kDynLds, s, keys, descs, pb.perm,     \
-                       pb.work, pb.n_work, arena, masks, status, flags)
+    static_assert(lds_bytes(NB, WG) <= kLdsMax, "LDS budget");                                                 \
+    hipLaunchKernelGGL((aes_gcm_kernel<SEAL, NB, WG, NR>), grid, dim3(WG), lds_bytes(NB, WG), s, keys, descs,   \
+                       pb.perm, pb.work, pb.n_work, arena, masks, status, flags)
     switch (v) {
-        case 0: QPP_AES_LAUNCH(4, 512); break;
-        case 1: QPP_AES_LAUNCH(8, 512); break;
-        case 2: QPP_AES_LAUNCH(2, 1024); break;
-        case 3: QPP_AES_LAUNCH(4, 512); break;
-        default: QPP_AES_LAUNCH(2, 512); break;
+        case 1: { QPP_AES_LAUNCH(2, 1024); break; }
+        case 2: { QPP_AES_LAUNCH(2, 512); break; }
+        case 3: { QPP_AES_LAUNCH(4, 256); break; }
+        default: { QPP_AES_LAUNCH(4, 512); break; }
     }
 #undef QPP_AES_LAUNCH
 }

@@ -235,8 +235,8 @@ __global__ __launch_bounds__(256) void chacha_kernel(const DevKey *__restrict__ 
 // lane's own round keys.  Sample at off + aad_len - pn_len + 4.
 __global__ __launch_bounds__(1024) void hp_mask_kernel(const DevKey *__restrict__ keys, const qpp_pkt *__restrict__ descs,
                                                       uint32_t n, const uint8_t *__restrict__ arena, uint8_t *masks) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsAes + 65536];
-    build_aes_tables(lds);
+    // 64 KiB of dynamic LDS (the launch reserves it), addressed by offset through lds_ld32/lds_st32
+    build_aes_tables(0);
     __syncthreads();
     const uint32_t pi = blockIdx.x * blockDim.x + threadIdx.x;
     if (pi >= n) return;
@@ -250,7 +250,7 @@ __global__ __launch_bounds__(1024) void hp_mask_kernel(const DevKey *__restrict_
         for (int i = 0; i < 8; i++) hk[i] = key->hp_rk[i];
         m0 = chacha_hp_word(hk, smp, &m1);
     } else {
-        const AesLds aes = make_aes(lds);
+        const AesLds aes = make_aes(0);
         uint4 m = key->hp_nr == 10 ? aes.encrypt<10>(smp, key->hp_rk) : aes.encrypt<14>(smp, key->hp_rk);
         m0 = m.x; m1 = m.y;
     }
@@ -274,7 +274,7 @@ hipError_t launch_chacha(bool seal, const DevKey *keys, const qpp_pkt *descs, ui
 hipError_t launch_hp_mask(const DevKey *keys, const qpp_pkt *descs, uint32_t n, const uint8_t *arena, uint8_t *masks,
                           hipStream_t s) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(hp_mask_kernel, dim3((n + 1023) / 1024), dim3(1024), 0, s, keys, descs, n,
+    hipLaunchKernelGGL(hp_mask_kernel, dim3((n + 1023) / 1024), dim3(1024), 65536, s, keys, descs, n,
                        arena, masks);
     return hipGetLastError();
 }

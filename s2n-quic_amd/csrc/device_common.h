@@ -8,8 +8,28 @@ namespace dev {
 
 constexpr uint32_t kLdsGhash = 0;
 constexpr uint32_t kLdsAes = 65536;
-constexpr uint32_t kLdsV = 131072;
-constexpr uint32_t kLdsBytes = kLdsV + 128 * 16;
+constexpr uint32_t kLdsV = 131072;      // GHASH key powers, only while the tables are built
+constexpr uint32_t kLdsStage = 131072;  // per-wave payload staging (aes_gcm.hip Stage), after the build
+constexpr uint32_t kLdsMax = 163840;    // 160 KiB per workgroup
+
+// LDS is addressed by plain 32-bit offsets into the workgroup's allocation.  Every kernel that uses these
+// helpers declares exactly one LDS array (which therefore starts at offset 0) and touches LDS only through
+// them, so there is no base-symbol add per access (with `lds + off` hipcc emitted a `v_add_u32 v, 0, v` per
+// table lookup: a quarter of the AES round's VALU work).
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) u32x4 lds_u128;
+__device__ __forceinline__ uint32_t lds_ld32(uint32_t a) { return *(const lds_u32 *)(size_t)a; }
+__device__ __forceinline__ uint4 lds_ld128(uint32_t a) {
+    const u32x4 v = *(const lds_u128 *)(size_t)a;
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void lds_st32(uint32_t a, uint32_t v) { *(lds_u32 *)(size_t)a = v; }
+__device__ __forceinline__ void lds_st128(uint32_t a, uint4 v) {
+    u32x4 t;
+    t.x = v.x; t.y = v.y; t.z = v.z; t.w = v.w;
+    *(lds_u128 *)(size_t)a = t;
+}
 
 static __device__ const uint8_t d_sbox[256] = {
 #define S(i) kSBox.v[i]
@@ -62,8 +82,7 @@ __device__ __forceinline__ uint4 xor3(uint4 a, uint4 b, uint4 c) {
 // Column c of a round: T0[s_c.b0] ^ T1[s_c+1.b1] ^ T2[s_c+2.b2] ^ T3[s_c+3.b3] ^ rk, with T2 = rotl16(T0) and
 // T3 = rotl16(T1), so only T0/T1 are stored (64 KiB replicated); per column: 4 lookups + 4 VALU.
 struct AesLds {
-    const uint8_t *lds;
-    uint32_t laneword;  // byte0 = 4 * (lane % 32), byte2 = 0x01 (64 KiB table base)
+    uint32_t laneword;  // byte0 = 4 * (lane % 32), byte2 = table base >> 16
 
     // address of T0[byte K of w] (T1 is at +128): ONE v_perm_b32
     template <int K>
@@ -72,9 +91,9 @@ struct AesLds {
         return __builtin_amdgcn_perm(w, laneword, (0x0cu << 24) | (2u << 16) | ((4u + K) << 8) | 0u);
     }
     template <int K>
-    __device__ __forceinline__ uint32_t t0(uint32_t w) const { return *(const uint32_t *)(lds + addr<K>(w)); }
+    __device__ __forceinline__ uint32_t t0(uint32_t w) const { return lds_ld32(addr<K>(w)); }
     template <int K>
-    __device__ __forceinline__ uint32_t t1(uint32_t w) const { return *(const uint32_t *)(lds + addr<K>(w) + 128); }
+    __device__ __forceinline__ uint32_t t1(uint32_t w) const { return lds_ld32(addr<K>(w) + 128); }
 
     __device__ __forceinline__ uint32_t col(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t k) const {
         return xor3(t0<0>(a), t1<1>(b), k) ^ rotl16(t0<2>(c) ^ t1<3>(d));
@@ -159,17 +178,18 @@ __device__ __forceinline__ void ctr_keystream(const AesLds &a, const CtrPage &pg
 
 // AES T0/T1 bank-replicated tables for the AesLds view: dword d -> row x = d >> 6, slot = d & 63
 // (slots 32..63 hold T1 = rotl8 T0).  No barrier inside.
-__device__ __forceinline__ void build_aes_tables(uint8_t *lds) {
+// base: LDS offset of the 64 KiB table region (a multiple of 64 KiB).
+__device__ __forceinline__ void build_aes_tables(uint32_t base) {
     for (uint32_t d = threadIdx.x; d < 16384; d += blockDim.x) {
         uint32_t x = d >> 6, slot = d & 63;
         uint32_t s = d_sbox[x], s2 = xtime4(s);
         uint32_t t0 = s2 | (s << 8) | (s << 16) | ((s2 ^ s) << 24);
-        *(uint32_t *)(lds + kLdsAes + 4 * d) = slot < 32 ? t0 : __builtin_amdgcn_alignbit(t0, t0, 24);
+        lds_st32(base + 4 * d, slot < 32 ? t0 : __builtin_amdgcn_alignbit(t0, t0, 24));
     }
 }
 
-__device__ __forceinline__ AesLds make_aes(const uint8_t *lds) {
-    return AesLds{lds, ((threadIdx.x & 31u) << 2) | (1u << 16)};
+__device__ __forceinline__ AesLds make_aes(uint32_t base) {
+    return AesLds{((threadIdx.x & 31u) << 2) | base};
 }
 
 }  // namespace dev

@@ -125,9 +125,11 @@ typedef struct qpp_pkt {
     uint16_t aad_len;  /* header length including the packet-number bytes */
     uint16_t pt_len;   /* payload length, tag excluded */
     uint8_t pn_len;    /* 1..4 packet-number bytes (header protection) */
-    uint8_t flags;     /* reserved, 0 */
+    uint8_t flags;     /* 0, or QPP_PKT_SKIP */
     uint16_t reserved;
 } qpp_pkt;             /* 24 bytes */
+
+#define QPP_PKT_SKIP 0x1u     /* qpp_pkt.flags: the kernels leave this packet (and its status) untouched */
 
 /* Batch flags */
 #define QPP_HP_MASK_OUT 0x1u   /* write the 5-byte HP mask of packet i to masks[5*i] */

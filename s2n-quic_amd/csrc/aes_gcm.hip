@@ -168,42 +168,6 @@ __device__ __forceinline__ uint4 ghash_aad_w(const Ghash &gh, const uint8_t *aad
     return w;
 }
 
-// Coalesced payload I/O through a per-wave LDS staging area.  A lane-per-packet load touches 64 scattered lines
-// per wave instruction (packets are ~1.2 KB apart) and thrashes L1 (measured: with the payload I/O confined to an
-// L1-resident window the seal ran 1.9 -> 1.5 ms at NB = 4, and 3.1 -> 1.2 ms at NB = 2 / 1024 threads).  So each
-// group's NB x 16 B per packet is moved cooperatively: in wave instruction i, the NB lanes of a lane-group of NB
-// load the NB chunks of ONE packet (p = PPI i + lane / NB, 64 B contiguous at NB = 4), write them to LDS at slot
-// 64 i + lane, and every lane then reads its own packet's NB blocks back.  Outputs go the other way.  The chunk a
-// lane moves is rotated by p / ROT so that the owner's reads (slot(p, k) = 64 (p / PPI) + NB (p % PPI) +
-// ((k + p / ROT) % NB)) hit 16 distinct bank quads per ds_read_b128 lane group (conflict-free).
-template <int NB>
-struct Stage {
-    static constexpr uint32_t PPI = 64 / NB, ROT = 16 / NB;
-    uint32_t base;  // this wave's 64 * NB * 16 byte region
-    uint32_t lane;
-    __device__ __forceinline__ uint32_t own(uint32_t k) const {  // LDS address of my packet's chunk k
-        return base + 16u * (64u * (lane / PPI) + NB * (lane % PPI) + ((k + lane / ROT) % NB));
-    }
-    __device__ __forceinline__ uint32_t coop(int i) const { return base + 16u * (64u * i + lane); }
-    __device__ __forceinline__ uint32_t coop_src(int i) const { return PPI * i + lane / NB; }  // packet lane
-    __device__ __forceinline__ uint32_t coop_chunk(int i) const {
-        const uint32_t p = coop_src(i);
-        return ((lane % NB) + NB - (p / ROT) % NB) % NB;
-    }
-};
-
-__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
-    return v;
-}
-__device__ __forceinline__ void wave_lds_sync() {
-    // the wave's own LDS traffic is in order; this keeps the compiler from moving LDS accesses across the exchange
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
 // One packet per lane (has = false: the lane only helps with the wave's cooperative I/O).  Counter blocks are
 // grouped [NB*g, NB*g + NB) with NB | 256, so a group never crosses a 256-block page (CtrPage constants hold for
 // the whole group) and the packet runs through ONE loop body:
@@ -332,7 +296,8 @@ __device__ __forceinline__ void process_packet(const AesLds &aes, const Ghash &g
         const uint4 diff = tag ^ want;
         const bool ok = (diff.x | diff.y | diff.z | diff.w) == 0;  // all 16 bytes compared, no early exit
         if (!ok) {
-            // never release unauthenticated plaintext
+            // never release unauthenticated plaintext (other lanes stored it: order these stores after theirs)
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             for (int b = 0; b < nfull; b++) st16(pay + 16 * b, make_uint4(0, 0, 0, 0));
             if (rem) st_bytes(pay + 16 * nfull, make_uint4(0, 0, 0, 0), rem);
         }
@@ -362,9 +327,10 @@ __global__ __launch_bounds__(WG) void aes_gcm_kernel(const DevKey *__restrict__ 
     st.base = kLdsStage + (threadIdx.x >> 6) * (64u * 16u * NB);
     for (uint32_t t0 = 0; t0 < w.count; t0 += WG) {  // WG < 1024: several passes over the work item
         const uint32_t t = t0 + threadIdx.x;
-        const bool has = t < w.count;
-        const uint32_t pi = has ? perm[w.begin + t] : 0;
+        const bool real = t < w.count;
+        const uint32_t pi = real ? perm[w.begin + t] : 0;
         const qpp_pkt d = descs[pi];  // (any valid descriptor for helper lanes)
+        const bool has = real && !(d.flags & QPP_PKT_SKIP);
         process_packet<NR, NB, SEAL>(aes, gh, st, key, rk, has, d, pi, arena, masks, status, flags);
     }
 }

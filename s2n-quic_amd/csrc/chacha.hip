@@ -125,24 +125,29 @@ __device__ __forceinline__ void apply_mask(uint8_t *base, uint32_t hdr_len, uint
     }
 }
 
-// One lane per packet, software-pipelined over 64-byte chunks: the keystream of chunk g+1 is computed in the same
-// basic block as the Poly1305 steps of chunk g (independent chains), and chunk g+1's input is loaded one chunk ahead.
+// One lane per packet, software-pipelined over 64-byte chunks: the keystream of chunk c+1 is computed in the same
+// basic block as the Poly1305 steps of chunk c (independent chains).  The payload moves through the per-wave LDS
+// staging (Stage<4>, device_common.h): each wave instruction loads/stores 16 packets x 64 contiguous bytes instead
+// of 64 scattered 16-byte pieces, and chunk c+1's input is loaded one chunk ahead.
 template <bool SEAL>
 __global__ __launch_bounds__(256) void chacha_kernel(const DevKey *__restrict__ keys, const qpp_pkt *__restrict__ descs,
                                                     uint32_t n, uint8_t *__restrict__ arena, uint8_t *masks,
                                                     int8_t *status, uint32_t flags) {
     const uint32_t pi = blockIdx.x * blockDim.x + threadIdx.x;
-    if (pi >= n) return;
-    const qpp_pkt d = descs[pi];
+    const qpp_pkt d = descs[pi < n ? pi : n - 1];  // (any valid descriptor for helper lanes)
     const DevKey *__restrict__ key = keys + d.key_idx;
-    if (key->suite != QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256) return;  // AES packets: aes_gcm_kernel
+    const bool has = pi < n && key->suite == QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256 && !(d.flags & QPP_PKT_SKIP);
+    if (!__any(has)) return;  // wave-uniform: AES packets go to aes_gcm_kernel
+    Stage<4> st;
+    st.lane = threadIdx.x & 63u;
+    st.base = (threadIdx.x >> 6) * (64u * 16u * 4u);
     uint32_t k[8];
 #pragma unroll
     for (int i = 0; i < 8; i++) k[i] = key->rk[i];
     // Iv::nonce (src/iv.rs:27-39)
     const uint32_t n0 = key->iv[0], n1 = key->iv[1] ^ bswap32((uint32_t)(d.pn >> 32)), n2 = key->iv[2] ^ bswap32((uint32_t)d.pn);
     uint8_t *base = arena + d.off;
-    const uint32_t aad_len = d.aad_len, len = d.pt_len;
+    const uint32_t aad_len = d.aad_len, len = has ? d.pt_len : 0;
     uint8_t *pay = base + aad_len;
 
     uint32_t ks[16];
@@ -150,66 +155,82 @@ __global__ __launch_bounds__(256) void chacha_kernel(const DevKey *__restrict__ 
     Poly1305 mac;
     mac.init(ks[0], ks[1], ks[2], ks[3]);
     const uint32_t sw0 = ks[4], sw1 = ks[5], sw2 = ks[6], sw3 = ks[7];
-    for (uint32_t off = 0; off < aad_len; off += 16) {
-        uint4 a = ld16(base + off);
-        if (aad_len - off < 16) a = keep_bytes(a, aad_len - off);
-        mac.block(a);
+    if (has)
+        for (uint32_t off = 0; off < aad_len; off += 16) {
+            uint4 a = ld16(base + off);
+            if (aad_len - off < 16) a = keep_bytes(a, aad_len - off);
+            mac.block(a);
+        }
+    // cooperative roles: payload offset / length of the packet whose chunk this lane moves in instruction i
+    const uint32_t nch = (len + 63) / 64;  // chunks, the partial tail included
+    const uint32_t C = wave_max(nch);
+    uint32_t co_off[4], co_len[4], co_k[4];
+    const uint32_t my_off = (uint32_t)(pay - arena);
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        co_off[i] = (uint32_t)__shfl((int)my_off, (int)st.coop_src(i), 64);
+        co_len[i] = (uint32_t)__shfl((int)len, (int)st.coop_src(i), 64);
+        co_k[i] = st.coop_chunk(i);
     }
-    // inputs of chunk c (4 blocks, each clamped inside payload||tag)
-    auto load_chunk = [&](uint32_t c, uint4 (&in)[4]) {
+    // block b = 4 c + k of the lane's assigned packet, clamped inside payload||tag (unused when out of range)
+    auto co_load = [&](uint32_t c, uint4 (&v)[4]) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const uint32_t o = 16u * (4u * c + co_k[i]);
+            v[i] = ld16(arena + co_off[i] + (o < co_len[i] ? o : 0u));
+        }
+    };
+    uint4 cin[4], cb[4];
+    co_load(0, cin);
+    chacha_block(k, 1, n0, n1, n2, ks);
+    for (uint32_t c = 0; c < C; c++) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) lds_st128(st.coop(i), cin[i]);
+        wave_lds_sync();
+        uint4 in[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) in[q] = lds_ld128(st.own(q));
+        co_load(c + 1, cin);
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             const uint32_t o = 64 * c + 16 * q;
-            in[q] = ld16(o <= len ? pay + o : pay);
-        }
-    };
-    const uint32_t nchunks = len / 64;  // full 64-byte chunks
-    uint4 in[4], cb[4];
-    load_chunk(0, in);
-    chacha_block(k, 1, n0, n1, n2, ks);
-    for (uint32_t c = 0; c < nchunks; c++) {
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const uint4 out = in[q] ^ make_uint4(ks[4 * q], ks[4 * q + 1], ks[4 * q + 2], ks[4 * q + 3]);
-            st16(pay + 64 * c + 16 * q, out);
-            cb[q] = SEAL ? out : in[q];
-        }
-        load_chunk(c + 1, in);
-        chacha_block(k, c + 2, n0, n1, n2, ks);  // next chunk (or the tail) ...
-#pragma unroll
-        for (int q = 0; q < 4; q++) mac.block(cb[q]);  // ... beside this chunk's MAC
-    }
-    // tail: < 64 bytes, keystream already in ks[]
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-        const uint32_t o = 64 * nchunks + 16 * q;
-        if (o < len) {
             uint4 out = in[q] ^ make_uint4(ks[4 * q], ks[4 * q + 1], ks[4 * q + 2], ks[4 * q + 3]);
-            const uint32_t r = len - o;
-            uint4 c;
-            if (r >= 16) {
-                st16(pay + o, out);
-                c = SEAL ? out : in[q];
-            } else {
+            lds_st128(st.own(q), out);  // full blocks leave through the cooperative store
+            cb[q] = SEAL ? out : in[q];
+            if (o < len && len - o < 16) {  // the partial last block: this lane stores its bytes
+                const uint32_t r = len - o;
                 out = keep_bytes(out, r);
                 st_bytes(pay + o, out, r);
-                c = SEAL ? out : keep_bytes(in[q], r);
+                cb[q] = SEAL ? out : keep_bytes(in[q], r);
             }
-            mac.block(c);
         }
+        wave_lds_sync();
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const uint4 v = lds_ld128(st.coop(i));
+            const uint32_t o = 16u * (4u * c + co_k[i]);
+            if (o + 16 <= co_len[i]) st16(arena + co_off[i] + o, v);
+        }
+        wave_lds_sync();
+        chacha_block(k, c + 2, n0, n1, n2, ks);  // next chunk ...
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            if (64 * c + 16 * q < len) mac.block(cb[q]);  // ... beside this chunk's MAC
     }
+    if (!has) return;
     mac.block(make_uint4(aad_len, 0, len, 0));  // le64(aad_len) || le64(ct_len)
     const uint4 tag = mac.finish(sw0, sw1, sw2, sw3);
 
     if (SEAL) {
         st16(pay + len, tag);
-        int8_t st = QPP_OK;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // other lanes stored this packet's ciphertext
+        int8_t st8 = QPP_OK;
         if (flags & (QPP_HP_MASK_OUT | QPP_HP_APPLY)) {
             const uint32_t s = 4 - d.pn_len;
             if (d.pn_len < 1 || d.pn_len > 4 || len < s) {
-                st = QPP_DECODE_ERROR;
+                st8 = QPP_DECODE_ERROR;
             } else {
-                const uint4 smp = ld16(pay + s);  // this lane's own ciphertext||tag bytes
+                const uint4 smp = ld16(pay + s);
                 uint32_t hk[8];
 #pragma unroll
                 for (int i = 0; i < 8; i++) hk[i] = key->hp_rk[i];
@@ -217,11 +238,12 @@ __global__ __launch_bounds__(256) void chacha_kernel(const DevKey *__restrict__ 
                 apply_mask(base, aad_len - d.pn_len, d.pn_len, m0, m1, masks + 5 * (size_t)pi, flags);
             }
         }
-        if (status) status[pi] = st;
+        if (status) status[pi] = st8;
     } else {
         const uint4 diff = tag ^ ld16(pay + len);
         const bool ok = (diff.x | diff.y | diff.z | diff.w) == 0;
         if (!ok) {
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             for (uint32_t o = 0; o < len; o += 16) {
                 if (len - o >= 16) st16(pay + o, make_uint4(0, 0, 0, 0));
                 else st_bytes(pay + o, make_uint4(0, 0, 0, 0), len - o);
@@ -264,10 +286,11 @@ hipError_t launch_chacha(bool seal, const DevKey *keys, const qpp_pkt *descs, ui
                          uint8_t *masks, int8_t *status, uint32_t flags, hipStream_t s) {
     if (!n) return hipSuccess;
     const dim3 grid((n + 255) / 256), block(256);
+    const uint32_t lds = 4u * 64u * 16u * 4u;  // Stage<4> per wave, 4 waves
     if (seal)
-        hipLaunchKernelGGL(chacha_kernel<true>, grid, block, 0, s, keys, descs, n, arena, masks, status, flags);
+        hipLaunchKernelGGL(chacha_kernel<true>, grid, block, lds, s, keys, descs, n, arena, masks, status, flags);
     else
-        hipLaunchKernelGGL(chacha_kernel<false>, grid, block, 0, s, keys, descs, n, arena, masks, status, flags);
+        hipLaunchKernelGGL(chacha_kernel<false>, grid, block, lds, s, keys, descs, n, arena, masks, status, flags);
     return hipGetLastError();
 }
 

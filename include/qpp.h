@@ -150,6 +150,35 @@ int qpp_open_batch(qpp_ctx *ctx, const qpp_pkt *descs, size_t n, uint8_t *arena,
 int qpp_hp_mask_batch(qpp_ctx *ctx, const qpp_pkt *descs, size_t n, const uint8_t *arena, uint8_t *masks,
                       void *stream);
 
+/* ------------------------------------------------------------------ receive path */
+
+/* One received, still protected packet of a GRO batch. */
+typedef struct qpp_rx_pkt {
+    uint64_t largest_pn;  /* largest acknowledged PN of the packet-number space (PacketNumber::as_u64) */
+    uint32_t key_idx[2];  /* KeySet crypto[0] / crypto[1] slots: the key-phase bit of a short header picks one
+                             (crypto/application/keyset.rs:113-143); long headers use key_idx[0].  The header key
+                             is key_idx[0]'s (header keys are not updated, RFC 9001 §6). */
+    uint32_t off;         /* first byte of the packet in the arena */
+    uint16_t header_len;  /* bytes before the packet-number field (tag byte || DCID for a short header) */
+    uint16_t len;         /* bytes of the whole packet: header || PN || payload || tag */
+} qpp_rx_pkt;             /* 24 bytes */
+
+/* Receive side of crypto::{unprotect, decrypt} for n packets, on the device: sample at header_len + 4
+ * (payload.rs:151-169) -> mask -> remove_header_protection in place (header_crypto.rs:98-123: pn_len from the
+ * unmasked first byte) -> expand the packet number against largest_pn (packet/number/mod.rs:191-238) -> choose the
+ * key by the key phase -> open in place.  descs_out[i] receives the resulting qpp_pkt (pn = expanded packet number,
+ * key_idx = chosen slot, aad_len = header_len + pn_len, pt_len, pn_len; flags = QPP_PKT_SKIP when rejected);
+ * status[i] = QPP_OK, QPP_DECODE_ERROR (no room for the sample, short.rs / payload.rs) or QPP_DECRYPT_ERROR.
+ * rx, descs_out, arena and status are device pointers.  Asynchronous. */
+int qpp_unprotect_open_batch(qpp_ctx *ctx, const qpp_rx_pkt *rx, size_t n, uint8_t *arena, qpp_pkt *descs_out,
+                             int8_t *status, uint32_t flags, void *stream);
+
+/* PacketNumber::truncate (packet/number/packet_number.rs:135-143, mod.rs:81-93): the 1..4-byte encoding of pn
+ * relative to the largest acknowledged PN.  QPP_DECODE_ERROR when pn < largest_acked or the distance needs > 4 bytes. */
+int qpp_pn_truncate(uint64_t pn, uint64_t largest_acked, uint64_t *truncated, size_t *pn_len);
+/* TruncatedPacketNumber::expand (packet/number/mod.rs:191-238, RFC 9000 A.3), clamped to 2^62 - 1. */
+uint64_t qpp_pn_expand(uint64_t largest_acked, uint64_t truncated, size_t pn_len);
+
 /* ------------------------------------------------------------------ device plumbing */
 
 int qpp_dev_alloc(qpp_ctx *ctx, size_t bytes, void **out);

@@ -590,3 +590,77 @@ void orc_open_batch(const orc_key *keys, const orc_pkt *pkts, size_t n, uint8_t 
                                      (size_t)p->pt_len + 16);
     }
 }
+
+/* ---- packet numbers ---- */
+uint64_t orc_decode_packet_number(uint64_t largest_pn, uint64_t truncated_pn, unsigned pn_nbits) {
+    /* tests.rs:141-158, the `catch!` blocks: a checked sub/add that overflows makes its condition false */
+    const uint64_t expected_pn = largest_pn + 1;
+    const uint64_t pn_win = (uint64_t)1 << pn_nbits;
+    const uint64_t pn_hwin = pn_win / 2;
+    const uint64_t pn_mask = pn_win - 1;
+    const uint64_t candidate_pn = (expected_pn & ~pn_mask) | truncated_pn;
+    const uint64_t limit62 = (uint64_t)1 << 62, varint_max = limit62 - 1;
+    uint64_t r = candidate_pn;
+    if (expected_pn >= pn_hwin && candidate_pn <= expected_pn - pn_hwin && limit62 >= pn_win &&
+        candidate_pn < limit62 - pn_win)
+        r = candidate_pn + pn_win;
+    else if (expected_pn <= UINT64_MAX - pn_hwin && candidate_pn > expected_pn + pn_hwin && candidate_pn >= pn_win)
+        r = candidate_pn - pn_win;
+    return r < varint_max ? r : varint_max;
+}
+
+int orc_truncate_packet_number(uint64_t pn, uint64_t largest_pn, uint64_t *truncated, size_t *pn_len) {
+    if (pn < largest_pn) return ORC_DECODE_ERROR;
+    const uint64_t d = pn - largest_pn;
+    if (d > (UINT64_MAX >> 1)) return ORC_DECODE_ERROR;
+    const uint64_t range = d * 2;
+    size_t len;
+    if (range <= 0xff) len = 1;
+    else if (range <= 0xffff) len = 2;
+    else if (range <= 0xffffff) len = 3;
+    else if (range <= 0xffffffffull) len = 4;
+    else return ORC_DECODE_ERROR;
+    *pn_len = len;
+    *truncated = pn & ((len == 4) ? 0xffffffffull : (((uint64_t)1 << (8 * len)) - 1));
+    return ORC_OK;
+}
+
+void orc_unprotect_open_batch(const orc_key *keys, const orc_rx_pkt *rx, size_t n, uint8_t *arena, orc_pkt *out,
+                              int8_t *status) {
+    for (size_t i = 0; i < n; i++) {
+        const orc_rx_pkt *r = &rx[i];
+        uint8_t *pkt = arena + r->off;
+        orc_pkt *d = &out[i];
+        memset(d, 0, sizeof *d);
+        d->off = r->off;
+        d->key_idx = r->key_idx[0];
+        d->aad_len = r->header_len;
+        /* payload.rs:151-169: the sample must fit */
+        if ((size_t)r->header_len + 4 + 16 > r->len) {
+            d->flags = 1;
+            status[i] = ORC_DECODE_ERROR;
+            continue;
+        }
+        const orc_key *hk = &keys[r->key_idx[0]];
+        uint8_t mask[5];
+        orc_hp_mask(hk->suite, hk->hp, pkt + r->header_len + 4, mask);
+        pkt[0] ^= (uint8_t)(mask[0] & ((pkt[0] & 0x80) ? 0x0f : 0x1f));
+        const size_t pn_len = (size_t)(pkt[0] & 3) + 1;
+        uint64_t trunc = 0;
+        for (size_t j = 0; j < pn_len; j++) {
+            pkt[r->header_len + j] ^= mask[1 + j];
+            trunc = (trunc << 8) | pkt[r->header_len + j];
+        }
+        const uint64_t pn = orc_decode_packet_number(r->largest_pn & (((uint64_t)1 << 62) - 1), trunc, (unsigned)(8 * pn_len));
+        const int phase = (pkt[0] & 0x80) ? 0 : ((pkt[0] >> 2) & 1); /* key_phase.rs:46-49 */
+        const orc_key *k = &keys[r->key_idx[phase]];
+        d->pn = pn;
+        d->key_idx = r->key_idx[phase];
+        d->aad_len = (uint16_t)(r->header_len + pn_len);
+        d->pt_len = (uint16_t)(r->len - r->header_len - pn_len - 16);
+        d->pn_len = (uint8_t)pn_len;
+        uint8_t nonce[12];
+        orc_nonce(k->iv, pn, nonce);
+        status[i] = (int8_t)orc_open(k->suite, k->key, nonce, pkt, d->aad_len, pkt + d->aad_len, (size_t)d->pt_len + 16);
+    }
+}

@@ -122,6 +122,27 @@ void orc_seal_batch(const orc_key *keys, const orc_pkt *pkts, size_t n, uint8_t 
                     uint8_t *masks, int flags);
 void orc_open_batch(const orc_key *keys, const orc_pkt *pkts, size_t n, uint8_t *arena, int8_t *status);
 
+/* ---- packet numbers (quic/s2n-quic-core/src/packet/number) ---- */
+/* RFC 9000 A.3 DecodePacketNumber, as rfc_decoder in packet/number/tests.rs:108-159 states it, clamped to
+ * VarInt::MAX (tests.rs:189-194; mod.rs:235). */
+uint64_t orc_decode_packet_number(uint64_t largest_pn, uint64_t truncated_pn, unsigned pn_nbits);
+/* PacketNumber::truncate (packet_number.rs:135-143, mod.rs:81-93, packet_number_len.rs:163-172).
+ * Returns ORC_DECODE_ERROR when pn < largest or the range needs more than 4 bytes. */
+int orc_truncate_packet_number(uint64_t pn, uint64_t largest_pn, uint64_t *truncated, size_t *pn_len);
+
+/* ---- receive batch (mirrors qpp_unprotect_open_batch; qpp_rx_pkt layout) ---- */
+typedef struct orc_rx_pkt {
+    uint64_t largest_pn;
+    uint32_t key_idx[2];
+    uint32_t off;
+    uint16_t header_len;
+    uint16_t len;
+} orc_rx_pkt;
+/* per packet: crypto::unprotect (mod.rs:195-204) -> TruncatedPacketNumber::expand -> key by key phase
+ * (keyset.rs:113-143) -> crypto::decrypt (mod.rs:251-264); out[i] / status[i] as the ABI documents */
+void orc_unprotect_open_batch(const orc_key *keys, const orc_rx_pkt *rx, size_t n, uint8_t *arena, orc_pkt *out,
+                              int8_t *status);
+
 #ifdef __cplusplus
 }
 #endif

@@ -501,6 +501,42 @@ int qpp_open_batch(qpp_ctx *ctx, const qpp_pkt *descs, size_t n, uint8_t *arena,
     return QPP_OK;
 }
 
+int qpp_unprotect_open_batch(qpp_ctx *ctx, const qpp_rx_pkt *rx, size_t n, uint8_t *arena, qpp_pkt *descs_out,
+                             int8_t *status, uint32_t flags, void *stream) {
+    if (!ctx || (n && (!rx || !arena || !descs_out || !status))) return QPP_INTERNAL_ERROR;
+    if (n > UINT32_MAX) return QPP_INTERNAL_ERROR;
+    if (!n) return QPP_OK;
+    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    int rc = flush_keys(ctx, s);
+    if (rc) return rc;
+    // 1. header unprotection + PN expansion + key-phase choice -> descs_out (device); 2. the open kernels on them,
+    // grouped by the chosen key like any batch (skipped packets keep their DECODE_ERROR status)
+    HIP_TRY(ctx, launch_unprotect(ctx->d_keys, rx, (uint32_t)n, arena, descs_out, status, s));
+    return qpp_open_batch(ctx, descs_out, n, arena, status, flags, s);
+}
+
+int qpp_pn_truncate(uint64_t pn, uint64_t largest_acked, uint64_t *truncated, size_t *pn_len) {
+    // derive_truncation_range: (pn - largest) * 2 must fit the 1..4-byte encoding (mod.rs:81-93, packet_number_len.rs:163-172)
+    if (!truncated || !pn_len) return QPP_INTERNAL_ERROR;
+    pn &= kPnMask;
+    largest_acked &= kPnMask;
+    if (pn < largest_acked) return QPP_DECODE_ERROR;
+    const uint64_t range = (pn - largest_acked) * 2;
+    size_t len = 0;
+    for (size_t b = 1; b <= 4 && !len; b++)
+        if (range <= (1ull << (8 * b)) - 1) len = b;
+    if (!len) return QPP_DECODE_ERROR;
+    *pn_len = len;
+    *truncated = pn & ((1ull << (8 * len)) - 1);
+    return QPP_OK;
+}
+
+uint64_t qpp_pn_expand(uint64_t largest_acked, uint64_t truncated, size_t pn_len) {
+    if (pn_len < 1 || pn_len > 4) return UINT64_MAX;
+    return decode_packet_number(largest_acked & kPnMask, truncated, (uint32_t)(8 * pn_len));
+}
+
 int qpp_hp_mask_batch(qpp_ctx *ctx, const qpp_pkt *descs, size_t n, const uint8_t *arena, uint8_t *masks,
                       void *stream) {
     if (!ctx || (n && (!descs || !arena || !masks))) return QPP_INTERNAL_ERROR;

@@ -280,7 +280,76 @@ __global__ __launch_bounds__(1024) void hp_mask_kernel(const DevKey *__restrict_
     o[0] = (uint8_t)m0; o[1] = (uint8_t)(m0 >> 8); o[2] = (uint8_t)(m0 >> 16); o[3] = (uint8_t)(m0 >> 24); o[4] = (uint8_t)m1;
 }
 
+// Receive-side header unprotection for a GRO batch, one lane per packet:
+//   sample at header_len + 4 (payload.rs:151-169) -> mask (header_key.rs:52-56) -> remove_header_protection in place
+//   (header_crypto.rs:98-123: first byte, pn_len = (b0 & 3) + 1, PN bytes) -> expand the PN against the space's
+//   largest acknowledged PN (packet/number/mod.rs:191-238) -> the packet key by the key-phase bit 0x04
+//   (key_phase.rs:12,46; KeySet::decrypt_packet, keyset.rs:113-143; long headers: key_idx[0]) -> the qpp_pkt the
+//   open kernels consume.  A packet too short for the sample is DECODE_ERROR and marked QPP_PKT_SKIP.
+__global__ __launch_bounds__(1024) void unprotect_kernel(const DevKey *__restrict__ keys, const qpp_rx_pkt *__restrict__ rx,
+                                                        uint32_t n, uint8_t *__restrict__ arena, qpp_pkt *descs_out,
+                                                        int8_t *status) {
+    // 64 KiB of dynamic LDS: the AES T-tables for the AES header keys
+    build_aes_tables(0);
+    __syncthreads();
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const qpp_rx_pkt r = rx[i];
+    qpp_pkt d{};
+    d.off = r.off;
+    d.key_idx = r.key_idx[0];
+    d.aad_len = r.header_len;
+    uint8_t *base = arena + r.off;
+    const uint32_t hdr = r.header_len;
+    if ((uint32_t)r.len < hdr + 4 + 16) {
+        d.flags = QPP_PKT_SKIP;
+        descs_out[i] = d;
+        status[i] = QPP_DECODE_ERROR;
+        return;
+    }
+    const DevKey *__restrict__ hk = keys + r.key_idx[0];
+    const uint4 smp = ld16(base + hdr + 4);
+    uint32_t m0, m1;
+    if (hk->suite == QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256) {
+        uint32_t k[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) k[j] = hk->hp_rk[j];
+        m0 = chacha_hp_word(k, smp, &m1);
+    } else {
+        const AesLds aes = make_aes(0);
+        const uint4 m = hk->hp_nr == 10 ? aes.encrypt<10>(smp, hk->hp_rk) : aes.encrypt<14>(smp, hk->hp_rk);
+        m0 = m.x;
+        m1 = m.y;
+    }
+    uint8_t b0 = base[0];
+    const bool is_long = (b0 & 0x80) != 0;
+    b0 ^= (uint8_t)m0 & (is_long ? 0x0f : 0x1f);
+    base[0] = b0;
+    const uint32_t pn_len = (b0 & 3u) + 1u;
+    const uint32_t mm = (m0 >> 8) | (m1 << 24);
+    uint64_t trunc = 0;
+    for (uint32_t j = 0; j < pn_len; j++) {
+        const uint8_t x = base[hdr + j] ^ (uint8_t)(mm >> (8 * j));
+        base[hdr + j] = x;
+        trunc = (trunc << 8) | x;
+    }
+    d.pn = decode_packet_number(r.largest_pn & kPnMask, trunc, 8 * pn_len);
+    d.key_idx = (!is_long && (b0 & 0x04)) ? r.key_idx[1] : r.key_idx[0];
+    d.aad_len = (uint16_t)(hdr + pn_len);
+    d.pt_len = (uint16_t)(r.len - hdr - pn_len - 16);
+    d.pn_len = (uint8_t)pn_len;
+    descs_out[i] = d;
+}
+
 }  // namespace
+
+hipError_t launch_unprotect(const DevKey *keys, const qpp_rx_pkt *rx, uint32_t n, uint8_t *arena, qpp_pkt *descs_out,
+                            int8_t *status, hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(unprotect_kernel, dim3((n + 1023) / 1024), dim3(1024), 65536, s, keys, rx, n, arena, descs_out,
+                       status);
+    return hipGetLastError();
+}
 
 hipError_t launch_chacha(bool seal, const DevKey *keys, const qpp_pkt *descs, uint32_t n, uint8_t *arena,
                          uint8_t *masks, int8_t *status, uint32_t flags, hipStream_t s) {

@@ -45,6 +45,23 @@ struct SBox {
 constexpr SBox kSBox{};
 static_assert(kSBox.v[0x00] == 0x63 && kSBox.v[0x53] == 0xed && kSBox.v[0xff] == 0x16, "sbox");
 
+// ---------------------------------------------------------------- packet numbers
+constexpr uint64_t kPnMask = (1ull << 62) - 1;  // PacketNumber::as_u64 drops the space bits
+// RFC 9000 A.3 DecodePacketNumber as quic/s2n-quic-core/src/packet/number/mod.rs:191-238 states it (no data-dependent
+// branches; the result is clamped to VarInt::MAX = 2^62 - 1 like VarInt::new(..).unwrap_or(MAX)).
+__host__ __device__ inline uint64_t decode_packet_number(uint64_t largest, uint64_t truncated, uint32_t nbits) {
+    const uint64_t expected = largest + 1, win = 1ull << nbits, hwin = win >> 1, mask = win - 1;
+    uint64_t cand = (expected & ~mask) | truncated;
+    const bool a = expected >= hwin && cand <= expected - hwin;
+    const bool b = cand < (1ull << 62) - win;
+    const bool c = cand > expected + hwin;
+    const bool d = cand >= win;
+    const bool ab = a && b, cd = !ab && c && d;
+    cand += ab ? win : 0;
+    cand -= cd ? win : 0;
+    return cand > kPnMask ? kPnMask : cand;
+}
+
 // ---------------------------------------------------------------- device key record
 // One per key slot, in HBM, replicated per GPU context.  Words are little-endian images of the
 // byte strings (dword c of an AES state = column c, row 0 in the low byte).
@@ -94,6 +111,9 @@ hipError_t launch_aes_gcm(bool seal, const DevKey *keys, const qpp_pkt *descs, c
                           uint32_t suites, hipStream_t s);
 hipError_t launch_chacha(bool seal, const DevKey *keys, const qpp_pkt *descs, uint32_t n, uint8_t *arena,
                          uint8_t *masks, int8_t *status, uint32_t flags, hipStream_t s);
+// receive side: remove header protection, expand the PN, choose the key by key phase -> descs_out (chacha.hip)
+hipError_t launch_unprotect(const DevKey *keys, const qpp_rx_pkt *rx, uint32_t n, uint8_t *arena, qpp_pkt *descs_out,
+                            int8_t *status, hipStream_t s);
 hipError_t launch_hp_mask(const DevKey *keys, const qpp_pkt *descs, uint32_t n, const uint8_t *arena,
                           uint8_t *masks, hipStream_t s);
 

@@ -33,6 +33,11 @@ ENDPOINT_CLIENT, ENDPOINT_SERVER = 0, 1
 PKT_DTYPE = np.dtype([("pn", "<u8"), ("key_idx", "<u4"), ("off", "<u4"), ("aad_len", "<u2"), ("pt_len", "<u2"),
                       ("pn_len", "u1"), ("flags", "u1"), ("reserved", "<u2")])
 assert PKT_DTYPE.itemsize == 24
+PKT_SKIP = 0x1
+# qpp_rx_pkt (24 bytes): one received, still protected packet
+RX_DTYPE = np.dtype([("largest_pn", "<u8"), ("key_idx", "<u4", (2,)), ("off", "<u4"), ("header_len", "<u2"),
+                     ("len", "<u2")])
+assert RX_DTYPE.itemsize == 24
 
 # every symbol include/qpp.h declares (tests/test_abi.py checks the library exports them all)
 EXPORTS = [
@@ -43,7 +48,7 @@ EXPORTS = [
     "qpp_seal_batch", "qpp_open_batch", "qpp_hp_mask_batch", "qpp_dev_alloc", "qpp_dev_free", "qpp_host_alloc",
     "qpp_host_free", "qpp_memcpy_h2d", "qpp_memcpy_d2h", "qpp_memset_d", "qpp_stream_create",
     "qpp_stream_destroy", "qpp_stream_synchronize", "qpp_event_create", "qpp_event_destroy", "qpp_event_record",
-    "qpp_event_elapsed_ms", "qpp_stream_wait_event",
+    "qpp_event_elapsed_ms", "qpp_stream_wait_event", "qpp_unprotect_open_batch", "qpp_pn_truncate", "qpp_pn_expand",
 ]
 
 
@@ -109,6 +114,9 @@ def lib():
             "qpp_event_record": (ctypes.c_int, [vp, vp, vp]),
             "qpp_event_elapsed_ms": (ctypes.c_int, [vp, vp, vp, ctypes.POINTER(ctypes.c_float)]),
             "qpp_stream_wait_event": (ctypes.c_int, [vp, vp, vp]),
+            "qpp_unprotect_open_batch": (ctypes.c_int, [vp, vp, sz, vp, vp, vp, u32, vp]),
+            "qpp_pn_truncate": (ctypes.c_int, [u64, u64, ctypes.POINTER(u64), ctypes.POINTER(sz)]),
+            "qpp_pn_expand": (u64, [u64, u64, sz]),
         }
         assert set(sig) == set(EXPORTS)
         for name, (res, args) in sig.items():
@@ -220,6 +228,11 @@ class Context:
     def open_batch(self, descs, n, arena, status, flags=0, stream=None):
         self._check(lib().qpp_open_batch(self.handle, _ptr(descs), n, _ptr(arena), _ptr(status), flags, stream),
                     "open_batch")
+
+    def unprotect_open_batch(self, rx, n, arena, descs_out, status, flags=0, stream=None):
+        """Receive path: remove HP, expand the PN, pick the key by key phase, open (qpp_unprotect_open_batch)."""
+        self._check(lib().qpp_unprotect_open_batch(self.handle, _ptr(rx), n, _ptr(arena), _ptr(descs_out), _ptr(status),
+                                                   flags, stream), "unprotect_open_batch")
 
     def hp_mask_batch(self, descs, n, arena, masks, stream=None):
         self._check(lib().qpp_hp_mask_batch(self.handle, _ptr(descs), n, _ptr(arena), _ptr(masks), stream),
@@ -373,3 +386,17 @@ def make_batch(n, pt_len, key_slots, seed, aad_len=21, pn_len=4, pn_base=0, stri
     if aad_len >= 1:
         arena.reshape(n, stride)[:, 0] = 0x43
     return descs, arena
+
+
+def pn_truncate(pn, largest_acked):
+    """PacketNumber::truncate -> (truncated, pn_len); raises QppError(DECODE_ERROR) when it cannot be encoded."""
+    t, ln = u64(), sz()
+    rc = lib().qpp_pn_truncate(pn, largest_acked, ctypes.byref(t), ctypes.byref(ln))
+    if rc != OK:
+        raise QppError(rc, "pn_truncate")
+    return t.value, ln.value
+
+
+def pn_expand(largest_acked, truncated, pn_len):
+    """TruncatedPacketNumber::expand (RFC 9000 A.3)."""
+    return lib().qpp_pn_expand(largest_acked, truncated, pn_len)

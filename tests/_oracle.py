@@ -113,6 +113,35 @@ def unprotect_packet(suite, key, iv, hp, full_pn, pkt, header_len):
     return rc, pn_len.value, bytes(b[:len(pkt)])
 
 
+class OrcRx(ctypes.Structure):
+    _fields_ = [("largest_pn", ctypes.c_uint64), ("key_idx", ctypes.c_uint32 * 2), ("off", ctypes.c_uint32),
+                ("header_len", ctypes.c_uint16), ("len", ctypes.c_uint16)]
+
+
+def decode_pn(largest, truncated, nbits):
+    f = lib().orc_decode_packet_number
+    f.restype = ctypes.c_uint64
+    return f(ctypes.c_uint64(largest), ctypes.c_uint64(truncated), ctypes.c_uint(nbits))
+
+
+def truncate_pn(pn, largest):
+    t, n = ctypes.c_uint64(), ctypes.c_size_t()
+    rc = lib().orc_truncate_packet_number(ctypes.c_uint64(pn), ctypes.c_uint64(largest), ctypes.byref(t), ctypes.byref(n))
+    return rc, t.value, n.value
+
+
+def unprotect_open_batch(keys, rx, arena):
+    """keys: OrcKey array; rx: numpy array with qpp_rx_pkt layout; arena modified in place -> (descs, status)."""
+    import numpy as np
+    n = len(rx)
+    out = np.zeros(n, dtype=[("pn", "<u8"), ("key_idx", "<u4"), ("off", "<u4"), ("aad_len", "<u2"),
+                             ("pt_len", "<u2"), ("pn_len", "u1"), ("flags", "u1"), ("reserved", "<u2")])
+    status = (ctypes.c_int8 * (n + 1))()
+    lib().orc_unprotect_open_batch(keys, rx.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(n),
+                                   arena.ctypes.data_as(ctypes.c_void_p), out.ctypes.data_as(ctypes.c_void_p), status)
+    return out, list(status[:n])
+
+
 def make_keys(keys):
     """keys: list of (suite, key, iv, hp) -> OrcKey array"""
     arr = (OrcKey * len(keys))()

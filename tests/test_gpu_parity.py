@@ -327,3 +327,90 @@ def test_full_size_round_trip(ctx, suite):
         b.free()
     for k in keys:
         k.free()
+
+
+# ------------------------------------------------------------------ receive path: unprotect -> PN expand -> open
+
+def _rx_batch(ctx, n, seed):
+    """Protected packets as a peer sends them: short headers (key phase 0/1) and long headers, PN truncated
+    against the receiver's largest acknowledged PN, some tampered tags and some too short for a sample."""
+    rng = np.random.default_rng(seed)
+    keys, orc_keys = [], []
+    for suite in (1, 2, 3):
+        k0 = ctx.key(suite, rng.integers(0, 256, qpp.HASH_LEN[suite], dtype=np.uint8).tobytes())
+        k1 = k0.derive_next_key()  # KeySet crypto[1]: the next phase, same header key
+        for k in (k0, k1):
+            keys.append(k)
+            orc_keys.append((suite, *k.material()))
+    okeys = orc.make_keys(orc_keys)
+    chunks, rx, orx, want_pn, want_payload = [], [], [], [], []
+    off = 0
+    for i in range(n):
+        s = int(rng.integers(0, 3))  # suite index
+        largest = int(rng.integers(0, 2**62 - 2**20)) if i % 3 else int(rng.integers(0, 300))
+        pn = largest + int(rng.integers(0, 400))
+        rc, _, pn_len = orc.truncate_pn(pn, largest)
+        pn_len = min(4, pn_len + int(rng.integers(0, 2)))  # a sender may use a longer encoding
+        long_hdr = i % 5 == 0
+        phase = 0 if long_hdr else int(rng.integers(0, 2))
+        if long_hdr:
+            first = 0xc0 | (int(rng.integers(0, 4)) << 4) | (pn_len - 1)
+            rest = rng.integers(0, 256, int(rng.integers(6, 40)), dtype=np.uint8).tobytes()
+        else:
+            first = 0x40 | (phase << 2) | (pn_len - 1)
+            rest = rng.integers(0, 256, int(rng.integers(0, 21)), dtype=np.uint8).tobytes()
+        header = bytes([first]) + rest
+        pt = int(rng.integers(max(0, 4 - pn_len), 1400)) if i % 7 else max(0, 4 - pn_len)
+        payload = rng.integers(0, 256, pt, dtype=np.uint8).tobytes()
+        kk = orc_keys[2 * s + phase]
+        rc, pkt = orc.protect_packet(kk[0], kk[1], kk[2], kk[3], pn, header, pn_len, payload)
+        assert rc == 0
+        pkt = bytearray(pkt)
+        if i % 11 == 3:
+            pkt[-1 - i % 16] ^= 0x20  # tampered tag / ciphertext -> DECRYPT_ERROR
+        length = len(pkt)
+        if i % 13 == 5:
+            length = len(header) + 19  # no room for the 16-byte sample at header_len + 4 -> DECODE_ERROR
+            pkt = pkt[:length]
+        chunks.append(bytes(pkt) + bytes(int(rng.integers(0, 7))))
+        rx.append((largest, (keys[2 * s].slot, keys[2 * s + 1].slot), off, len(header), length))
+        orx.append((largest, (2 * s, 2 * s + 1), off, len(header), length))
+        want_pn.append(pn)
+        want_payload.append(payload)
+        off += len(chunks[-1])
+    arena = np.frombuffer(b"".join(chunks) + bytes(64), dtype=np.uint8).copy()
+    return keys, okeys, np.array(rx, dtype=qpp.RX_DTYPE), np.array(orx, dtype=qpp.RX_DTYPE), arena, want_pn, want_payload
+
+
+def test_unprotect_open_batch(ctx):
+    n = 1500
+    keys, okeys, rx, orx, arena, want_pn, want_payload = _rx_batch(ctx, n, seed=21)
+    d_rx, d_arena = ctx.alloc(rx.nbytes), ctx.alloc(arena.nbytes)
+    d_out, d_status = ctx.alloc(n * qpp.PKT_DTYPE.itemsize), ctx.alloc(n)
+    d_rx.upload(rx)
+    d_arena.upload(arena)
+    ctx.unprotect_open_batch(d_rx, n, d_arena, d_out, d_status)
+    ctx.sync()
+    got_arena = d_arena.download()
+    got_out = d_out.download(dtype=qpp.PKT_DTYPE)
+    got_st = d_status.download(dtype=np.int8)
+    want_arena = arena.copy()
+    want_out, want_st = orc.unprotect_open_batch(okeys, orx, want_arena)
+    assert list(got_st) == want_st
+    assert (got_arena == want_arena).all()
+    slot_of = [k.slot for k in keys]
+    for f in ("pn", "aad_len", "pt_len", "pn_len", "flags", "off"):
+        assert (got_out[f] == want_out[f]).all(), f
+    assert [int(s) for s in got_out["key_idx"]] == [slot_of[int(k)] for k in want_out["key_idx"]]
+    # every authentic packet decodes to the sender's packet number and plaintext
+    ok = np.nonzero(got_st == 0)[0]
+    assert len(ok) > n // 2 and (got_st[[i for i in range(n) if i % 13 == 5]] == qpp.DECODE_ERROR).all()
+    for i in ok:
+        d = got_out[i]
+        assert int(d["pn"]) == want_pn[i]
+        a = int(d["off"]) + int(d["aad_len"])
+        assert got_arena[a:a + int(d["pt_len"])].tobytes() == want_payload[i]
+    for b in (d_rx, d_arena, d_out, d_status):
+        b.free()
+    for k in keys:
+        k.free()

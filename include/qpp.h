@@ -85,6 +85,13 @@ uint64_t qpp_integrity_limit(const qpp_key *key);
 /* Test introspection: copies the derived key (16/32), iv (12) and hp (16/32) bytes. */
 int qpp_key_material(const qpp_key *key, uint8_t *key_out, uint8_t iv_out[12], uint8_t *hp_out);
 
+/* Batched key installation on the GPU (key-update churn): n traffic secrets (host memory,
+ * n * hash_len bytes) each go through `updates` TLS_*::update steps ("quic ku", cipher_suite.rs:68-83), then
+ * TLS_*::new's key / iv derivation; the header key is the one of the given secret (not updated, RFC 9001 §6).
+ * HKDF, AES key expansion and the GHASH key powers all run in one device pass; out[0..n) receive the handles
+ * (each equivalent to qpp_key_new(secret) followed by `updates` qpp_key_update calls). */
+int qpp_key_new_batch(qpp_ctx *ctx, int suite, const uint8_t *secrets, size_t n, uint32_t updates, qpp_key **out);
+
 /* InitialKey::new_{client,server}(dcid): AES-128-GCM keys from the Initial salt
  * (quic/s2n-quic-crypto/src/initial.rs:29-80).  Returns the endpoint's sealer and opener. */
 int qpp_initial_keys(qpp_ctx *ctx, int endpoint, const uint8_t *dcid, size_t dcid_len,

@@ -304,6 +304,49 @@ int qpp_key_new(qpp_ctx *ctx, int suite, const uint8_t *secret, size_t secret_le
     return QPP_OK;
 }
 
+int qpp_key_new_batch(qpp_ctx *ctx, int suite, const uint8_t *secrets, size_t n, uint32_t updates, qpp_key **out) {
+    if (!ctx || !out || (n && !secrets)) return QPP_INTERNAL_ERROR;
+    if (!valid_suite(suite)) return QPP_UNSUPPORTED;
+    if (n > (1u << 24)) return QPP_INTERNAL_ERROR;
+    if (!n) return QPP_OK;
+    const size_t hl = suite_hash_len(suite), kl = suite_key_len(suite), mb = key_material_bytes();
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    int rc = flush_keys(ctx, s);  // pending host records first: a later flush never covers these device-made ones
+    if (rc) return rc;
+    const uint32_t first = ctx->next_slot;  // a contiguous range of fresh slots
+    rc = grow_keys(ctx, first + (uint32_t)n);
+    if (rc) return rc;
+    rc = ensure_stage(ctx, n * (hl + mb));
+    if (rc) return rc;
+    uint8_t *h = ctx->h_stage, *d = ctx->d_stage;
+    memcpy(h, secrets, n * hl);
+    HIP_TRY(ctx, hipMemcpyAsync(d, h, n * hl, hipMemcpyHostToDevice, s));
+    HIP_TRY(ctx, launch_key_derive(ctx->d_keys, first, (uint32_t)n, suite, d, updates, d + n * hl, s));
+    HIP_TRY(ctx, hipMemcpyAsync(h + n * hl, d + n * hl, n * mb, hipMemcpyDeviceToHost, s));
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->h_keys.data() + first, ctx->d_keys + first, sizeof(DevKey) * n,
+                                hipMemcpyDeviceToHost, s));  // host mirror of the records the device wrote
+    HIP_TRY(ctx, hipStreamSynchronize(s));
+    HIP_TRY(ctx, hipMemsetAsync(d, 0, n * (hl + mb), s));
+    ctx->next_slot = first + (uint32_t)n;
+    ctx->live_by_suite[suite] += (uint32_t)n;
+    for (size_t i = 0; i < n; i++) {
+        const uint8_t *m = h + n * hl + i * mb;
+        qpp_key *k = new qpp_key();
+        k->ctx = ctx;
+        k->suite = suite;
+        k->slot = first + (uint32_t)i;
+        k->has_secret = true;
+        memcpy(k->secret, m, hl);
+        memcpy(k->key, m + 48, kl);
+        memcpy(k->iv, m + 80, 12);
+        memcpy(k->hp, m + 96, kl);
+        out[i] = k;
+    }
+    secure_zero(h, n * (hl + mb));
+    return QPP_OK;
+}
+
 int qpp_key_new_raw(qpp_ctx *ctx, int suite, const uint8_t *key, size_t key_len, const uint8_t iv[12],
                     const uint8_t *hp, size_t hp_len, qpp_key **out) {
     if (!ctx || !out || !key || !iv || !hp) return QPP_INTERNAL_ERROR;

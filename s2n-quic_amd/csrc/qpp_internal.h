@@ -101,6 +101,11 @@ struct PlanBuffers {
 };
 
 hipError_t launch_key_setup(DevKey *keys, uint32_t first, uint32_t count, hipStream_t s);
+// keysched.hip: n secrets -> updates x "quic ku" -> key/iv (+ hp of the first secret) -> DevKey records
+// keys[first .. first+n) and per-key material (secret' | key | iv | hp, key_material_bytes() each); then key setup
+hipError_t launch_key_derive(DevKey *keys, uint32_t first, uint32_t n, int suite, const uint8_t *secrets,
+                             uint32_t updates, uint8_t *material, hipStream_t s);
+uint32_t key_material_bytes();
 hipError_t launch_plan(const DevKey *keys, uint32_t key_cap, const qpp_pkt *descs, uint32_t n, PlanBuffers pb,
                        uint32_t per, hipStream_t s);
 uint32_t plan_max_work(uint32_t n, uint32_t key_cap, uint32_t per);

@@ -49,6 +49,7 @@ EXPORTS = [
     "qpp_host_free", "qpp_memcpy_h2d", "qpp_memcpy_d2h", "qpp_memset_d", "qpp_stream_create",
     "qpp_stream_destroy", "qpp_stream_synchronize", "qpp_event_create", "qpp_event_destroy", "qpp_event_record",
     "qpp_event_elapsed_ms", "qpp_stream_wait_event", "qpp_unprotect_open_batch", "qpp_pn_truncate", "qpp_pn_expand",
+    "qpp_key_new_batch",
 ]
 
 
@@ -117,6 +118,7 @@ def lib():
             "qpp_unprotect_open_batch": (ctypes.c_int, [vp, vp, sz, vp, vp, vp, u32, vp]),
             "qpp_pn_truncate": (ctypes.c_int, [u64, u64, ctypes.POINTER(u64), ctypes.POINTER(sz)]),
             "qpp_pn_expand": (u64, [u64, u64, sz]),
+            "qpp_key_new_batch": (ctypes.c_int, [vp, ctypes.c_int, vp, sz, u32, ctypes.POINTER(vp)]),
         }
         assert set(sig) == set(EXPORTS)
         for name, (res, args) in sig.items():
@@ -201,6 +203,16 @@ class Context:
         if rc != OK:
             raise QppError(rc, "qpp_key_new")
         return Key(self, h.value)
+
+    def keys_batch(self, suite, secrets, updates=0):
+        """qpp_key_new_batch: every secret -> `updates` x derive_next_key, derived on the GPU in one pass."""
+        secrets = [bytes(x) for x in secrets]
+        n = len(secrets)
+        arr = (vp * max(n, 1))()
+        rc = lib().qpp_key_new_batch(self.handle, suite, _bytes_ptr(b"".join(secrets)), n, updates, arr)
+        if rc != OK:
+            raise QppError(rc, "qpp_key_new_batch")
+        return [Key(self, arr[i]) for i in range(n)]
 
     def raw_key(self, suite, key, iv, hp):
         h = vp()

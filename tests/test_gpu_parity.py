@@ -414,3 +414,38 @@ def test_unprotect_open_batch(ctx):
         b.free()
     for k in keys:
         k.free()
+
+
+# ------------------------------------------------------------------ device key schedule (key-update churn)
+
+@pytest.mark.parametrize("suite", [1, 2, 3])
+def test_key_new_batch_matches_host_chain(ctx, suite):
+    rng = np.random.default_rng(40 + suite)
+    hl = qpp.HASH_LEN[suite]
+    secrets = [rng.integers(0, 256, hl, dtype=np.uint8).tobytes() for _ in range(300)]
+    for updates in (0, 1, 3):
+        batch = ctx.keys_batch(suite, secrets, updates)
+        for i in range(0, 300, 37):
+            k = ctx.key(suite, secrets[i])
+            hp0 = k.material()[2]
+            for _ in range(updates):
+                k = k.derive_next_key()
+            assert batch[i].material() == k.material()
+            assert batch[i].material()[2] == hp0  # the header key is never updated
+            # the oracle agrees on the whole chain
+            s = secrets[i]
+            for _ in range(updates):
+                s = orc.update_secret(suite, s)
+            key, iv, _ = orc.derive(suite, s)
+            assert batch[i].material()[:2] == (key, iv)
+            k.free()
+        # the device-made records seal bit-exactly (round keys, H powers, nonce)
+        slots = [k.slot for k in batch]
+        descs, arena = qpp.make_batch(600, 700, slots, seed=77 + updates)
+        okeys = orc.make_keys([(suite, *k.material()) for k in batch])
+        got, masks, st = _run_seal(ctx, descs, arena, qpp.HP_MASK_OUT)
+        want = arena.copy()
+        want_masks = orc.seal_batch(okeys, _oracle_keys_for(okeys, descs, slots), want, qpp.HP_MASK_OUT)
+        assert (st == 0).all() and (got == want).all() and masks.tobytes() == want_masks
+        for k in batch:
+            k.free()

@@ -157,6 +157,29 @@ int qpp_open_batch(qpp_ctx *ctx, const qpp_pkt *descs, size_t n, uint8_t *arena,
 int qpp_hp_mask_batch(qpp_ctx *ctx, const qpp_pkt *descs, size_t n, const uint8_t *arena, uint8_t *masks,
                       void *stream);
 
+/* ------------------------------------------------------------------ deferred transmit queue */
+
+/* The transport seals one packet at a time, in place, into the GSO segment buffer and applies header protection
+ * right after (packet/encoding.rs:274-278, crypto/mod.rs:182-247; platform socket/io/tx.rs:204-268).  A qpp_txq
+ * defers both: the transport encodes header || PN || plaintext into the queue's ring (pinned host memory, the
+ * segment buffer), qpp_txq_push records what Key::encrypt + HeaderKey::sealing_header_protection_mask would have
+ * done, and qpp_txq_flush (at the end of a GSO burst / queue.flush(), endpoint/mod.rs:158) protects every pushed
+ * packet in one device batch: the ring then holds the protected packets, tags included. */
+typedef struct qpp_txq qpp_txq;
+int qpp_txq_create(qpp_ctx *ctx, size_t ring_bytes, size_t max_packets, qpp_txq **out);
+void qpp_txq_destroy(qpp_txq *q);
+/* Host pointer to the ring (ring_bytes, pinned). */
+uint8_t *qpp_txq_ring(qpp_txq *q);
+/* The packet at ring[off]: header (header_len bytes, PN excluded) || PN (pn_len bytes) || payload_len bytes of
+ * plaintext, with 16 bytes after it for the tag.  QPP_DECODE_ERROR when payload_len + pn_len < 4 (no room for
+ * the HP sample, encoding.rs:178-188); QPP_INTERNAL_ERROR on a bad range, a full queue or a key of another
+ * context. */
+int qpp_txq_push(qpp_txq *q, const qpp_key *key, uint64_t pn, size_t off, size_t header_len, size_t pn_len,
+                 size_t payload_len);
+/* Seal + header-protect every pushed packet (one qpp_seal_batch with QPP_HP_APPLY), wait, empty the queue. */
+int qpp_txq_flush(qpp_txq *q);
+size_t qpp_txq_pending(const qpp_txq *q);
+
 /* ------------------------------------------------------------------ receive path */
 
 /* One received, still protected packet of a GRO batch. */

@@ -664,3 +664,98 @@ int qpp_stream_wait_event(qpp_ctx *ctx, void *stream, void *event) {
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------- deferred transmit queue
+
+struct qpp_txq {
+    qpp_ctx *ctx = nullptr;
+    size_t ring_bytes = 0, max_packets = 0;
+    uint8_t *h_ring = nullptr, *d_ring = nullptr;
+    qpp_pkt *h_desc = nullptr, *d_desc = nullptr;
+    size_t count = 0, lo = SIZE_MAX, hi = 0;
+    uint32_t suites = 0;
+};
+
+extern "C" {
+
+int qpp_txq_create(qpp_ctx *ctx, size_t ring_bytes, size_t max_packets, qpp_txq **out) {
+    if (!ctx || !out || !ring_bytes || !max_packets || ring_bytes > UINT32_MAX) return QPP_INTERNAL_ERROR;
+    *out = nullptr;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    qpp_txq *q = new qpp_txq();
+    q->ctx = ctx;
+    q->ring_bytes = ring_bytes;
+    q->max_packets = max_packets;
+    if (fail(ctx, hipHostMalloc(&q->h_ring, ring_bytes, hipHostMallocDefault), "txq ring") ||
+        fail(ctx, hipMalloc(&q->d_ring, ring_bytes), "txq ring") ||
+        fail(ctx, hipHostMalloc(&q->h_desc, sizeof(qpp_pkt) * max_packets, hipHostMallocDefault), "txq descs") ||
+        fail(ctx, hipMalloc(&q->d_desc, sizeof(qpp_pkt) * max_packets), "txq descs")) {
+        qpp_txq_destroy(q);
+        return QPP_DEVICE_ERROR;
+    }
+    memset(q->h_ring, 0, ring_bytes);
+    *out = q;
+    return QPP_OK;
+}
+
+void qpp_txq_destroy(qpp_txq *q) {
+    if (!q) return;
+    hipSetDevice(q->ctx->device);
+    hipStreamSynchronize(q->ctx->stream);
+    if (q->h_ring) { secure_zero(q->h_ring, q->ring_bytes); hipHostFree(q->h_ring); }
+    if (q->d_ring) { hipMemset(q->d_ring, 0, q->ring_bytes); hipFree(q->d_ring); }
+    if (q->h_desc) hipHostFree(q->h_desc);
+    if (q->d_desc) hipFree(q->d_desc);
+    delete q;
+}
+
+uint8_t *qpp_txq_ring(qpp_txq *q) { return q ? q->h_ring : nullptr; }
+size_t qpp_txq_pending(const qpp_txq *q) { return q ? q->count : 0; }
+
+int qpp_txq_push(qpp_txq *q, const qpp_key *key, uint64_t pn, size_t off, size_t header_len, size_t pn_len,
+                 size_t payload_len) {
+    if (!q || !key || key->ctx != q->ctx) return QPP_INTERNAL_ERROR;
+    if (q->count >= q->max_packets) return QPP_INTERNAL_ERROR;  // flush first
+    if (pn_len < 1 || pn_len > 4 || header_len + pn_len > 0xffff || payload_len > 0xffff) return QPP_INTERNAL_ERROR;
+    const size_t end = off + header_len + pn_len + payload_len + 16;
+    if (end > q->ring_bytes || end < off) return QPP_INTERNAL_ERROR;
+    if (payload_len + pn_len < 4) return QPP_DECODE_ERROR;  // the sample at header_len + 4 must fit
+    qpp_pkt &d = q->h_desc[q->count++];
+    d = qpp_pkt{};
+    d.pn = pn;
+    d.key_idx = key->slot;
+    d.off = (uint32_t)off;
+    d.aad_len = (uint16_t)(header_len + pn_len);
+    d.pt_len = (uint16_t)payload_len;
+    d.pn_len = (uint8_t)pn_len;
+    q->lo = std::min(q->lo, off);
+    q->hi = std::max(q->hi, end);
+    q->suites |= 1u << key->suite;
+    return QPP_OK;
+}
+
+int qpp_txq_flush(qpp_txq *q) {
+    if (!q) return QPP_INTERNAL_ERROR;
+    if (!q->count) return QPP_OK;
+    qpp_ctx *ctx = q->ctx;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    const size_t span = q->hi - q->lo;
+    HIP_TRY(ctx, hipMemcpyAsync(q->d_ring + q->lo, q->h_ring + q->lo, span, hipMemcpyHostToDevice, s));
+    HIP_TRY(ctx, hipMemcpyAsync(q->d_desc, q->h_desc, sizeof(qpp_pkt) * q->count, hipMemcpyHostToDevice, s));
+    const uint32_t aes = (1u << QPP_SUITE_TLS_AES_128_GCM_SHA256) | (1u << QPP_SUITE_TLS_AES_256_GCM_SHA384);
+    uint32_t flags = QPP_HP_APPLY;
+    if (!(q->suites & ~aes)) flags |= QPP_ONLY_AES;
+    else if (!(q->suites & aes)) flags |= QPP_ONLY_CHACHA;
+    int rc = qpp_seal_batch(ctx, q->d_desc, q->count, q->d_ring, nullptr, nullptr, flags, s);
+    if (rc) return rc;
+    HIP_TRY(ctx, hipMemcpyAsync(q->h_ring + q->lo, q->d_ring + q->lo, span, hipMemcpyDeviceToHost, s));
+    HIP_TRY(ctx, hipStreamSynchronize(s));
+    q->count = 0;
+    q->lo = SIZE_MAX;
+    q->hi = 0;
+    q->suites = 0;
+    return QPP_OK;
+}
+
+}  // extern "C"

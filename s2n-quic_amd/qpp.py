@@ -49,7 +49,8 @@ EXPORTS = [
     "qpp_host_free", "qpp_memcpy_h2d", "qpp_memcpy_d2h", "qpp_memset_d", "qpp_stream_create",
     "qpp_stream_destroy", "qpp_stream_synchronize", "qpp_event_create", "qpp_event_destroy", "qpp_event_record",
     "qpp_event_elapsed_ms", "qpp_stream_wait_event", "qpp_unprotect_open_batch", "qpp_pn_truncate", "qpp_pn_expand",
-    "qpp_key_new_batch",
+    "qpp_key_new_batch", "qpp_txq_create", "qpp_txq_destroy", "qpp_txq_ring", "qpp_txq_push", "qpp_txq_flush",
+    "qpp_txq_pending",
 ]
 
 
@@ -119,6 +120,12 @@ def lib():
             "qpp_pn_truncate": (ctypes.c_int, [u64, u64, ctypes.POINTER(u64), ctypes.POINTER(sz)]),
             "qpp_pn_expand": (u64, [u64, u64, sz]),
             "qpp_key_new_batch": (ctypes.c_int, [vp, ctypes.c_int, vp, sz, u32, ctypes.POINTER(vp)]),
+            "qpp_txq_create": (ctypes.c_int, [vp, sz, sz, ctypes.POINTER(vp)]),
+            "qpp_txq_destroy": (None, [vp]),
+            "qpp_txq_ring": (vp, [vp]),
+            "qpp_txq_push": (ctypes.c_int, [vp, vp, u64, sz, sz, sz, sz]),
+            "qpp_txq_flush": (ctypes.c_int, [vp]),
+            "qpp_txq_pending": (sz, [vp]),
         }
         assert set(sig) == set(EXPORTS)
         for name, (res, args) in sig.items():
@@ -412,3 +419,34 @@ def pn_truncate(pn, largest_acked):
 def pn_expand(largest_acked, truncated, pn_len):
     """TruncatedPacketNumber::expand (RFC 9000 A.3)."""
     return lib().qpp_pn_expand(largest_acked, truncated, pn_len)
+
+
+class TxQueue:
+    """qpp_txq: deferred Key::encrypt + header protection over a pinned ring (the GSO segment buffer)."""
+
+    def __init__(self, ctx, ring_bytes, max_packets):
+        h = vp()
+        rc = lib().qpp_txq_create(ctx.handle, ring_bytes, max_packets, ctypes.byref(h))
+        if rc != OK:
+            raise QppError(rc, "qpp_txq_create")
+        self.handle, self.ctx = h.value, ctx
+        self.ring = np.ctypeslib.as_array((ctypes.c_uint8 * ring_bytes).from_address(lib().qpp_txq_ring(self.handle)))
+
+    def push(self, key, pn, off, header_len, pn_len, payload_len):
+        rc = lib().qpp_txq_push(self.handle, key.handle, pn, off, header_len, pn_len, payload_len)
+        if rc != OK:
+            raise QppError(rc, "qpp_txq_push")
+
+    def flush(self):
+        rc = lib().qpp_txq_flush(self.handle)
+        if rc != OK:
+            raise QppError(rc, "qpp_txq_flush")
+
+    def pending(self):
+        return lib().qpp_txq_pending(self.handle)
+
+    def close(self):
+        if self.handle:
+            self.ring = None
+            lib().qpp_txq_destroy(self.handle)
+            self.handle = None

@@ -449,3 +449,43 @@ def test_key_new_batch_matches_host_chain(ctx, suite):
         assert (st == 0).all() and (got == want).all() and masks.tobytes() == want_masks
         for k in batch:
             k.free()
+
+
+# ------------------------------------------------------------------ deferred transmit queue (the TX caller)
+
+def test_txq_deferred_seal_matches_encode_packet(ctx):
+    """Packets encoded into the queue's ring the way PacketEncoder::encode_packet lays them out
+    (packet/encoding.rs:115-282: header, truncated PN, payload, tag room), pushed instead of sealed, then one
+    flush: every packet equals crypto::encrypt + crypto::protect of the oracle."""
+    rng = np.random.default_rng(8)
+    keys = [ctx.key(s, rng.integers(0, 256, qpp.HASH_LEN[s], dtype=np.uint8).tobytes()) for s in (1, 2, 3)]
+    q = qpp.TxQueue(ctx, 1 << 20, 1024)
+    want, off = [], 0
+    largest = int(rng.integers(0, 2**40))
+    for i in range(600):
+        k = keys[i % 3]
+        pn = largest + 1 + i
+        trunc, pn_len = qpp.pn_truncate(pn, largest)
+        header = bytes([0x40 | (pn_len - 1)]) + rng.integers(0, 256, 16, dtype=np.uint8).tobytes()  # short header
+        payload = rng.integers(0, 256, int(rng.integers(4, 1300)), dtype=np.uint8).tobytes()
+        pkt = header + trunc.to_bytes(pn_len, "big") + payload
+        q.ring[off:off + len(pkt)] = np.frombuffer(pkt, dtype=np.uint8)
+        q.push(k, pn, off, len(header), pn_len, len(payload))
+        suite, (kk, iv, hp) = k.suite, k.material()
+        rc, protected = orc.protect_packet(suite, kk, iv, hp, pn, header, pn_len, payload)
+        want.append((off, protected))
+        off += len(protected) + int(rng.integers(0, 5))
+    assert q.pending() == 600
+    q.flush()
+    assert q.pending() == 0
+    for o, p in want:
+        assert q.ring[o:o + len(p)].tobytes() == p
+    # the sample must fit (encoding.rs:178-188 pads short payloads); the queue refuses instead of sealing
+    with pytest.raises(qpp.QppError) as e:
+        q.push(keys[0], 1, 0, 17, 1, 2)
+    assert e.value.code == qpp.DECODE_ERROR
+    with pytest.raises(qpp.QppError):
+        q.push(keys[0], 1, (1 << 20) - 20, 17, 1, 100)  # does not fit the ring
+    q.close()
+    for k in keys:
+        k.free()

@@ -76,7 +76,9 @@ def main():
     ap.add_argument("--pt", type=int, default=1200, help="payload bytes per packet")
     ap.add_argument("--aad", type=int, default=21, help="short header: 0x43 || DCID16 || PN4")
     ap.add_argument("--keys", type=int, default=1)
-    ap.add_argument("--mode", default="device", choices=["device", "e2e"])
+    ap.add_argument("--mode", default="device", choices=["device", "e2e", "rx", "keys"],
+                    help="device: seal+open in HBM (headline); e2e: pinned host -> HBM -> host; rx: receive path "
+                         "(unprotect -> PN expand -> open); keys: device key schedule (key-update churn)")
     ap.add_argument("--cpu-seconds", type=float, default=1.5)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-hp", action="store_true", help="seal without the HP mask (diagnostic)")
@@ -101,6 +103,10 @@ def main():
 
     if args.mode == "e2e":
         return e2e(args, ctx, keys, descs, arena, d_desc, d_mask, d_status, flags, rank, world, barrier, max_over_ranks)
+    if args.mode == "rx":
+        return rx(args, ctx, keys, descs, arena, d_desc, d_mask, d_status, flags, rank, world, barrier, max_over_ranks)
+    if args.mode == "keys":
+        return keys_churn(args, ctx, suite, rank, world, barrier, max_over_ranks)
 
     d_arena = ctx.alloc(arena.nbytes)
     d_arena.upload(arena)
@@ -226,6 +232,82 @@ def e2e(args, ctx, keys, descs, arena, d_desc, d_mask, d_status, flags, rank, wo
             "value": round(2.0 * n * pt * args.steps * world / t / GiB, 3), "unit": "GiB/s", "n_gpus": world,
             "steps": args.steps, "ms_per_step": round(1e3 * t / args.steps, 3), "chunks": chunks,
             "h2d_d2h_bytes_per_step": 2 * arena.nbytes, "suite": args.suite,
+        }), flush=True)
+    ctx.close()
+
+
+def rx(args, ctx, keys, descs, arena, d_desc, d_mask, d_status, flags, rank, world, barrier, max_over_ranks):
+    """Receive path: a GRO batch of protected packets (sealed + header-protected on the device
+    first) -> qpp_unprotect_open_batch: HP removal, PN expansion against largest_pn, key choice by key phase, open.
+    Each step restores the protected arena (device copy, excluded from the timed kernel events) and opens it."""
+    n, pt, aad = args.packets, args.pt, args.aad
+    stride = arena.size // n
+    # the header's 4 PN bytes carry the packet number (truncated against largest_pn = pn - 1)
+    pnb = (descs["pn"] & np.uint64(0xffffffff)).astype(">u4").view(np.uint8).reshape(n, 4)
+    arena.reshape(n, stride)[:, aad - 4:aad] = pnb
+    d_arena, d_prot = ctx.alloc(arena.nbytes), ctx.alloc(arena.nbytes)
+    d_arena.upload(arena)
+    ctx.seal_batch(d_desc, n, d_arena, d_mask, d_status, flags | qpp.HP_APPLY)
+    ctx.sync()
+    lib = qpp.lib()
+    rxd = np.zeros(n, dtype=qpp.RX_DTYPE)
+    rxd["largest_pn"] = np.maximum(descs["pn"], np.uint64(1)) - np.uint64(1)
+    rxd["key_idx"][:, 0] = descs["key_idx"]
+    rxd["key_idx"][:, 1] = descs["key_idx"]
+    rxd["off"] = descs["off"]
+    rxd["header_len"] = aad - descs["pn_len"]
+    rxd["len"] = aad + pt + 16
+    d_rx, d_out = ctx.alloc(rxd.nbytes), ctx.alloc(n * qpp.PKT_DTYPE.itemsize)
+    d_rx.upload(rxd)
+    s = ctx.stream
+
+    def hip_d2d(dst, src):
+        ctx._check(lib.qpp_memcpy_d2d(ctx.handle, dst.ptr, src.ptr, arena.nbytes, s), "d2d")
+
+    hip_d2d(d_prot, d_arena)  # keep the protected image
+    ms = []
+    for k in range(args.warmup + args.steps):
+        hip_d2d(d_arena, d_prot)
+        e0, e1 = ctx.event(), ctx.event()
+        ctx.record(e0, s)
+        ctx.unprotect_open_batch(d_rx, n, d_arena, d_out, d_status, flags & ~qpp.HP_MASK_OUT, stream=s)
+        ctx.record(e1, s)
+        ctx.sync(s)
+        if k >= args.warmup:
+            ms.append(ctx.elapsed_ms(e0, e1))
+    st = d_status.download(dtype=np.int8)
+    assert (st == 0).all(), f"{int((st != 0).sum())} packets failed to open"
+    t = max_over_ranks(float(np.mean(ms)))
+    if rank == 0:
+        print(json.dumps({
+            "metric": "GiB/s receive path (unprotect -> PN expand -> open), device-resident, 1200 B packets",
+            "value": round(n * pt * world / (t / 1e3) / GiB, 3), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+            "ms_per_step": round(t, 4), "suite": args.suite, "packets_per_gpu": n, "keys": args.keys,
+        }), flush=True)
+    ctx.close()
+
+
+def keys_churn(args, ctx, suite, rank, world, barrier, max_over_ranks):
+    """Device key schedule (BASELINE configs[4] key churn): qpp_key_new_batch derives
+    args.keys keys per step (1 "quic ku" update each) -- HKDF, AES expansion and GHASH powers on the GPU."""
+    rng = np.random.default_rng(0x5eed0000 + 5)
+    hl = qpp.HASH_LEN[suite]
+    secrets = [rng.integers(0, 256, hl, dtype=np.uint8).tobytes() for _ in range(args.keys)]
+    times = []
+    for k in range(args.warmup + args.steps):
+        t0 = time.perf_counter()
+        ks = ctx.keys_batch(suite, secrets, 1)
+        t = time.perf_counter() - t0
+        for key in ks:
+            key.free()
+        if k >= args.warmup:
+            times.append(t)
+    t = max_over_ranks(float(np.mean(times)))
+    if rank == 0:
+        print(json.dumps({
+            "metric": "keys/s installed (secret -> quic ku -> key/iv/hp -> AES schedule + GHASH powers), host wall",
+            "value": round(args.keys * world / t, 1), "unit": "keys/s", "n_gpus": world, "steps": args.steps,
+            "ms_per_step": round(1e3 * t, 3), "suite": args.suite, "keys_per_step": args.keys,
         }), flush=True)
     ctx.close()
 

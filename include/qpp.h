@@ -217,6 +217,7 @@ int qpp_host_alloc(qpp_ctx *ctx, size_t bytes, void **out); /* pinned host memor
 void qpp_host_free(qpp_ctx *ctx, void *ptr);
 int qpp_memcpy_h2d(qpp_ctx *ctx, void *dst, const void *src, size_t bytes, void *stream);
 int qpp_memcpy_d2h(qpp_ctx *ctx, void *dst, const void *src, size_t bytes, void *stream);
+int qpp_memcpy_d2d(qpp_ctx *ctx, void *dst, const void *src, size_t bytes, void *stream);
 int qpp_memset_d(qpp_ctx *ctx, void *dst, int value, size_t bytes, void *stream);
 int qpp_stream_create(qpp_ctx *ctx, void **out);
 void qpp_stream_destroy(qpp_ctx *ctx, void *stream);

@@ -612,6 +612,12 @@ int qpp_host_alloc(qpp_ctx *ctx, size_t bytes, void **out) {
 void qpp_host_free(qpp_ctx *, void *ptr) {
     if (ptr) hipHostFree(ptr);
 }
+int qpp_memcpy_d2d(qpp_ctx *ctx, void *dst, const void *src, size_t bytes, void *stream) {
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    HIP_TRY(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, stream ? (hipStream_t)stream : ctx->stream));
+    return QPP_OK;
+}
+
 int qpp_memcpy_h2d(qpp_ctx *ctx, void *dst, const void *src, size_t bytes, void *stream) {
     HIP_TRY(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, stream ? (hipStream_t)stream : ctx->stream));
     return QPP_OK;

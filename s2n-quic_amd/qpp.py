@@ -50,7 +50,7 @@ EXPORTS = [
     "qpp_stream_destroy", "qpp_stream_synchronize", "qpp_event_create", "qpp_event_destroy", "qpp_event_record",
     "qpp_event_elapsed_ms", "qpp_stream_wait_event", "qpp_unprotect_open_batch", "qpp_pn_truncate", "qpp_pn_expand",
     "qpp_key_new_batch", "qpp_txq_create", "qpp_txq_destroy", "qpp_txq_ring", "qpp_txq_push", "qpp_txq_flush",
-    "qpp_txq_pending",
+    "qpp_txq_pending", "qpp_memcpy_d2d",
 ]
 
 
@@ -126,6 +126,7 @@ def lib():
             "qpp_txq_push": (ctypes.c_int, [vp, vp, u64, sz, sz, sz, sz]),
             "qpp_txq_flush": (ctypes.c_int, [vp]),
             "qpp_txq_pending": (sz, [vp]),
+            "qpp_memcpy_d2d": (ctypes.c_int, [vp, vp, vp, sz, vp]),
         }
         assert set(sig) == set(EXPORTS)
         for name, (res, args) in sig.items():

@@ -145,6 +145,17 @@ def main():
     t_max = max_over_ranks(t_ms)
 
     payload = 2.0 * n * pt * args.steps * world  # seal + open, all ranks
+    # HBM bytes per seal launch from the committed PMC profile of this workload (tools/profile.sh + tools/traffic.py);
+    # rocprof counters cannot be read from inside this process
+    traffic = None
+    try:
+        tdb = json.load(open(os.path.join(ROOT, "profiles", "traffic.json")))
+        t = tdb.get(f"{args.suite}/{pt}/{args.keys}")
+        if t and n == 1 << 20:
+            traffic = {"bytes": t["traffic_bytes"], "per_alg": round(t["traffic_bytes"] / (n * seal_bytes_per_packet(pt, aad)), 3),
+                       "source": "profiles/traffic.json: " + t["source"]}
+    except (OSError, ValueError, KeyError):
+        traffic = None
     value = payload / (t_max / 1e3) / GiB
     seal_avg = float(np.mean(seal_ms))
     achieved = n * seal_bytes_per_packet(pt, aad) / (seal_avg / 1e3) / 1e9
@@ -164,7 +175,7 @@ def main():
             },
             "roofline": {
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "kernel": "aes_gcm_kernel<seal> + plan (per seal call)" if suite != 3 else "chacha_kernel<seal>",
                 "bytes_per_packet": seal_bytes_per_packet(pt, aad),
             },

@@ -12,5 +12,8 @@ run c4_aes128_pt300 --pt 300 --packets 4194304 && \
 run c4_aes128_pt1452 --pt 1452 && \
 run c4_aes128_pt8000 --pt 8000 --packets 131072 && \
 run c5_aes128_4ki_keys --keys 4096 --packets 2097152 && \
+run rx_aes128 --mode rx && \
+run rx_chacha_64keys --mode rx --suite chacha20poly1305 --keys 64 && \
+run keys_4ki_aes128 --mode keys --keys 4096 && \
 run e2e_aes128 --mode e2e --steps 3 && \
 run e2e_c5_4ki_keys --mode e2e --keys 4096 --packets 2097152 --steps 3

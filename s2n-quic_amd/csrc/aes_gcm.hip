@@ -69,6 +69,27 @@ struct Ghash {
         return lds_ld128(kLdsGhash + __builtin_amdgcn_perm(wk, lc[K], sel[I]));
     }
     // (Z * H) ^ c in natural word order, from W = rot(Z)
+#ifdef QPP_GHASH_SPLIT
+    // Two halves of 8 lookups: the second half's addresses are made to depend on the first half's sum (an empty
+    // asm), so at most 8 ds_read_b128 results (32 VGPRs) are live per step instead of 16 (64 VGPRs).
+    __device__ __forceinline__ static uint32_t after(uint32_t v, uint32_t dep) {
+        asm volatile("; ghash split" : "+v"(v) : "v"(dep));
+        return v;
+    }
+    __device__ __forceinline__ uint4 prod(const uint4 &w, uint4 c) const {
+        const uint4 a = xor3(look<0, 0>(w), look<0, 1>(w), look<0, 2>(w));
+        const uint4 b = xor3(look<0, 3>(w), look<1, 0>(w), look<1, 1>(w));
+        const uint4 d = xor3(look<1, 2>(w), look<1, 3>(w), c);
+        const uint4 h1 = xor3(a, b, d);
+        uint4 w2 = w;
+        w2.z = after(w.z, h1.x);
+        w2.w = after(w.w, h1.x);
+        const uint4 e = xor3(look<2, 0>(w2), look<2, 1>(w2), look<2, 2>(w2));
+        const uint4 f = xor3(look<2, 3>(w2), look<3, 0>(w2), look<3, 1>(w2));
+        const uint4 g = xor3(look<3, 2>(w2), look<3, 3>(w2), h1);
+        return xor3(e, f, g);
+    }
+#else
     __device__ __forceinline__ uint4 prod(const uint4 &w, uint4 c) const {
         const uint4 a = xor3(look<0, 0>(w), look<0, 1>(w), look<0, 2>(w));
         const uint4 b = xor3(look<0, 3>(w), look<1, 0>(w), look<1, 1>(w));
@@ -79,6 +100,7 @@ struct Ghash {
         const uint4 h = xor3(e, f, look<3, 3>(w));
         return xor3(g, h, c);
     }
+#endif
     // one chain step: W' = rot(Z * H ^ c)
     __device__ __forceinline__ uint4 mulx(const uint4 &w, uint4 c) const { return rot(prod(w, c)); }
 };
@@ -214,11 +236,28 @@ __device__ __forceinline__ void process_packet(const AesLds &aes, const Ghash &g
 
     uint4 ks[NB], cin[NB], cprev[NB], ek0 = make_uint4(0, 0, 0, 0);
     int bprev = -NB;  // first block index of the previous group (for its GHASH validity)
+    // Cooperative stores of group g-1 are issued at the top of iteration g, AFTER this group's prefetched loads
+    // have been consumed: vmcnt counts loads and stores together, so a store issued behind a prefetch would make
+    // the next wait for that prefetch also wait for the store's write acknowledgement.
+    auto co_store = [&](int g, const uint4 (&v)[NB]) {
+#pragma unroll
+        for (int i = 0; i < NB; i++) {
+            const int b = NB * g - 2 + (int)co_k[i];
+            if (b >= 0 && b < (int)(co_len[i] >> 4)) st16(arena + co_off[i] + 16u * (uint32_t)b, v[i]);
+        }
+    };
     co_load(0, cin);
     for (int g = 0; g < G; g++) {
+        uint4 co_out[NB];
+        if (g) {  // the previous group's outputs, still in the staging area
+#pragma unroll
+            for (int i = 0; i < NB; i++) co_out[i] = lds_ld128(st.coop(i));
+            wave_lds_sync();
+        }
         // this group's inputs: coalesced chunks -> LDS -> my packet's blocks
 #pragma unroll
         for (int i = 0; i < NB; i++) lds_st128(st.coop(i), cin[i]);
+        if (g) co_store(g - 1, co_out);
         wave_lds_sync();
         uint4 in[NB];
 #pragma unroll
@@ -233,6 +272,7 @@ __device__ __forceinline__ void process_packet(const AesLds &aes, const Ghash &g
 #else
         ctr_keystream<NR, NB>(aes, pg, rk, c, ks);
 #endif
+#ifndef QPP_LEAN
         // GHASH of the previous group (independent of the keystream just issued)
 #pragma unroll
         for (int j = 0; j < NB; j++)
@@ -242,12 +282,23 @@ __device__ __forceinline__ void process_packet(const AesLds &aes, const Ghash &g
             if (bprev + j >= 0 && bprev + j < nblk) z = gh.mulx(z, cprev[j]);
 #endif
         if (g == 0) ek0 = ks[1];
+#endif
         const int b0 = NB * g - 2;  // data block of slot 0
 #pragma unroll
         for (int j = 0; j < NB; j++) {
             const int b = b0 + j;
             const uint4 out = in[j] ^ ks[j];
             lds_st128(st.own(j), out);  // full blocks leave through the cooperative store below
+#ifdef QPP_LEAN
+            // lean form: this group's GHASH right away (no deferred ciphertext registers)
+            if (b >= 0 && b < nfull) {
+                z = gh.mulx(z, SEAL ? out : in[j]);
+            } else if (b == nfull && rem) {
+                const uint4 o = keep_bytes(out, rem);
+                st_bytes(pay + 16 * b, o, rem);
+                z = gh.mulx(z, SEAL ? o : keep_bytes(in[j], rem));
+            }
+#else
             if (b >= 0 && b < nfull) {
                 cprev[j] = SEAL ? out : in[j];
             } else if (b == nfull && rem) {
@@ -255,20 +306,27 @@ __device__ __forceinline__ void process_packet(const AesLds &aes, const Ghash &g
                 st_bytes(pay + 16 * b, o, rem);
                 cprev[j] = SEAL ? o : keep_bytes(in[j], rem);
             }
+#endif
         }
         bprev = b0;
         wave_lds_sync();
-#pragma unroll
-        for (int i = 0; i < NB; i++) {
-            const uint4 v = lds_ld128(st.coop(i));
-            const int b = b0 + (int)co_k[i];
-            if (b >= 0 && b < (int)(co_len[i] >> 4)) st16(arena + co_off[i] + 16u * (uint32_t)b, v);
-        }
-        wave_lds_sync();  // the next group's staging writes come after these reads
     }
+    if (G) {
+        uint4 co_out[NB];
+#pragma unroll
+        for (int i = 0; i < NB; i++) co_out[i] = lds_ld128(st.coop(i));
+        co_store(G - 1, co_out);
+        wave_lds_sync();  // the next packet pass reuses the staging area
+    }
+#ifdef QPP_LEAN
+    (void)cprev;
+    (void)bprev;
+    ek0 = aes.encrypt<NR>(make_uint4(p.n0, p.n1, p.n2, bswap32(1u)), rk);  // E_K(J0), recomputed: 4 fewer VGPRs
+#else
 #pragma unroll
     for (int j = 0; j < NB; j++)
         if (bprev + j >= 0 && bprev + j < nblk) z = gh.mulx(z, cprev[j]);
+#endif
     if (!has) return;
     // length block: be64(aad bits) || be64(payload bits); tag = Y * H ^ E_K(J0)
     z = gh.mulx(z, make_uint4(0, bswap32(p.aad_len * 8), 0, bswap32(p.len * 8)));
@@ -286,8 +344,12 @@ __device__ __forceinline__ void process_packet(const AesLds &aes, const Ghash &g
             } else {
                 const uint4 smp = ld16(pay + s);
                 const uint32_t hdr_len = p.aad_len - p.pn_len;
+#ifndef QPP_DIAG_NOHP
                 hp_finish<NR == 10 ? 10 : 14>(aes, key->hp_rk, smp, p.base, hdr_len, p.pn_len,
                                               masks + 5 * (size_t)pkt_index, flags);
+#else
+                masks[pkt_index] = (uint8_t)(smp.x ^ hdr_len);
+#endif
             }
         }
         if (status) status[pkt_index] = st;

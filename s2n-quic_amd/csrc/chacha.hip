@@ -180,12 +180,28 @@ __global__ __launch_bounds__(256) void chacha_kernel(const DevKey *__restrict__ 
             v[i] = ld16(arena + co_off[i] + (o < co_len[i] ? o : 0u));
         }
     };
+    // cooperative stores of chunk c-1 go out at the top of iteration c, after chunk c's prefetched loads were
+    // consumed (vmcnt counts loads and stores together: see aes_gcm.hip)
+    auto co_store = [&](uint32_t c, const uint4 (&v)[4]) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const uint32_t o = 16u * (4u * c + co_k[i]);
+            if (o + 16 <= co_len[i]) st16(arena + co_off[i] + o, v[i]);
+        }
+    };
     uint4 cin[4], cb[4];
     co_load(0, cin);
     chacha_block(k, 1, n0, n1, n2, ks);
     for (uint32_t c = 0; c < C; c++) {
+        uint4 co_out[4];
+        if (c) {
+#pragma unroll
+            for (int i = 0; i < 4; i++) co_out[i] = lds_ld128(st.coop(i));
+            wave_lds_sync();
+        }
 #pragma unroll
         for (int i = 0; i < 4; i++) lds_st128(st.coop(i), cin[i]);
+        if (c) co_store(c - 1, co_out);
         wave_lds_sync();
         uint4 in[4];
 #pragma unroll
@@ -205,17 +221,16 @@ __global__ __launch_bounds__(256) void chacha_kernel(const DevKey *__restrict__ 
             }
         }
         wave_lds_sync();
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const uint4 v = lds_ld128(st.coop(i));
-            const uint32_t o = 16u * (4u * c + co_k[i]);
-            if (o + 16 <= co_len[i]) st16(arena + co_off[i] + o, v);
-        }
-        wave_lds_sync();
         chacha_block(k, c + 2, n0, n1, n2, ks);  // next chunk ...
 #pragma unroll
         for (int q = 0; q < 4; q++)
             if (64 * c + 16 * q < len) mac.block(cb[q]);  // ... beside this chunk's MAC
+    }
+    if (C) {
+        uint4 co_out[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) co_out[i] = lds_ld128(st.coop(i));
+        co_store(C - 1, co_out);
     }
     if (!has) return;
     mac.block(make_uint4(aad_len, 0, len, 0));  // le64(aad_len) || le64(ct_len)

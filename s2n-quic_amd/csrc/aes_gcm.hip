@@ -386,7 +386,11 @@ __global__ __launch_bounds__(WG) void aes_gcm_kernel(const DevKey *__restrict__ 
     for (int i = 0; i < 4 * (NR + 1); i++) rk[i] = __builtin_amdgcn_readfirstlane(key->rk[i]);
     Stage<NB> st;
     st.lane = threadIdx.x & 63u;
+#ifdef QPP_DIAG_ALIAS_STAGE  // diagnostic: waves share staging slots (wrong data) so any WG size fits in LDS
+    st.base = kLdsStage + ((threadIdx.x >> 6) % (8 / (NB / 2))) * (64u * 16u * NB);
+#else
     st.base = kLdsStage + (threadIdx.x >> 6) * (64u * 16u * NB);
+#endif
     for (uint32_t t0 = 0; t0 < w.count; t0 += WG) {  // WG < 1024: several passes over the work item
         const uint32_t t = t0 + threadIdx.x;
         const bool real = t < w.count;
@@ -457,9 +461,20 @@ namespace {
 struct Variant {
     int nb, wg, per;
 };
+#ifdef QPP_DIAG_ALIAS_STAGE
+constexpr Variant kVariants[] = {{4, 512, 1024}, {2, 1024, 1024}, {2, 512, 1024}, {4, 256, 1024}, {4, 768, 768}};
+#else
 constexpr Variant kVariants[] = {{4, 512, 1024}, {2, 1024, 1024}, {2, 512, 1024}, {4, 256, 1024}};
+#endif
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
-constexpr uint32_t lds_bytes(int nb, int wg) { return kLdsStage + (uint32_t)(wg / 64) * 1024u * (uint32_t)nb; }
+constexpr uint32_t lds_bytes(int nb, int wg) {
+    const uint32_t b = kLdsStage + (uint32_t)(wg / 64) * 1024u * (uint32_t)nb;
+#ifdef QPP_DIAG_ALIAS_STAGE
+    return b > kLdsMax ? kLdsMax : b;
+#else
+    return b;
+#endif
+}
 
 template <bool SEAL, int NR>
 void launch_variant(int v, dim3 grid, hipStream_t s, const DevKey *keys, const qpp_pkt *descs, const PlanBuffers &pb,
@@ -472,6 +487,9 @@ void launch_variant(int v, dim3 grid, hipStream_t s, const DevKey *keys, const q
         case 1: { QPP_AES_LAUNCH(2, 1024); break; }
         case 2: { QPP_AES_LAUNCH(2, 512); break; }
         case 3: { QPP_AES_LAUNCH(4, 256); break; }
+#ifdef QPP_DIAG_ALIAS_STAGE
+        case 4: { QPP_AES_LAUNCH(4, 768); break; }
+#endif
         default: { QPP_AES_LAUNCH(4, 512); break; }
     }
 #undef QPP_AES_LAUNCH

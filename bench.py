@@ -80,6 +80,7 @@ def main():
                     help="device: seal+open in HBM (headline); e2e: pinned host -> HBM -> host; rx: receive path "
                          "(unprotect -> PN expand -> open); keys: device key schedule (key-update churn)")
     ap.add_argument("--cpu-seconds", type=float, default=1.5)
+    ap.add_argument("--chunks", type=int, default=16, help="e2e: pipeline chunks (H2D / seal+open / D2H overlap)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-hp", action="store_true", help="seal without the HP mask (diagnostic)")
     ap.add_argument("--no-check", action="store_true", help="skip the warmup open-status check (diagnostic builds)")
@@ -193,7 +194,7 @@ def e2e(args, ctx, keys, descs, arena, d_desc, d_mask, d_status, flags, rank, wo
     on the compute stream, D2H on a third, with events between them."""
     n, pt = args.packets, args.pt
     stride = arena.size // n
-    chunks = 8
+    chunks = args.chunks
     per = (n + chunks - 1) // chunks
     h_in = ctx.host_alloc(arena.nbytes)
     h_in[:] = arena

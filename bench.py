@@ -76,7 +76,7 @@ def main():
     ap.add_argument("--pt", type=int, default=1200, help="payload bytes per packet")
     ap.add_argument("--aad", type=int, default=21, help="short header: 0x43 || DCID16 || PN4")
     ap.add_argument("--keys", type=int, default=1)
-    ap.add_argument("--mode", default="device", choices=["device", "e2e", "rx", "keys"],
+    ap.add_argument("--mode", default="device", choices=["device", "e2e", "rx", "keys", "txq"],
                     help="device: seal+open in HBM (headline); e2e: pinned host -> HBM -> host; rx: receive path "
                          "(unprotect -> PN expand -> open); keys: device key schedule (key-update churn)")
     ap.add_argument("--cpu-seconds", type=float, default=1.5)
@@ -108,6 +108,8 @@ def main():
         return rx(args, ctx, keys, descs, arena, d_desc, d_mask, d_status, flags, rank, world, barrier, max_over_ranks)
     if args.mode == "keys":
         return keys_churn(args, ctx, suite, rank, world, barrier, max_over_ranks)
+    if args.mode == "txq":
+        return txq_bursts(args, ctx, keys, rank, world, max_over_ranks)
 
     d_arena = ctx.alloc(arena.nbytes)
     d_arena.upload(arena)
@@ -321,6 +323,35 @@ def keys_churn(args, ctx, suite, rank, world, barrier, max_over_ranks):
             "value": round(args.keys * world / t, 1), "unit": "keys/s", "n_gpus": world, "steps": args.steps,
             "ms_per_step": round(1e3 * t, 3), "suite": args.suite, "keys_per_step": args.keys,
         }), flush=True)
+    ctx.close()
+
+
+def txq_bursts(args, ctx, keys, rank, world, max_over_ranks, burst=64):
+    """GSO-style bursts (BASELINE configs[3]): the transport encodes `burst` packets into the pinned ring and flushes
+    (qpp_txq_flush = H2D + one seal/HP batch + D2H + wait).  Reports the per-flush latency and the burst rate."""
+    pt, aad = args.pt, args.aad
+    stride = ((aad + pt + 16 + 15) // 16) * 16
+    q = qpp.TxQueue(ctx, burst * stride, burst)
+    rng = np.random.default_rng(9)
+    q.ring[:] = rng.integers(0, 256, q.ring.size, dtype=np.uint8)
+    lat = []
+    pn = 1 << 20
+    for k in range(args.warmup + args.steps * 20):
+        for i in range(burst):
+            q.push(keys[i % len(keys)], pn, i * stride, aad - 4, 4, pt)
+            pn += 1
+        t0 = time.perf_counter()
+        q.flush()
+        if k >= args.warmup:
+            lat.append(time.perf_counter() - t0)
+    t = max_over_ranks(float(np.median(lat)))
+    if rank == 0:
+        print(json.dumps({
+            "metric": f"txq flush latency, {burst}-packet GSO burst of {pt} B (pinned ring -> HBM -> ring), median",
+            "value": round(1e6 * t, 1), "unit": "us", "higher_is_better": False, "n_gpus": world,
+            "burst_gib_s": round(burst * pt / t / GiB, 3), "suite": args.suite, "flushes": len(lat),
+        }), flush=True)
+    q.close()
     ctx.close()
 
 

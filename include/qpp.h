@@ -128,7 +128,9 @@ int qpp_hp_mask(const qpp_key *key, const uint8_t *sample, size_t sample_len, ui
 typedef struct qpp_pkt {
     uint64_t pn;       /* full packet number (62-bit) -> Iv::nonce (iv.rs:27-39) */
     uint32_t key_idx;  /* qpp_key_slot() of the key to use */
-    uint32_t off;      /* byte offset of the packet in the arena */
+    uint32_t off;      /* byte offset of the packet in the arena; the whole packet (header, payload, tag) must
+                          lie in [arena, arena + 4 GiB): one batch addresses a 4 GiB window, larger sets of
+                          packets go in several batches (keeps the descriptor at 24 B) */
     uint16_t aad_len;  /* header length including the packet-number bytes */
     uint16_t pt_len;   /* payload length, tag excluded */
     uint8_t pn_len;    /* 1..4 packet-number bytes (header protection) */

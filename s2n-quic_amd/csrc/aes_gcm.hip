@@ -505,13 +505,25 @@ int aes_variant() {
 }
 }  // namespace
 
-uint32_t aes_packets_per_item() { return (uint32_t)kVariants[aes_variant()].per; }
+uint32_t aes_packets_per_item(uint32_t n, uint32_t n_cu) {
+    // rounds of one-workgroup-per-CU residency the batch needs at the variant's item size; then the smallest whole-wave
+    // item size that still fits the batch in that many rounds.  (128 Ki packets at 1024 per item were 128 items on
+    // 256 CUs: half the chip idle, 0.63x the rate of the balanced split.)
+    const uint32_t full = (uint32_t)kVariants[aes_variant()].per;
+    if (!n_cu) return full;
+    const uint64_t slots = (uint64_t)n_cu * full;
+    const uint64_t rounds = (n + slots - 1) / slots;
+    uint64_t per = (n + (uint64_t)n_cu * rounds - 1) / ((uint64_t)n_cu * rounds);
+    per = (per + 63) & ~uint64_t(63);
+    if (per < (uint64_t)kMinPacketsPerItem) per = kMinPacketsPerItem;
+    return per > full ? full : (uint32_t)per;
+}
 
 hipError_t launch_aes_gcm(bool seal, const DevKey *keys, const qpp_pkt *descs, const PlanBuffers &pb, uint32_t n,
-                          uint32_t key_cap, uint8_t *arena, uint8_t *masks, int8_t *status, uint32_t flags,
-                          uint32_t suites, hipStream_t s) {
+                          uint32_t key_cap, uint32_t per, uint8_t *arena, uint8_t *masks, int8_t *status,
+                          uint32_t flags, uint32_t suites, hipStream_t s) {
     if (!n) return hipSuccess;
-    const dim3 grid(plan_max_work(n, key_cap, aes_packets_per_item()));
+    const dim3 grid(plan_max_work(n, key_cap, per));
     const int v = aes_variant();
     if (suites & (1u << QPP_SUITE_TLS_AES_128_GCM_SHA256)) {
         if (seal) launch_variant<true, 10>(v, grid, s, keys, descs, pb, arena, masks, status, flags);

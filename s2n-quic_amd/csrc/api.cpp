@@ -14,6 +14,7 @@ using namespace qpp;
 
 struct qpp_ctx {
     int device = 0;
+    uint32_t n_cu = 0;  // compute units (AES work-item sizing)
     hipStream_t stream = nullptr;
     // device key table + host mirror
     DevKey *d_keys = nullptr;
@@ -207,8 +208,8 @@ int run_one(const qpp_key *k, bool seal, uint64_t pn, const uint8_t *header, siz
         HIP_TRY(ctx, hipMemcpyAsync(ctx->plan1.work, &w, sizeof w, hipMemcpyHostToDevice, s));
         HIP_TRY(ctx, hipMemcpyAsync(ctx->plan1.n_work, &one, 4, hipMemcpyHostToDevice, s));
         // key_cap = 0: grid = plan_max_work(1, 0, per) = 1; only work item 0 exists
-        HIP_TRY(ctx, launch_aes_gcm(seal, ctx->d_keys, ctx->d_desc1, ctx->plan1, 1, 0, ctx->d_stage, ctx->d_mask1,
-                                    ctx->d_status1, 0, 1u << k->suite, s));
+        HIP_TRY(ctx, launch_aes_gcm(seal, ctx->d_keys, ctx->d_desc1, ctx->plan1, 1, 0, 1, ctx->d_stage,
+                                    ctx->d_mask1, ctx->d_status1, 0, 1u << k->suite, s));
     } else {
         HIP_TRY(ctx, launch_chacha(seal, ctx->d_keys, ctx->d_desc1, 1, ctx->d_stage, ctx->d_mask1, ctx->d_status1, 0, s));
     }
@@ -239,6 +240,7 @@ int qpp_ctx_create(int device, qpp_ctx **out) {
     if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return QPP_DEVICE_ERROR;  // kernels are built for gfx950 only
     qpp_ctx *ctx = new qpp_ctx();
     ctx->device = device;
+    ctx->n_cu = (uint32_t)prop.multiProcessorCount;
     int rc = QPP_OK;
     do {
         if (fail(ctx, hipSetDevice(device), "hipSetDevice")) { rc = QPP_DEVICE_ERROR; break; }
@@ -514,9 +516,10 @@ int qpp_seal_batch(qpp_ctx *ctx, const qpp_pkt *descs, size_t n, uint8_t *arena,
     if (!(flags & QPP_ONLY_CHACHA)) {
         rc = ensure_plan(ctx, (uint32_t)n);
         if (rc) return rc;
-        HIP_TRY(ctx, launch_plan(ctx->d_keys, ctx->key_cap, descs, (uint32_t)n, ctx->plan, aes_packets_per_item(), s));
-        HIP_TRY(ctx, launch_aes_gcm(true, ctx->d_keys, descs, ctx->plan, (uint32_t)n, ctx->key_cap, arena, masks, status,
-                                    flags, suite_mask(ctx), s));
+        const uint32_t per = aes_packets_per_item((uint32_t)n, ctx->n_cu);
+        HIP_TRY(ctx, launch_plan(ctx->d_keys, ctx->key_cap, descs, (uint32_t)n, ctx->plan, per, s));
+        HIP_TRY(ctx, launch_aes_gcm(true, ctx->d_keys, descs, ctx->plan, (uint32_t)n, ctx->key_cap, per, arena,
+                                    masks, status, flags, suite_mask(ctx), s));
     }
     if (!(flags & QPP_ONLY_AES))
         HIP_TRY(ctx, launch_chacha(true, ctx->d_keys, descs, (uint32_t)n, arena, masks, status, flags, s));
@@ -535,9 +538,10 @@ int qpp_open_batch(qpp_ctx *ctx, const qpp_pkt *descs, size_t n, uint8_t *arena,
     if (!(flags & QPP_ONLY_CHACHA)) {
         rc = ensure_plan(ctx, (uint32_t)n);
         if (rc) return rc;
-        HIP_TRY(ctx, launch_plan(ctx->d_keys, ctx->key_cap, descs, (uint32_t)n, ctx->plan, aes_packets_per_item(), s));
-        HIP_TRY(ctx, launch_aes_gcm(false, ctx->d_keys, descs, ctx->plan, (uint32_t)n, ctx->key_cap, arena, nullptr,
-                                    status, 0, suite_mask(ctx), s));
+        const uint32_t per = aes_packets_per_item((uint32_t)n, ctx->n_cu);
+        HIP_TRY(ctx, launch_plan(ctx->d_keys, ctx->key_cap, descs, (uint32_t)n, ctx->plan, per, s));
+        HIP_TRY(ctx, launch_aes_gcm(false, ctx->d_keys, descs, ctx->plan, (uint32_t)n, ctx->key_cap, per, arena,
+                                    nullptr, status, 0, suite_mask(ctx), s));
     }
     if (!(flags & QPP_ONLY_AES))
         HIP_TRY(ctx, launch_chacha(false, ctx->d_keys, descs, (uint32_t)n, arena, nullptr, status, 0, s));

@@ -86,7 +86,7 @@ struct WorkItem {
     uint32_t nr;     // AES rounds for this key
 };
 
-constexpr int kMinPacketsPerItem = 256;  // smallest AES work item (sizes plan scratch)
+constexpr int kMinPacketsPerItem = 64;   // smallest AES work item, one wave (sizes plan scratch)
 constexpr int kDefaultAesVariant = 0;  // see aes_gcm.hip launch_variant
 constexpr int kMaxPlanKeys = 8192;      // keys binned in LDS by the plan kernels (larger tables: global bins)
 
@@ -109,11 +109,13 @@ uint32_t key_material_bytes();
 hipError_t launch_plan(const DevKey *keys, uint32_t key_cap, const qpp_pkt *descs, uint32_t n, PlanBuffers pb,
                        uint32_t per, hipStream_t s);
 uint32_t plan_max_work(uint32_t n, uint32_t key_cap, uint32_t per);
-uint32_t aes_packets_per_item();  // work-item size of the selected AES-GCM kernel variant
+// AES work-item size for an n-packet batch on n_cu compute units: the selected variant's size, shrunk (in whole
+// waves) so that the work items fill every CU in balanced rounds when n is small (one workgroup per CU).
+uint32_t aes_packets_per_item(uint32_t n, uint32_t n_cu);
 // suites: bit (1 << suite) for every suite with a live key in the context (launches only what can occur)
 hipError_t launch_aes_gcm(bool seal, const DevKey *keys, const qpp_pkt *descs, const PlanBuffers &pb, uint32_t n,
-                          uint32_t key_cap, uint8_t *arena, uint8_t *masks, int8_t *status, uint32_t flags,
-                          uint32_t suites, hipStream_t s);
+                          uint32_t key_cap, uint32_t per, uint8_t *arena, uint8_t *masks, int8_t *status,
+                          uint32_t flags, uint32_t suites, hipStream_t s);
 hipError_t launch_chacha(bool seal, const DevKey *keys, const qpp_pkt *descs, uint32_t n, uint8_t *arena,
                          uint8_t *masks, int8_t *status, uint32_t flags, hipStream_t s);
 // receive side: remove header protection, expand the PN, choose the key by key phase -> descs_out (chacha.hip)

@@ -386,6 +386,9 @@ def make_batch(n, pt_len, key_slots, seed, aad_len=21, pn_len=4, pn_base=0, stri
     when mixed, else key_slots[0].  Returns (descs, arena).
     """
     stride = stride or ((aad_len + pt_len + 16 + 15) // 16) * 16
+    if n * stride > 1 << 32:
+        raise ValueError(f"{n} x {stride} B exceeds the 4 GiB arena window of one batch (qpp_pkt.off is 32-bit); "
+                         "split the batch")
     arena = xoshiro_bytes(seed, n * stride)
     descs = np.zeros(n, dtype=PKT_DTYPE)
     idx = np.arange(n, dtype=np.uint64)

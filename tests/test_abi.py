@@ -56,3 +56,9 @@ def test_synthetic_batch_layout():
     assert set(np.unique(descs["key_idx"])) <= {3, 7} and len(np.unique(descs["key_idx"])) == 2
     assert (arena.reshape(64, 1248)[:, 0] == 0x43).all()
     assert descs["pn"][5] == 5
+
+
+def test_batch_arena_window_is_4gib():
+    # qpp_pkt.off is 32-bit: one batch addresses a 4 GiB arena window (include/qpp.h); larger sets are split
+    with pytest.raises(ValueError):
+        qpp.make_batch(4 << 20, 1200, [0], seed=1)

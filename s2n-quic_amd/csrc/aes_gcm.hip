@@ -128,56 +128,6 @@ __device__ void build_tables(const DevKey *__restrict__ key) {
     __syncthreads();
 }
 
-struct PacketView {
-    uint8_t *base;       // packet start (AAD)
-    uint32_t aad_len, len, pn_len;
-    uint32_t n0, n1, n2; // nonce words
-};
-
-__device__ __forceinline__ PacketView load_packet(const qpp_pkt &d, const DevKey *__restrict__ key, uint8_t *arena) {
-    PacketView p;
-    p.base = arena + d.off;
-    p.aad_len = d.aad_len;
-    p.len = d.pt_len;
-    p.pn_len = d.pn_len;
-    // Iv::nonce: iv XOR (0u32 || pn_be64)  (src/iv.rs:27-39)
-    p.n0 = key->iv[0];
-    p.n1 = key->iv[1] ^ bswap32((uint32_t)(d.pn >> 32));
-    p.n2 = key->iv[2] ^ bswap32((uint32_t)d.pn);
-    return p;
-}
-
-// Header protection mask from the 16-byte sample (first 5 bytes of AES_hp(sample)).  The HP round keys are read
-// here, once per packet, into VGPRs: hoisted into SGPRs for the whole kernel they pushed the packet round keys out
-// of SGPRs (measured: 36 SGPR spills and per-iteration round-key reloads, a slower seal).
-template <int HNR>
-__device__ __forceinline__ void hp_finish(const AesLds &aes, const uint32_t *hp_rk_g, uint4 sample,
-                                          uint8_t *base, uint32_t hdr_len, uint32_t pn_len, uint8_t *mask_out,
-                                          uint32_t flags) {
-    // launder the pointer through a VGPR: the loads below cannot be hoisted or kept in SGPRs
-    uint64_t a = (uint64_t)hp_rk_g;
-    asm volatile("" : "+v"(a));
-    const uint4 *src = (const uint4 *)a;
-    uint32_t hp_rk[4 * (HNR + 1)];
-#pragma unroll
-    for (int i = 0; i < HNR + 1; i++) {
-        const uint4 v = src[i];
-        hp_rk[4 * i] = v.x; hp_rk[4 * i + 1] = v.y; hp_rk[4 * i + 2] = v.z; hp_rk[4 * i + 3] = v.w;
-    }
-    uint4 m = aes.encrypt<HNR>(sample, hp_rk);
-    if (flags & QPP_HP_MASK_OUT) {
-        mask_out[0] = (uint8_t)m.x; mask_out[1] = (uint8_t)(m.x >> 8); mask_out[2] = (uint8_t)(m.x >> 16);
-        mask_out[3] = (uint8_t)(m.x >> 24); mask_out[4] = (uint8_t)m.y;
-    }
-    if (flags & QPP_HP_APPLY) {
-        // header_crypto.rs:80-95
-        uint8_t b0 = base[0];
-        base[0] = b0 ^ ((uint8_t)m.x & ((b0 & 0x80) ? 0x0f : 0x1f));
-        uint32_t mm = (m.x >> 8) | (m.y << 24);
-        for (uint32_t i = 0; i < pn_len; i++) base[hdr_len + i] ^= (uint8_t)(mm >> (8 * i));
-    }
-}
-
 // GHASH over the AAD (zero-padded to 16 bytes), as the pending (rotated) Z of the chain.
 __device__ __forceinline__ uint4 ghash_aad_w(const Ghash &gh, const uint8_t *aad, uint32_t aad_len) {
     uint4 w = make_uint4(0, 0, 0, 0);

@@ -15,6 +15,7 @@ using namespace qpp;
 struct qpp_ctx {
     int device = 0;
     uint32_t n_cu = 0;  // compute units (AES work-item sizing)
+    uint32_t burst_max = kBurstMaxDefault;  // AES batches up to this size take the wave-per-packet kernel
     hipStream_t stream = nullptr;
     // device key table + host mirror
     DevKey *d_keys = nullptr;
@@ -208,8 +209,10 @@ int run_one(const qpp_key *k, bool seal, uint64_t pn, const uint8_t *header, siz
         HIP_TRY(ctx, hipMemcpyAsync(ctx->plan1.work, &w, sizeof w, hipMemcpyHostToDevice, s));
         HIP_TRY(ctx, hipMemcpyAsync(ctx->plan1.n_work, &one, 4, hipMemcpyHostToDevice, s));
         // key_cap = 0: grid = plan_max_work(1, 0, per) = 1; only work item 0 exists
-        HIP_TRY(ctx, launch_aes_gcm(seal, ctx->d_keys, ctx->d_desc1, ctx->plan1, 1, 0, 1, ctx->d_stage,
-                                    ctx->d_mask1, ctx->d_status1, 0, 1u << k->suite, s));
+        HIP_TRY(ctx, (ctx->burst_max ? launch_aes_gcm_burst : launch_aes_gcm)(seal, ctx->d_keys, ctx->d_desc1,
+                                                                             ctx->plan1, 1, 0, 1, ctx->d_stage,
+                                                                             ctx->d_mask1, ctx->d_status1, 0,
+                                                                             1u << k->suite, s));
     } else {
         HIP_TRY(ctx, launch_chacha(seal, ctx->d_keys, ctx->d_desc1, 1, ctx->d_stage, ctx->d_mask1, ctx->d_status1, 0, s));
     }
@@ -241,6 +244,7 @@ int qpp_ctx_create(int device, qpp_ctx **out) {
     qpp_ctx *ctx = new qpp_ctx();
     ctx->device = device;
     ctx->n_cu = (uint32_t)prop.multiProcessorCount;
+    if (const char *e = getenv("QPP_BURST_MAX")) ctx->burst_max = (uint32_t)strtoul(e, nullptr, 10);
     int rc = QPP_OK;
     do {
         if (fail(ctx, hipSetDevice(device), "hipSetDevice")) { rc = QPP_DEVICE_ERROR; break; }
@@ -258,6 +262,12 @@ int qpp_ctx_create(int device, qpp_ctx **out) {
         return rc;
     }
     *out = ctx;
+    return QPP_OK;
+}
+
+int qpp_ctx_set_burst_max(qpp_ctx *ctx, size_t max_packets) {
+    if (!ctx) return QPP_INTERNAL_ERROR;
+    ctx->burst_max = max_packets > UINT32_MAX ? UINT32_MAX : (uint32_t)max_packets;
     return QPP_OK;
 }
 
@@ -516,10 +526,13 @@ int qpp_seal_batch(qpp_ctx *ctx, const qpp_pkt *descs, size_t n, uint8_t *arena,
     if (!(flags & QPP_ONLY_CHACHA)) {
         rc = ensure_plan(ctx, (uint32_t)n);
         if (rc) return rc;
-        const uint32_t per = aes_packets_per_item((uint32_t)n, ctx->n_cu);
+        const bool burst = n <= ctx->burst_max;
+        const uint32_t per = burst ? burst_packets_per_item((uint32_t)n, ctx->n_cu)
+                                   : aes_packets_per_item((uint32_t)n, ctx->n_cu);
         HIP_TRY(ctx, launch_plan(ctx->d_keys, ctx->key_cap, descs, (uint32_t)n, ctx->plan, per, s));
-        HIP_TRY(ctx, launch_aes_gcm(true, ctx->d_keys, descs, ctx->plan, (uint32_t)n, ctx->key_cap, per, arena,
-                                    masks, status, flags, suite_mask(ctx), s));
+        HIP_TRY(ctx, (burst ? launch_aes_gcm_burst : launch_aes_gcm)(true, ctx->d_keys, descs, ctx->plan, (uint32_t)n,
+                                                                    ctx->key_cap, per, arena, masks, status, flags,
+                                                                    suite_mask(ctx), s));
     }
     if (!(flags & QPP_ONLY_AES))
         HIP_TRY(ctx, launch_chacha(true, ctx->d_keys, descs, (uint32_t)n, arena, masks, status, flags, s));
@@ -538,10 +551,13 @@ int qpp_open_batch(qpp_ctx *ctx, const qpp_pkt *descs, size_t n, uint8_t *arena,
     if (!(flags & QPP_ONLY_CHACHA)) {
         rc = ensure_plan(ctx, (uint32_t)n);
         if (rc) return rc;
-        const uint32_t per = aes_packets_per_item((uint32_t)n, ctx->n_cu);
+        const bool burst = n <= ctx->burst_max;
+        const uint32_t per = burst ? burst_packets_per_item((uint32_t)n, ctx->n_cu)
+                                   : aes_packets_per_item((uint32_t)n, ctx->n_cu);
         HIP_TRY(ctx, launch_plan(ctx->d_keys, ctx->key_cap, descs, (uint32_t)n, ctx->plan, per, s));
-        HIP_TRY(ctx, launch_aes_gcm(false, ctx->d_keys, descs, ctx->plan, (uint32_t)n, ctx->key_cap, per, arena,
-                                    nullptr, status, 0, suite_mask(ctx), s));
+        HIP_TRY(ctx, (burst ? launch_aes_gcm_burst : launch_aes_gcm)(false, ctx->d_keys, descs, ctx->plan, (uint32_t)n,
+                                                                    ctx->key_cap, per, arena, nullptr, status, 0,
+                                                                    suite_mask(ctx), s));
     }
     if (!(flags & QPP_ONLY_AES))
         HIP_TRY(ctx, launch_chacha(false, ctx->d_keys, descs, (uint32_t)n, arena, nullptr, status, 0, s));
@@ -684,6 +700,16 @@ struct qpp_txq {
     qpp_pkt *h_desc = nullptr, *d_desc = nullptr;
     size_t count = 0, lo = SIZE_MAX, hi = 0;
     uint32_t suites = 0;
+    // zero-copy flush of small bursts: the kernels read and write the pinned ring, descriptors and a host-built
+    // plan directly over PCIe (no DMA copies, no plan launches); device views of the pinned buffers
+    uint32_t zc_max = 0;
+    uint32_t *h_perm = nullptr;  // pinned: perm[max_packets] | n_work | WorkItem work[max_packets + 1]
+    WorkItem *h_work = nullptr;
+    uint32_t *h_nwork = nullptr;
+    uint8_t *v_ring = nullptr;
+    qpp_pkt *v_desc = nullptr;
+    PlanBuffers v_plan{};
+    std::vector<uint32_t> order;
 };
 
 extern "C" {
@@ -699,10 +725,26 @@ int qpp_txq_create(qpp_ctx *ctx, size_t ring_bytes, size_t max_packets, qpp_txq 
     if (fail(ctx, hipHostMalloc(&q->h_ring, ring_bytes, hipHostMallocDefault), "txq ring") ||
         fail(ctx, hipMalloc(&q->d_ring, ring_bytes), "txq ring") ||
         fail(ctx, hipHostMalloc(&q->h_desc, sizeof(qpp_pkt) * max_packets, hipHostMallocDefault), "txq descs") ||
-        fail(ctx, hipMalloc(&q->d_desc, sizeof(qpp_pkt) * max_packets), "txq descs")) {
+        fail(ctx, hipMalloc(&q->d_desc, sizeof(qpp_pkt) * max_packets), "txq descs") ||
+        fail(ctx, hipHostMalloc(&q->h_perm, 4 * (max_packets + 4) + sizeof(WorkItem) * (max_packets + 1),
+                                hipHostMallocDefault), "txq plan")) {
         qpp_txq_destroy(q);
         return QPP_DEVICE_ERROR;
     }
+    q->h_nwork = q->h_perm + max_packets;
+    q->h_work = (WorkItem *)(q->h_perm + max_packets + 4);  // 16-byte aligned
+    void *v = nullptr;
+    if (fail(ctx, hipHostGetDevicePointer(&v, q->h_ring, 0), "txq ring view")) { qpp_txq_destroy(q); return QPP_DEVICE_ERROR; }
+    q->v_ring = (uint8_t *)v;
+    if (fail(ctx, hipHostGetDevicePointer(&v, q->h_desc, 0), "txq desc view")) { qpp_txq_destroy(q); return QPP_DEVICE_ERROR; }
+    q->v_desc = (qpp_pkt *)v;
+    if (fail(ctx, hipHostGetDevicePointer(&v, q->h_perm, 0), "txq plan view")) { qpp_txq_destroy(q); return QPP_DEVICE_ERROR; }
+    q->v_plan.perm = (uint32_t *)v;
+    q->v_plan.n_work = q->v_plan.perm + max_packets;
+    q->v_plan.work = (WorkItem *)(q->v_plan.perm + max_packets + 4);
+    q->zc_max = kTxqZeroCopyMax;
+    if (const char *e = getenv("QPP_TXQ_ZC_MAX")) q->zc_max = (uint32_t)strtoul(e, nullptr, 10);
+    q->order.reserve(max_packets);
     memset(q->h_ring, 0, ring_bytes);
     *out = q;
     return QPP_OK;
@@ -716,6 +758,7 @@ void qpp_txq_destroy(qpp_txq *q) {
     if (q->d_ring) { hipMemset(q->d_ring, 0, q->ring_bytes); hipFree(q->d_ring); }
     if (q->h_desc) hipHostFree(q->h_desc);
     if (q->d_desc) hipFree(q->d_desc);
+    if (q->h_perm) hipHostFree(q->h_perm);
     delete q;
 }
 
@@ -744,23 +787,65 @@ int qpp_txq_push(qpp_txq *q, const qpp_key *key, uint64_t pn, size_t off, size_t
     return QPP_OK;
 }
 
+// Zero-copy flush: host plan (AES packets grouped by key, work items of whole waves) in pinned memory, then the
+// burst kernel (AES) and the ChaCha kernel on the pinned ring itself; one launch per suite family, one sync.
+static int txq_flush_zero_copy(qpp_txq *q, hipStream_t s) {
+    qpp_ctx *ctx = q->ctx;
+    const uint32_t aes = (1u << QPP_SUITE_TLS_AES_128_GCM_SHA256) | (1u << QPP_SUITE_TLS_AES_256_GCM_SHA384);
+    const uint32_t n = (uint32_t)q->count;
+    if (q->suites & aes) {
+        std::vector<uint32_t> &ord = q->order;
+        ord.clear();
+        for (uint32_t i = 0; i < n; i++)
+            if (is_aes(ctx->h_keys[q->h_desc[i].key_idx].suite)) ord.push_back(i);
+        std::stable_sort(ord.begin(), ord.end(),
+                         [q](uint32_t a, uint32_t b) { return q->h_desc[a].key_idx < q->h_desc[b].key_idx; });
+        const uint32_t per = burst_packets_per_item((uint32_t)ord.size(), ctx->n_cu);
+        uint32_t items = 0, keys = 0;
+        for (uint32_t i = 0; i < ord.size();) {
+            const uint32_t slot = q->h_desc[ord[i]].key_idx;
+            uint32_t j = i;
+            while (j < ord.size() && q->h_desc[ord[j]].key_idx == slot) j++;
+            for (uint32_t b = i; b < j; b += per)
+                q->h_work[items++] = WorkItem{slot, b, std::min(per, j - b), ctx->h_keys[slot].nr};
+            keys++;
+            i = j;
+        }
+        std::copy(ord.begin(), ord.end(), q->h_perm);
+        *q->h_nwork = items;
+        HIP_TRY(ctx, launch_aes_gcm_burst(true, ctx->d_keys, q->v_desc, q->v_plan, (uint32_t)ord.size(), keys, per,
+                                          q->v_ring, nullptr, nullptr, QPP_HP_APPLY, q->suites & aes, s));
+    }
+    if (q->suites & ~aes)
+        HIP_TRY(ctx, launch_chacha(true, ctx->d_keys, q->v_desc, n, q->v_ring, nullptr, nullptr, QPP_HP_APPLY, s));
+    HIP_TRY(ctx, hipStreamSynchronize(s));
+    return QPP_OK;
+}
+
 int qpp_txq_flush(qpp_txq *q) {
     if (!q) return QPP_INTERNAL_ERROR;
     if (!q->count) return QPP_OK;
     qpp_ctx *ctx = q->ctx;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream;
-    const size_t span = q->hi - q->lo;
-    HIP_TRY(ctx, hipMemcpyAsync(q->d_ring + q->lo, q->h_ring + q->lo, span, hipMemcpyHostToDevice, s));
-    HIP_TRY(ctx, hipMemcpyAsync(q->d_desc, q->h_desc, sizeof(qpp_pkt) * q->count, hipMemcpyHostToDevice, s));
-    const uint32_t aes = (1u << QPP_SUITE_TLS_AES_128_GCM_SHA256) | (1u << QPP_SUITE_TLS_AES_256_GCM_SHA384);
-    uint32_t flags = QPP_HP_APPLY;
-    if (!(q->suites & ~aes)) flags |= QPP_ONLY_AES;
-    else if (!(q->suites & aes)) flags |= QPP_ONLY_CHACHA;
-    int rc = qpp_seal_batch(ctx, q->d_desc, q->count, q->d_ring, nullptr, nullptr, flags, s);
+    int rc = flush_keys(ctx, s);
     if (rc) return rc;
-    HIP_TRY(ctx, hipMemcpyAsync(q->h_ring + q->lo, q->d_ring + q->lo, span, hipMemcpyDeviceToHost, s));
-    HIP_TRY(ctx, hipStreamSynchronize(s));
+    if (q->count <= q->zc_max) {
+        rc = txq_flush_zero_copy(q, s);
+    } else {
+        const size_t span = q->hi - q->lo;
+        HIP_TRY(ctx, hipMemcpyAsync(q->d_ring + q->lo, q->h_ring + q->lo, span, hipMemcpyHostToDevice, s));
+        HIP_TRY(ctx, hipMemcpyAsync(q->d_desc, q->h_desc, sizeof(qpp_pkt) * q->count, hipMemcpyHostToDevice, s));
+        const uint32_t aes = (1u << QPP_SUITE_TLS_AES_128_GCM_SHA256) | (1u << QPP_SUITE_TLS_AES_256_GCM_SHA384);
+        uint32_t flags = QPP_HP_APPLY;
+        if (!(q->suites & ~aes)) flags |= QPP_ONLY_AES;
+        else if (!(q->suites & aes)) flags |= QPP_ONLY_CHACHA;
+        rc = qpp_seal_batch(ctx, q->d_desc, q->count, q->d_ring, nullptr, nullptr, flags, s);
+        if (rc) return rc;
+        HIP_TRY(ctx, hipMemcpyAsync(q->h_ring + q->lo, q->d_ring + q->lo, span, hipMemcpyDeviceToHost, s));
+        HIP_TRY(ctx, hipStreamSynchronize(s));
+    }
+    if (rc) return rc;
     q->count = 0;
     q->lo = SIZE_MAX;
     q->hi = 0;

@@ -1,0 +1,235 @@
+// burst.hip — small-batch AES-128/256-GCM seal/open (+ AES header protection) for gfx950: one WAVE per packet.
+//
+// Same operations and outputs as aes_gcm.hip (seal_in_place_scatter / open_in_place, src/aead/default.rs:44-93;
+// HeaderKey::header_protection_mask, src/header_key.rs:52-56), for the batches the transport actually flushes:
+// a GSO burst is at most 64 packets (quic/s2n-quic-platform/src/features/gso.rs:86).  The lane-per-packet kernel
+// needs ~10^5 packets to fill the chip and takes one lane's serial time per packet (~135 us for 1200 B: 77 blocks
+// x 10 dependent LDS rounds); here the 64 lanes of a wave split one packet's blocks, so a burst costs a few AES
+// round chains instead.
+//
+// GHASH in parallel.  The packet's blocks X_0 .. X_{m-1} (AAD, ciphertext, length block) are front-padded with
+// zeros to 64 K blocks (leading zeros do not change a Horner sum), lane l takes blocks l, l + 64, ...:
+//   Y = sum_j X'_j H^(64K - j) = H * sum_l acc_l H^(63 - l),   acc_l = Horner over the lane's blocks with H^64,
+// and the lane sum is a 6-level tree whose level t multiplies the left half by H^(2^t).  All multiplications are
+// by one of 7 fixed powers P_t = H^(2^t), t = 0..6, each through a 4-bit table per nibble position
+// (T_t[pos][nib] = (nib at nibble pos) * P_t, 32 x 16 x 16 B = 8 KiB): 32 ds_read_b128 per product, and every
+// lane of a step reads the same 256-byte row, so the 16 nibble values sit in 16 distinct bank quads (no conflicts).
+// T_0 comes from the key record's V[m] = H x^m; T_{t+1}[e] = T_t[e] * P_t through T_t.
+//
+// LDS (dynamic, offsets): [0, 64 KiB) AES T0/T1 bank-replicated (as aes_gcm.hip); [64, 120 KiB) T_0 .. T_6.
+#include "device_common.h"
+
+namespace qpp {
+namespace {
+using namespace dev;
+
+constexpr uint32_t kBurstAes = 0;
+constexpr uint32_t kBurstGh = 65536;
+constexpr uint32_t kBurstTab = 8192;
+constexpr uint32_t kBurstLds = kBurstGh + 7 * kBurstTab;  // 120 KiB: one workgroup per CU
+constexpr int kBurstWG = 256;                             // 4 waves = 4 packets in flight per CU
+static_assert(kBurstLds <= kLdsMax, "LDS budget");
+
+__device__ __forceinline__ uint32_t tab(int t) { return kBurstGh + (uint32_t)t * kBurstTab; }
+
+// Z * P_t through T_t: nibble pos 2k = high nibble of byte k, 2k + 1 = its low nibble (GCM bit order: the byte's
+// 0x80 bit is the lowest power of x).
+__device__ __forceinline__ uint4 gmul(uint32_t base, uint4 z) {
+    const uint32_t w[4] = {z.x, z.y, z.z, z.w};
+    uint4 acc[4];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const uint32_t byte = w[k >> 2] >> (8 * (k & 3));
+        const uint4 hi = lds_ld128(base + 512u * k + (byte & 0xf0u));
+        const uint4 lo = lds_ld128(base + 512u * k + 256u + ((byte & 0x0fu) << 4));
+        acc[k & 3] = k < 4 ? hi ^ lo : xor3(acc[k & 3], hi, lo);
+    }
+    return xor3(acc[0], acc[1], acc[2] ^ acc[3]);
+}
+
+// AES tables + T_0 .. T_6 for one key.  All threads take part; ends with a barrier.
+__device__ void burst_tables(const DevKey *__restrict__ key) {
+    build_aes_tables(kBurstAes);
+    const uint4 *V = (const uint4 *)key->V;
+    for (uint32_t e = threadIdx.x; e < 512; e += blockDim.x) {
+        const uint32_t pos = e >> 4, nib = e & 15u;
+        uint4 acc = make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < 4; j++)  // nibble bit j <-> GCM bit index 4 pos + 3 - j
+            if ((nib >> j) & 1u) acc = acc ^ V[4 * pos + 3 - j];
+        lds_st128(tab(0) + 16u * e, acc);
+    }
+    __syncthreads();
+    for (int t = 0; t < 6; t++) {
+        for (uint32_t e = threadIdx.x; e < 512; e += blockDim.x)
+            lds_st128(tab(t + 1) + 16u * e, gmul(tab(t), lds_ld128(tab(t) + 16u * e)));
+        __syncthreads();
+    }
+}
+
+__device__ __forceinline__ uint4 shfl4(uint4 v, int src) {
+    return make_uint4((uint32_t)__shfl((int)v.x, src, 64), (uint32_t)__shfl((int)v.y, src, 64),
+                      (uint32_t)__shfl((int)v.z, src, 64), (uint32_t)__shfl((int)v.w, src, 64));
+}
+__device__ __forceinline__ uint4 shfl4_down(uint4 v, unsigned d) {
+    return make_uint4((uint32_t)__shfl_down((int)v.x, d, 64), (uint32_t)__shfl_down((int)v.y, d, 64),
+                      (uint32_t)__shfl_down((int)v.z, d, 64), (uint32_t)__shfl_down((int)v.w, d, 64));
+}
+__device__ __forceinline__ uint32_t byte_of(uint4 v, uint32_t i) {  // byte i (< 16) of v
+    const uint32_t w = i < 4 ? v.x : i < 8 ? v.y : i < 12 ? v.z : v.w;
+    return (w >> (8 * (i & 3))) & 0xffu;
+}
+
+// One packet on one wave (all 64 lanes; d is wave-uniform).
+template <int NR, bool SEAL>
+__device__ __forceinline__ void burst_packet(const AesLds &aes, const DevKey *__restrict__ key,
+                                             const uint32_t *__restrict__ rk, const qpp_pkt &d, uint32_t pi,
+                                             uint8_t *arena, uint8_t *masks, int8_t *status, uint32_t flags) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const PacketView p = load_packet(d, key, arena);
+    uint8_t *pay = p.base + p.aad_len;
+    const uint32_t a = (p.aad_len + 15u) >> 4, c = (p.len + 15u) >> 4, m = a + c + 1;
+    const uint32_t K = (m + 63u) >> 6, pad = 64u * K - m;
+    uint4 acc = make_uint4(0, 0, 0, 0), ct0 = acc, ct1 = acc;  // ct0/ct1: ciphertext blocks 0/1 where owned
+    for (uint32_t k = 0; k < K; k++) {
+        const int i = (int)(lane + 64u * k) - (int)pad;  // block index in the GHASH sequence
+        uint4 x = make_uint4(0, 0, 0, 0);
+        if (i >= 0 && i < (int)a) {
+            const uint32_t off = 16u * (uint32_t)i;
+            x = ld16(p.base + off);
+            if (p.aad_len - off < 16u) x = keep_bytes(x, p.aad_len - off);
+        } else if (i >= (int)a && i < (int)(a + c)) {
+            const uint32_t b = (uint32_t)i - a, r = p.len - 16u * b;  // data block b uses counter b + 2
+            const uint4 ks = aes.encrypt<NR>(make_uint4(p.n0, p.n1, p.n2, bswap32(b + 2u)), rk);
+            uint4 in = ld16(pay + 16u * b);
+            uint4 out = in ^ ks;
+            if (r >= 16u) {
+                st16(pay + 16u * b, out);
+            } else {
+                out = keep_bytes(out, r);
+                in = keep_bytes(in, r);
+                st_bytes(pay + 16u * b, out, r);
+            }
+            x = SEAL ? out : in;
+            if (b == 0) ct0 = x;
+            if (b == 1) ct1 = x;
+        } else if (i == (int)m - 1) {
+            x = make_uint4(0, bswap32(p.aad_len * 8u), 0, bswap32(p.len * 8u));  // be64 bit lengths
+        }
+        acc = k ? gmul(tab(6), acc) ^ x : x;
+    }
+    // lane tree: level t combines lanes l and l + 2^t (l a multiple of 2^(t+1)) as v_l * H^(2^t) ^ v_(l+2^t)
+#pragma unroll
+    for (int t = 0; t < 6; t++) acc = gmul(tab(t), acc) ^ shfl4_down(acc, 1u << t);
+    const uint4 ek0 = aes.encrypt<NR>(make_uint4(p.n0, p.n1, p.n2, bswap32(1u)), rk);  // E_K(J0)
+    const uint4 tag = shfl4(gmul(tab(0), acc), 0) ^ ek0;                                 // Y = Q * H, from lane 0
+
+    if (SEAL) {
+        if (lane == 0) st16(pay + p.len, tag);
+        int8_t st = QPP_OK;
+        if (flags & (QPP_HP_MASK_OUT | QPP_HP_APPLY)) {
+            // sample = (ciphertext || tag)[4 - pn_len, 20 - pn_len)  (payload.rs:151-169), from registers
+            const uint32_t s = 4u - p.pn_len;
+            if (p.pn_len < 1 || p.pn_len > 4 || p.len < s) {
+                st = QPP_DECODE_ERROR;
+            } else {
+                const uint32_t o0 = (pad + a) & 63u;
+                const uint4 c0 = shfl4(ct0, (int)o0), c1 = shfl4(ct1, (int)((o0 + 1u) & 63u));
+                uint4 smp;
+                if (p.len >= s + 16u) {  // the sample lies in ciphertext blocks 0 and 1
+                    smp = make_uint4(__builtin_amdgcn_alignbyte(c0.y, c0.x, s), __builtin_amdgcn_alignbyte(c0.z, c0.y, s),
+                                     __builtin_amdgcn_alignbyte(c0.w, c0.z, s), __builtin_amdgcn_alignbyte(c1.x, c0.w, s));
+                } else {  // short payload: the sample runs into the tag
+                    uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+                    for (uint32_t q = 0; q < 16; q++) {
+                        const uint32_t pos = s + q;
+                        const uint32_t v = pos < p.len ? (pos < 16u ? byte_of(c0, pos) : byte_of(c1, pos - 16u))
+                                                       : byte_of(tag, pos - p.len);
+                        w[q >> 2] |= v << (8 * (q & 3));
+                    }
+                    smp = make_uint4(w[0], w[1], w[2], w[3]);
+                }
+                if (lane == 0)
+                    hp_finish<NR == 10 ? 10 : 14>(aes, key->hp_rk, smp, p.base, p.aad_len - p.pn_len, p.pn_len,
+                                                  masks + 5 * (size_t)pi, flags);
+            }
+        }
+        if (status && lane == 0) status[pi] = st;
+    } else {
+        const uint4 want = ld16(pay + p.len);
+        const uint4 diff = tag ^ want;
+        const bool ok = (diff.x | diff.y | diff.z | diff.w) == 0;  // all 16 bytes compared, no early exit
+        if (!ok) {
+            // never release unauthenticated plaintext: each lane zeroes the blocks it wrote (same-lane order)
+            for (uint32_t k = 0; k < K; k++) {
+                const int i = (int)(lane + 64u * k) - (int)pad;
+                if (i >= (int)a && i < (int)(a + c)) {
+                    const uint32_t b = (uint32_t)i - a, r = p.len - 16u * b;
+                    if (r >= 16u) st16(pay + 16u * b, make_uint4(0, 0, 0, 0));
+                    else st_bytes(pay + 16u * b, make_uint4(0, 0, 0, 0), r);
+                }
+            }
+        }
+        if (lane == 0) status[pi] = ok ? QPP_OK : QPP_DECRYPT_ERROR;
+    }
+}
+
+template <bool SEAL, int NR>
+__global__ __launch_bounds__(kBurstWG) void aes_gcm_burst_kernel(const DevKey *__restrict__ keys,
+                                                                  const qpp_pkt *__restrict__ descs,
+                                                                  const uint32_t *__restrict__ perm,
+                                                                  const WorkItem *__restrict__ work,
+                                                                  const uint32_t *__restrict__ n_work,
+                                                                  uint8_t *__restrict__ arena, uint8_t *masks,
+                                                                  int8_t *status, uint32_t flags) {
+    if (blockIdx.x >= *n_work) return;  // uniform: grid is sized for the worst case
+    const WorkItem w = work[blockIdx.x];
+    if (w.nr != NR) return;
+    const DevKey *__restrict__ key = keys + w.key;
+    burst_tables(key);
+    const AesLds aes = make_aes(kBurstAes);
+    uint32_t rk[4 * (NR + 1)];
+#pragma unroll
+    for (int i = 0; i < 4 * (NR + 1); i++) rk[i] = __builtin_amdgcn_readfirstlane(key->rk[i]);
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    for (uint32_t q = wave; q < w.count; q += kBurstWG / 64) {
+        const uint32_t pi = perm[w.begin + q];
+        const qpp_pkt d = descs[pi];
+        if (d.flags & QPP_PKT_SKIP) continue;
+        burst_packet<NR, SEAL>(aes, key, rk, d, pi, arena, masks, status, flags);
+    }
+}
+
+template <bool SEAL, int NR>
+void launch_burst(dim3 grid, hipStream_t s, const DevKey *keys, const qpp_pkt *descs, const PlanBuffers &pb,
+                  uint8_t *arena, uint8_t *masks, int8_t *status, uint32_t flags) {
+    hipLaunchKernelGGL((aes_gcm_burst_kernel<SEAL, NR>), grid, dim3(kBurstWG), kBurstLds, s, keys, descs, pb.perm,
+                       pb.work, pb.n_work, arena, masks, status, flags);
+}
+}  // namespace
+
+uint32_t burst_packets_per_item(uint32_t n, uint32_t n_cu) {
+    // whole waves (4 per workgroup), enough items to spread the batch over every CU, at most 64 packets per item
+    uint32_t per = n_cu ? (n + n_cu - 1) / n_cu : 64u;
+    per = (per + 3u) & ~3u;
+    return per < 4u ? 4u : per > 64u ? 64u : per;
+}
+
+hipError_t launch_aes_gcm_burst(bool seal, const DevKey *keys, const qpp_pkt *descs, const PlanBuffers &pb,
+                                uint32_t n, uint32_t key_cap, uint32_t per, uint8_t *arena, uint8_t *masks,
+                                int8_t *status, uint32_t flags, uint32_t suites, hipStream_t s) {
+    if (!n) return hipSuccess;
+    const dim3 grid(plan_max_work(n, key_cap, per));
+    if (suites & (1u << QPP_SUITE_TLS_AES_128_GCM_SHA256)) {
+        if (seal) launch_burst<true, 10>(grid, s, keys, descs, pb, arena, masks, status, flags);
+        else launch_burst<false, 10>(grid, s, keys, descs, pb, arena, masks, status, flags);
+    }
+    if (suites & (1u << QPP_SUITE_TLS_AES_256_GCM_SHA384)) {
+        if (seal) launch_burst<true, 14>(grid, s, keys, descs, pb, arena, masks, status, flags);
+        else launch_burst<false, 14>(grid, s, keys, descs, pb, arena, masks, status, flags);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace qpp

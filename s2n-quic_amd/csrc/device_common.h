@@ -176,20 +176,75 @@ __device__ __forceinline__ void ctr_keystream(const AesLds &a, const CtrPage &pg
     for (int j = 0; j < NB; j++) ks[j] = a.final(s[j], rk + 4 * NR);
 }
 
-// AES T0/T1 bank-replicated tables for the AesLds view: dword d -> row x = d >> 6, slot = d & 63
-// (slots 32..63 hold T1 = rotl8 T0).  No barrier inside.
+// AES T0/T1 bank-replicated tables for the AesLds view: row x = 256 B, dword slot 0..31 = T0[x], 32..63 =
+// T1[x] = rotl8 T0[x].  Thread t owns S-box value x = t % 256 (one S-box load) and writes its row's slots in an
+// order rotated by x, so a wave's 64 stores of one step go to 32 distinct banks per 32-lane group.  Needs
+// blockDim.x % 256 == 0 (every launch: 256..1024 threads).  No barrier inside.
 // base: LDS offset of the 64 KiB table region (a multiple of 64 KiB).
 __device__ __forceinline__ void build_aes_tables(uint32_t base) {
+    const uint32_t x = threadIdx.x & 255u;
+    const uint32_t s = d_sbox[x], s2 = xtime4(s);
+    const uint32_t t0 = s2 | (s << 8) | (s << 16) | ((s2 ^ s) << 24);
+    const uint32_t t1 = __builtin_amdgcn_alignbit(t0, t0, 24);
     for (uint32_t d = threadIdx.x; d < 16384; d += blockDim.x) {
-        uint32_t x = d >> 6, slot = d & 63;
-        uint32_t s = d_sbox[x], s2 = xtime4(s);
-        uint32_t t0 = s2 | (s << 8) | (s << 16) | ((s2 ^ s) << 24);
-        lds_st32(base + 4 * d, slot < 32 ? t0 : __builtin_amdgcn_alignbit(t0, t0, 24));
+        const uint32_t slot = ((d >> 8) + x) & 63u;
+        lds_st32(base + 256u * x + 4u * slot, slot < 32 ? t0 : t1);
     }
 }
 
 __device__ __forceinline__ AesLds make_aes(uint32_t base) {
     return AesLds{((threadIdx.x & 31u) << 2) | base};
+}
+
+// ---------------------------------------------------------------- packet view, header protection (both AES kernels)
+struct PacketView {
+    uint8_t *base;       // packet start (AAD)
+    uint32_t aad_len, len, pn_len;
+    uint32_t n0, n1, n2; // nonce words
+};
+
+__device__ __forceinline__ PacketView load_packet(const qpp_pkt &d, const DevKey *__restrict__ key, uint8_t *arena) {
+    PacketView p;
+    p.base = arena + d.off;
+    p.aad_len = d.aad_len;
+    p.len = d.pt_len;
+    p.pn_len = d.pn_len;
+    // Iv::nonce: iv XOR (0u32 || pn_be64)  (src/iv.rs:27-39)
+    p.n0 = key->iv[0];
+    p.n1 = key->iv[1] ^ bswap32((uint32_t)(d.pn >> 32));
+    p.n2 = key->iv[2] ^ bswap32((uint32_t)d.pn);
+    return p;
+}
+
+// Header protection mask from the 16-byte sample (first 5 bytes of AES_hp(sample)).  The HP round keys are read
+// here, once per packet, into VGPRs: hoisted into SGPRs for the whole kernel they pushed the packet round keys out
+// of SGPRs (measured: 36 SGPR spills and per-iteration round-key reloads, a slower seal).
+template <int HNR>
+__device__ __forceinline__ void hp_finish(const AesLds &aes, const uint32_t *hp_rk_g, uint4 sample,
+                                          uint8_t *base, uint32_t hdr_len, uint32_t pn_len, uint8_t *mask_out,
+                                          uint32_t flags) {
+    // launder the pointer through a VGPR: the loads below cannot be hoisted or kept in SGPRs
+    uint64_t a = (uint64_t)hp_rk_g;
+    asm volatile("" : "+v"(a));
+    const uint4 *src = (const uint4 *)a;
+    uint32_t hp_rk[4 * (HNR + 1)];
+#pragma unroll
+    for (int i = 0; i < HNR + 1; i++) {
+        const uint4 v = src[i];
+        hp_rk[4 * i] = v.x; hp_rk[4 * i + 1] = v.y; hp_rk[4 * i + 2] = v.z; hp_rk[4 * i + 3] = v.w;
+    }
+    uint4 m = aes.encrypt<HNR>(sample, hp_rk);
+    if (flags & QPP_HP_MASK_OUT) {
+        mask_out[0] = (uint8_t)m.x; mask_out[1] = (uint8_t)(m.x >> 8); mask_out[2] = (uint8_t)(m.x >> 16);
+        mask_out[3] = (uint8_t)(m.x >> 24); mask_out[4] = (uint8_t)m.y;
+    }
+    if (flags & QPP_HP_APPLY) {
+        // header_crypto.rs:80-95
+        uint8_t b0 = base[0];
+        base[0] = b0 ^ ((uint8_t)m.x & ((b0 & 0x80) ? 0x0f : 0x1f));
+        uint32_t mm = (m.x >> 8) | (m.y << 24);
+        for (uint32_t i = 0; i < pn_len; i++) base[hdr_len + i] ^= (uint8_t)(mm >> (8 * i));
+    }
 }
 
 // ---------------------------------------------------------------- per-wave payload staging

@@ -86,7 +86,9 @@ struct WorkItem {
     uint32_t nr;     // AES rounds for this key
 };
 
-constexpr int kMinPacketsPerItem = 64;   // smallest AES work item, one wave (sizes plan scratch)
+constexpr int kMinPacketsPerItem = 4;    // smallest AES work item: burst kernel, one packet per wave (plan scratch)
+constexpr uint32_t kBurstMaxDefault = 8192;   // batches up to this many packets use the wave-per-packet kernel
+constexpr uint32_t kTxqZeroCopyMax = 256;     // txq flushes up to this many packets run on the pinned ring in place
 constexpr int kDefaultAesVariant = 0;  // see aes_gcm.hip launch_variant
 constexpr int kMaxPlanKeys = 8192;      // keys binned in LDS by the plan kernels (larger tables: global bins)
 
@@ -112,6 +114,11 @@ uint32_t plan_max_work(uint32_t n, uint32_t key_cap, uint32_t per);
 // AES work-item size for an n-packet batch on n_cu compute units: the selected variant's size, shrunk (in whole
 // waves) so that the work items fill every CU in balanced rounds when n is small (one workgroup per CU).
 uint32_t aes_packets_per_item(uint32_t n, uint32_t n_cu);
+// burst.hip: one wave per packet for small batches (GSO bursts); work items of whole waves, <= 64 packets
+uint32_t burst_packets_per_item(uint32_t n, uint32_t n_cu);
+hipError_t launch_aes_gcm_burst(bool seal, const DevKey *keys, const qpp_pkt *descs, const PlanBuffers &pb,
+                                uint32_t n, uint32_t key_cap, uint32_t per, uint8_t *arena, uint8_t *masks,
+                                int8_t *status, uint32_t flags, uint32_t suites, hipStream_t s);
 // suites: bit (1 << suite) for every suite with a live key in the context (launches only what can occur)
 hipError_t launch_aes_gcm(bool seal, const DevKey *keys, const qpp_pkt *descs, const PlanBuffers &pb, uint32_t n,
                           uint32_t key_cap, uint32_t per, uint8_t *arena, uint8_t *masks, int8_t *status,

@@ -50,7 +50,7 @@ EXPORTS = [
     "qpp_stream_destroy", "qpp_stream_synchronize", "qpp_event_create", "qpp_event_destroy", "qpp_event_record",
     "qpp_event_elapsed_ms", "qpp_stream_wait_event", "qpp_unprotect_open_batch", "qpp_pn_truncate", "qpp_pn_expand",
     "qpp_key_new_batch", "qpp_txq_create", "qpp_txq_destroy", "qpp_txq_ring", "qpp_txq_push", "qpp_txq_flush",
-    "qpp_txq_pending", "qpp_memcpy_d2d",
+    "qpp_txq_pending", "qpp_memcpy_d2d", "qpp_ctx_set_burst_max",
 ]
 
 
@@ -127,6 +127,7 @@ def lib():
             "qpp_txq_flush": (ctypes.c_int, [vp]),
             "qpp_txq_pending": (sz, [vp]),
             "qpp_memcpy_d2d": (ctypes.c_int, [vp, vp, vp, sz, vp]),
+            "qpp_ctx_set_burst_max": (ctypes.c_int, [vp, sz]),
         }
         assert set(sig) == set(EXPORTS)
         for name, (res, args) in sig.items():
@@ -200,6 +201,10 @@ class Context:
     @property
     def stream(self):
         return lib().qpp_ctx_stream(self.handle)
+
+    def set_burst_max(self, max_packets):
+        """AES batches of <= max_packets run one wave per packet (burst kernel); 0 = always lane per packet."""
+        self._check(lib().qpp_ctx_set_burst_max(self.handle, int(max_packets)), "set_burst_max")
 
     def sync(self, stream=None):
         self._check(lib().qpp_stream_synchronize(self.handle, stream), "sync")

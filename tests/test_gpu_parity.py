@@ -23,6 +23,14 @@ def ctx():
     c.close()
 
 
+@pytest.fixture(params=["burst", "lane"])
+def path(request, ctx):
+    """AES-GCM kernel path: wave per packet (small batches) or lane per packet (large); same outputs."""
+    ctx.set_burst_max(1 << 30 if request.param == "burst" else 0)
+    yield request.param
+    ctx.set_burst_max(8192)
+
+
 # ------------------------------------------------------------------ RFC 9001 Appendix A through the trait mirror
 
 def test_initial_keys_and_a2_seal(ctx, rfc):
@@ -94,7 +102,7 @@ def test_limits_and_lengths(ctx):
 
 @pytest.mark.parametrize("name,suite", [("aead_aes128gcm.json", 1), ("aead_aes256gcm.json", 2),
                                         ("aead_chacha20poly1305.json", 3)])
-def test_aead_fixtures(ctx, name, suite):
+def test_aead_fixtures(ctx, name, suite, path):
     for c in load_golden(name)["cases"]:
         k = ctx.raw_key(suite, H(c["key"]), H(c["iv"]), bytes(qpp.KEY_LEN[suite]))
         sealed = k.encrypt(c["pn"], H(c["aad"]), H(c["pt"]))
@@ -210,7 +218,7 @@ def _oracle_keys_for(keys_orc, descs, slots):
 
 
 @pytest.mark.parametrize("specs", [[1], [2], [3], [1, 1, 2, 3, 3, 2, 1, 3]], ids=["aes128", "aes256", "chacha", "mixed"])
-def test_batch_seal_open_ragged(ctx, specs):
+def test_batch_seal_open_ragged(ctx, specs, path):
     keys, okeys = _keys(ctx, specs, seed=len(specs) * 31 + specs[0])
     slots = [k.slot for k in keys]
     descs, arena = _ragged_batch(2048, slots, seed=7 + len(specs))
@@ -246,7 +254,7 @@ def test_batch_seal_open_ragged(ctx, specs):
         k.free()
 
 
-def test_jumbo_and_edges(ctx):
+def test_jumbo_and_edges(ctx, path):
     keys, okeys = _keys(ctx, [1, 2, 3], seed=99)
     slots = [k.slot for k in keys]
     lens = [0, 1, 4, 8000, 8000, 1452, 300, 65535 - 100]
@@ -382,7 +390,7 @@ def _rx_batch(ctx, n, seed):
     return keys, okeys, np.array(rx, dtype=qpp.RX_DTYPE), np.array(orx, dtype=qpp.RX_DTYPE), arena, want_pn, want_payload
 
 
-def test_unprotect_open_batch(ctx):
+def test_unprotect_open_batch(ctx, path):
     n = 1500
     keys, okeys, rx, orx, arena, want_pn, want_payload = _rx_batch(ctx, n, seed=21)
     d_rx, d_arena = ctx.alloc(rx.nbytes), ctx.alloc(arena.nbytes)
@@ -453,10 +461,13 @@ def test_key_new_batch_matches_host_chain(ctx, suite):
 
 # ------------------------------------------------------------------ deferred transmit queue (the TX caller)
 
-def test_txq_deferred_seal_matches_encode_packet(ctx):
+@pytest.mark.parametrize("flush", ["zero_copy", "dma"])
+def test_txq_deferred_seal_matches_encode_packet(ctx, path, flush, monkeypatch):
     """Packets encoded into the queue's ring the way PacketEncoder::encode_packet lays them out
     (packet/encoding.rs:115-282: header, truncated PN, payload, tag room), pushed instead of sealed, then one
-    flush: every packet equals crypto::encrypt + crypto::protect of the oracle."""
+    flush: every packet equals crypto::encrypt + crypto::protect of the oracle.  zero_copy: the kernels work on
+    the pinned ring in place with a host-built plan; dma: ring -> HBM -> ring around a device batch."""
+    monkeypatch.setenv("QPP_TXQ_ZC_MAX", "1024" if flush == "zero_copy" else "0")
     rng = np.random.default_rng(8)
     keys = [ctx.key(s, rng.integers(0, 256, qpp.HASH_LEN[s], dtype=np.uint8).tobytes()) for s in (1, 2, 3)]
     q = qpp.TxQueue(ctx, 1 << 20, 1024)

@@ -214,7 +214,8 @@ int run_one(const qpp_key *k, bool seal, uint64_t pn, const uint8_t *header, siz
                                                                              ctx->d_mask1, ctx->d_status1, 0,
                                                                              1u << k->suite, s));
     } else {
-        HIP_TRY(ctx, launch_chacha(seal, ctx->d_keys, ctx->d_desc1, 1, ctx->d_stage, ctx->d_mask1, ctx->d_status1, 0, s));
+        HIP_TRY(ctx, launch_chacha(seal, ctx->d_keys, ctx->d_desc1, 1, ctx->d_stage, ctx->d_mask1, ctx->d_status1, 0,
+                                   ctx->burst_max > 0, s));
     }
     int8_t st = QPP_OK;
     HIP_TRY(ctx, hipMemcpyAsync(h, ctx->d_stage, total, hipMemcpyDeviceToHost, s));
@@ -535,7 +536,8 @@ int qpp_seal_batch(qpp_ctx *ctx, const qpp_pkt *descs, size_t n, uint8_t *arena,
                                                                     suite_mask(ctx), s));
     }
     if (!(flags & QPP_ONLY_AES))
-        HIP_TRY(ctx, launch_chacha(true, ctx->d_keys, descs, (uint32_t)n, arena, masks, status, flags, s));
+        HIP_TRY(ctx, launch_chacha(true, ctx->d_keys, descs, (uint32_t)n, arena, masks, status, flags,
+                                   n <= ctx->burst_max, s));
     return QPP_OK;
 }
 
@@ -560,7 +562,8 @@ int qpp_open_batch(qpp_ctx *ctx, const qpp_pkt *descs, size_t n, uint8_t *arena,
                                                                     suite_mask(ctx), s));
     }
     if (!(flags & QPP_ONLY_AES))
-        HIP_TRY(ctx, launch_chacha(false, ctx->d_keys, descs, (uint32_t)n, arena, nullptr, status, 0, s));
+        HIP_TRY(ctx, launch_chacha(false, ctx->d_keys, descs, (uint32_t)n, arena, nullptr, status, 0,
+                                   n <= ctx->burst_max, s));
     return QPP_OK;
 }
 
@@ -817,7 +820,7 @@ static int txq_flush_zero_copy(qpp_txq *q, hipStream_t s) {
                                           q->v_ring, nullptr, nullptr, QPP_HP_APPLY, q->suites & aes, s));
     }
     if (q->suites & ~aes)
-        HIP_TRY(ctx, launch_chacha(true, ctx->d_keys, q->v_desc, n, q->v_ring, nullptr, nullptr, QPP_HP_APPLY, s));
+        HIP_TRY(ctx, launch_chacha(true, ctx->d_keys, q->v_desc, n, q->v_ring, nullptr, nullptr, QPP_HP_APPLY, true, s));
     HIP_TRY(ctx, hipStreamSynchronize(s));
     return QPP_OK;
 }

@@ -268,6 +268,186 @@ __global__ __launch_bounds__(256) void chacha_kernel(const DevKey *__restrict__ 
     }
 }
 
+// ---------------------------------------------------------------- small batches: one WAVE per packet
+// The burst form of chacha_kernel (the AES twin is burst.hip): the 64 lanes of a wave split one packet.  Lane l
+// takes the MAC-stream blocks j = l, l + 64, ... of the zero-front-padded stream (AAD, ciphertext, lengths), so
+//   tag_pre = sum_j X'_j r^(64K - j) = r * sum_l acc_l r^(63 - l),   acc_l = Horner over the lane's blocks in r^64,
+// and the lanes are summed by a 6-level tree (level t multiplies the left half by r^(2^t)).  The powers r^(2^t)
+// are six squarings of the packet's own r (every lane computes them; no tables).  A ciphertext block's keystream is
+// the 16-byte quarter of its ChaCha20 block (counter 1 + b/4) that the lane computes itself.
+
+struct P130 {  // element mod 2^130 - 5, 5 x 26-bit limbs (partially reduced, as Poly1305::block leaves them)
+    uint32_t l0, l1, l2, l3, l4;
+};
+__device__ __forceinline__ P130 p_block(uint4 m, uint32_t hibit) {
+    return P130{m.x & 0x3ffffff, ((m.x >> 26) | (m.y << 6)) & 0x3ffffff, ((m.y >> 20) | (m.z << 12)) & 0x3ffffff,
+                ((m.z >> 14) | (m.w << 18)) & 0x3ffffff, (m.w >> 8) | hibit};
+}
+__device__ __forceinline__ P130 p_add(P130 a, P130 b) {
+    return P130{a.l0 + b.l0, a.l1 + b.l1, a.l2 + b.l2, a.l3 + b.l3, a.l4 + b.l4};
+}
+// a * b mod p for general operands: limbs of a < 2^29 (a tree level adds up to 7 reduced values), limbs of b
+// < 2^26 + 2^11 (a reduced power of r; unlike the clamped r itself its top limb bits are not cleared), so the
+// column sums reach 2^60 and every carry is kept in 64 bits (a 32-bit carry, as Poly1305::block may use with the
+// clamped r, truncates here: found by the ragged-batch parity test).
+__device__ __forceinline__ P130 p_mul(P130 a, P130 b) {
+    const uint32_t s1 = b.l1 * 5, s2 = b.l2 * 5, s3 = b.l3 * 5, s4 = b.l4 * 5;
+    uint64_t d0 = (uint64_t)a.l0 * b.l0 + (uint64_t)a.l1 * s4 + (uint64_t)a.l2 * s3 + (uint64_t)a.l3 * s2 + (uint64_t)a.l4 * s1;
+    uint64_t d1 = (uint64_t)a.l0 * b.l1 + (uint64_t)a.l1 * b.l0 + (uint64_t)a.l2 * s4 + (uint64_t)a.l3 * s3 + (uint64_t)a.l4 * s2;
+    uint64_t d2 = (uint64_t)a.l0 * b.l2 + (uint64_t)a.l1 * b.l1 + (uint64_t)a.l2 * b.l0 + (uint64_t)a.l3 * s4 + (uint64_t)a.l4 * s3;
+    uint64_t d3 = (uint64_t)a.l0 * b.l3 + (uint64_t)a.l1 * b.l2 + (uint64_t)a.l2 * b.l1 + (uint64_t)a.l3 * b.l0 + (uint64_t)a.l4 * s4;
+    uint64_t d4 = (uint64_t)a.l0 * b.l4 + (uint64_t)a.l1 * b.l3 + (uint64_t)a.l2 * b.l2 + (uint64_t)a.l3 * b.l1 + (uint64_t)a.l4 * b.l0;
+    P130 h;
+    uint64_t c;
+    c = d0 >> 26; h.l0 = (uint32_t)d0 & 0x3ffffff;
+    d1 += c; c = d1 >> 26; h.l1 = (uint32_t)d1 & 0x3ffffff;
+    d2 += c; c = d2 >> 26; h.l2 = (uint32_t)d2 & 0x3ffffff;
+    d3 += c; c = d3 >> 26; h.l3 = (uint32_t)d3 & 0x3ffffff;
+    d4 += c; c = d4 >> 26; h.l4 = (uint32_t)d4 & 0x3ffffff;
+    const uint64_t t = (uint64_t)h.l0 + c * 5;  // c < 2^35
+    h.l0 = (uint32_t)t & 0x3ffffff;
+    h.l1 += (uint32_t)(t >> 26);
+    return h;
+}
+__device__ __forceinline__ P130 p_shfl_down(P130 v, unsigned d) {
+    return P130{(uint32_t)__shfl_down((int)v.l0, d, 64), (uint32_t)__shfl_down((int)v.l1, d, 64),
+                (uint32_t)__shfl_down((int)v.l2, d, 64), (uint32_t)__shfl_down((int)v.l3, d, 64),
+                (uint32_t)__shfl_down((int)v.l4, d, 64)};
+}
+__device__ __forceinline__ uint4 shfl4(uint4 v, int src) {
+    return make_uint4((uint32_t)__shfl((int)v.x, src, 64), (uint32_t)__shfl((int)v.y, src, 64),
+                      (uint32_t)__shfl((int)v.z, src, 64), (uint32_t)__shfl((int)v.w, src, 64));
+}
+__device__ __forceinline__ uint32_t byte_of(uint4 v, uint32_t i) {  // byte i (< 16) of v
+    const uint32_t w = i < 4 ? v.x : i < 8 ? v.y : i < 12 ? v.z : v.w;
+    return (w >> (8 * (i & 3))) & 0xffu;
+}
+
+template <bool SEAL>
+__global__ __launch_bounds__(256) void chacha_burst_kernel(const DevKey *__restrict__ keys,
+                                                          const qpp_pkt *__restrict__ descs, uint32_t n,
+                                                          uint8_t *__restrict__ arena, uint8_t *masks, int8_t *status,
+                                                          uint32_t flags) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t pi = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+    if (pi >= n) return;
+    const qpp_pkt d = descs[pi];
+    const DevKey *__restrict__ key = keys + d.key_idx;
+    if (key->suite != QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256 || (d.flags & QPP_PKT_SKIP)) return;  // wave-uniform
+    uint32_t k[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) k[i] = key->rk[i];
+    const uint32_t n0 = key->iv[0], n1 = key->iv[1] ^ bswap32((uint32_t)(d.pn >> 32)), n2 = key->iv[2] ^ bswap32((uint32_t)d.pn);
+    uint8_t *base = arena + d.off;
+    const uint32_t aad_len = d.aad_len, len = d.pt_len;
+    uint8_t *pay = base + aad_len;
+
+    uint32_t ks[16];
+    chacha_block(k, 0, n0, n1, n2, ks);  // one-time Poly1305 key (every lane: uniform)
+    Poly1305 key_r;
+    key_r.init(ks[0], ks[1], ks[2], ks[3]);
+    const uint32_t sw0 = ks[4], sw1 = ks[5], sw2 = ks[6], sw3 = ks[7];
+    P130 rp[7];  // r^(2^t)
+    rp[0] = P130{key_r.r0, key_r.r1, key_r.r2, key_r.r3, key_r.r4};
+#pragma unroll
+    for (int t = 1; t < 7; t++) rp[t] = p_mul(rp[t - 1], rp[t - 1]);
+
+    const uint32_t a = (aad_len + 15u) >> 4, c = (len + 15u) >> 4, m = a + c + 1;
+    const uint32_t K = (m + 63u) >> 6, pad = 64u * K - m;
+    P130 acc{0, 0, 0, 0, 0};
+    uint4 ct0 = make_uint4(0, 0, 0, 0), ct1 = ct0;  // ciphertext blocks 0/1 where this lane owns them (HP sample)
+    for (uint32_t kk = 0; kk < K; kk++) {
+        const int i = (int)(lane + 64u * kk) - (int)pad;
+        uint4 x = make_uint4(0, 0, 0, 0);
+        uint32_t hib = 1u << 24;  // the 2^128 bit of every (padded, full) MAC block
+        if (i < 0) {
+            hib = 0;  // front padding: a zero term
+        } else if (i < (int)a) {
+            const uint32_t off = 16u * (uint32_t)i;
+            x = ld16(base + off);
+            if (aad_len - off < 16u) x = keep_bytes(x, aad_len - off);
+        } else if (i < (int)(a + c)) {
+            const uint32_t b = (uint32_t)i - a, r = len - 16u * b, q = b & 3u;
+            chacha_block(k, 1u + (b >> 2), n0, n1, n2, ks);
+            const uint4 kq = make_uint4(q == 0 ? ks[0] : q == 1 ? ks[4] : q == 2 ? ks[8] : ks[12],
+                                        q == 0 ? ks[1] : q == 1 ? ks[5] : q == 2 ? ks[9] : ks[13],
+                                        q == 0 ? ks[2] : q == 1 ? ks[6] : q == 2 ? ks[10] : ks[14],
+                                        q == 0 ? ks[3] : q == 1 ? ks[7] : q == 2 ? ks[11] : ks[15]);
+            uint4 in = ld16(pay + 16u * b);
+            uint4 out = in ^ kq;
+            if (r >= 16u) {
+                st16(pay + 16u * b, out);
+            } else {
+                out = keep_bytes(out, r);
+                in = keep_bytes(in, r);
+                st_bytes(pay + 16u * b, out, r);
+            }
+            x = SEAL ? out : in;
+            if (b == 0) ct0 = x;
+            if (b == 1) ct1 = x;
+        } else {
+            x = make_uint4(aad_len, 0, len, 0);  // le64(aad_len) || le64(ct_len)
+        }
+        const P130 xb = p_block(x, hib);
+        acc = kk ? p_add(p_mul(acc, rp[6]), xb) : xb;
+    }
+#pragma unroll
+    for (int t = 0; t < 6; t++) acc = p_add(p_mul(acc, rp[t]), p_shfl_down(acc, 1u << t));
+    const P130 y = p_mul(acc, rp[0]);
+    Poly1305 fin;
+    fin.h0 = y.l0; fin.h1 = y.l1; fin.h2 = y.l2; fin.h3 = y.l3; fin.h4 = y.l4;
+    const uint4 tag = shfl4(fin.finish(sw0, sw1, sw2, sw3), 0);  // lane 0 holds the sum
+
+    if (SEAL) {
+        if (lane == 0) st16(pay + len, tag);
+        int8_t st8 = QPP_OK;
+        if (flags & (QPP_HP_MASK_OUT | QPP_HP_APPLY)) {
+            const uint32_t s = 4u - d.pn_len;
+            if (d.pn_len < 1 || d.pn_len > 4 || len < s) {
+                st8 = QPP_DECODE_ERROR;
+            } else {
+                const uint32_t o0 = (pad + a) & 63u;
+                const uint4 c0 = shfl4(ct0, (int)o0), c1 = shfl4(ct1, (int)((o0 + 1u) & 63u));
+                uint4 smp;
+                if (len >= s + 16u) {  // sample = (ciphertext || tag)[s, s + 16) from ciphertext blocks 0 and 1
+                    smp = make_uint4(__builtin_amdgcn_alignbyte(c0.y, c0.x, s), __builtin_amdgcn_alignbyte(c0.z, c0.y, s),
+                                     __builtin_amdgcn_alignbyte(c0.w, c0.z, s), __builtin_amdgcn_alignbyte(c1.x, c0.w, s));
+                } else {
+                    uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+                    for (uint32_t q = 0; q < 16; q++) {
+                        const uint32_t pos = s + q;
+                        const uint32_t v = pos < len ? (pos < 16u ? byte_of(c0, pos) : byte_of(c1, pos - 16u))
+                                                     : byte_of(tag, pos - len);
+                        w[q >> 2] |= v << (8 * (q & 3));
+                    }
+                    smp = make_uint4(w[0], w[1], w[2], w[3]);
+                }
+                uint32_t hk[8];
+#pragma unroll
+                for (int i = 0; i < 8; i++) hk[i] = key->hp_rk[i];
+                uint32_t m1, m0 = chacha_hp_word(hk, smp, &m1);
+                if (lane == 0) apply_mask(base, aad_len - d.pn_len, d.pn_len, m0, m1, masks + 5 * (size_t)pi, flags);
+            }
+        }
+        if (status && lane == 0) status[pi] = st8;
+    } else {
+        const uint4 diff = tag ^ ld16(pay + len);
+        const bool ok = (diff.x | diff.y | diff.z | diff.w) == 0;
+        if (!ok) {  // each lane zeroes the plaintext blocks it wrote (same-lane order)
+            for (uint32_t kk = 0; kk < K; kk++) {
+                const int i = (int)(lane + 64u * kk) - (int)pad;
+                if (i >= (int)a && i < (int)(a + c)) {
+                    const uint32_t b = (uint32_t)i - a, r = len - 16u * b;
+                    if (r >= 16u) st16(pay + 16u * b, make_uint4(0, 0, 0, 0));
+                    else st_bytes(pay + 16u * b, make_uint4(0, 0, 0, 0), r);
+                }
+            }
+        }
+        if (lane == 0) status[pi] = ok ? QPP_OK : QPP_DECRYPT_ERROR;
+    }
+}
+
 // Header-protection masks for any suite, one lane per packet; AES keys use the LDS T-tables with the
 // lane's own round keys.  Sample at off + aad_len - pn_len + 4.
 __global__ __launch_bounds__(1024) void hp_mask_kernel(const DevKey *__restrict__ keys, const qpp_pkt *__restrict__ descs,
@@ -367,8 +547,17 @@ hipError_t launch_unprotect(const DevKey *keys, const qpp_rx_pkt *rx, uint32_t n
 }
 
 hipError_t launch_chacha(bool seal, const DevKey *keys, const qpp_pkt *descs, uint32_t n, uint8_t *arena,
-                         uint8_t *masks, int8_t *status, uint32_t flags, hipStream_t s) {
+                         uint8_t *masks, int8_t *status, uint32_t flags, bool burst, hipStream_t s) {
     if (!n) return hipSuccess;
+    if (burst) {  // one wave per packet, 4 per workgroup
+        if (seal)
+            hipLaunchKernelGGL(chacha_burst_kernel<true>, dim3((n + 3) / 4), dim3(256), 0, s, keys, descs, n, arena,
+                               masks, status, flags);
+        else
+            hipLaunchKernelGGL(chacha_burst_kernel<false>, dim3((n + 3) / 4), dim3(256), 0, s, keys, descs, n, arena,
+                               masks, status, flags);
+        return hipGetLastError();
+    }
     const dim3 grid((n + 255) / 256), block(256);
     const uint32_t lds = 4u * 64u * 16u * 4u;  // Stage<4> per wave, 4 waves
     if (seal)

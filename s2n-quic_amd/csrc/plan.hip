@@ -120,6 +120,86 @@ __global__ __launch_bounds__(kPlanBlock) void plan_scatter(const DevKey *__restr
     }
 }
 
+// Small batches (n <= kPlanSmallMax, key_cap <= kMaxPlanKeys): the three stages above in ONE workgroup and one
+// launch (a GSO burst pays ~4 us here instead of a memset + three launches, ~17 us).  Each thread keeps the keys
+// of its <= 8 packets in registers; keys are scanned 8 per thread with a wave scan + a 16-entry workgroup scan.
+// Dynamic LDS: cur[kMaxPlanKeys + 1] (counts, then scatter cursors), ist[kMaxPlanKeys + 1] (first work item),
+// wave totals.
+constexpr uint32_t kPlanSmallMax = 8 * kPlanBlock;
+constexpr uint32_t kPlanSmallLds = 4 * (2 * (kMaxPlanKeys + 1) + 64);
+
+__global__ __launch_bounds__(kPlanBlock) void plan_small(const DevKey *__restrict__ keys, uint32_t key_cap,
+                                                        const qpp_pkt *__restrict__ descs, uint32_t n,
+                                                        uint32_t *__restrict__ perm, WorkItem *__restrict__ work,
+                                                        uint32_t *__restrict__ n_work, uint32_t per) {
+    extern __shared__ uint32_t smem[];
+    uint32_t *cur = smem, *ist = smem + kMaxPlanKeys + 1, *wt = ist + kMaxPlanKeys + 1;  // wt: [2][16]
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    for (uint32_t k = tid; k <= key_cap; k += kPlanBlock) cur[k] = 0;
+    __syncthreads();
+    uint32_t mine[kPlanSmallMax / kPlanBlock];  // key slot of packets tid + 1024 j (~0u: not an AES packet)
+#pragma unroll
+    for (uint32_t j = 0; j < kPlanSmallMax / kPlanBlock; j++) {
+        const uint32_t pi = tid + kPlanBlock * j;
+        uint32_t k = ~0u;
+        if (pi < n) {
+            k = descs[pi].key_idx;
+            if (k >= key_cap || !is_aes(keys, k)) k = ~0u;
+            else atomicAdd(&cur[k], 1u);
+        }
+        mine[j] = k;
+    }
+    __syncthreads();
+    // exclusive scans over keys of counts (-> cursors) and work items (-> ist), kpt consecutive keys per thread
+    const uint32_t kpt = (key_cap + kPlanBlock - 1) / kPlanBlock, k0 = tid * kpt;
+    uint32_t lc = 0, li = 0;
+    for (uint32_t j = 0; j < kpt; j++) {
+        const uint32_t c = k0 + j < key_cap ? cur[k0 + j] : 0;
+        lc += c;
+        li += (c + per - 1) / per;
+    }
+    uint32_t sc = lc, si = li;  // inclusive wave scan
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t a = (uint32_t)__shfl_up((int)sc, o, 64), b = (uint32_t)__shfl_up((int)si, o, 64);
+        if (lane >= (uint32_t)o) { sc += a; si += b; }
+    }
+    if (lane == 63) { wt[wave] = sc; wt[16 + wave] = si; }
+    __syncthreads();
+    uint32_t bc = 0, bi = 0, tc = 0, ti = 0;
+    for (uint32_t w = 0; w < kPlanBlock / 64; w++) {
+        if (w < wave) { bc += wt[w]; bi += wt[16 + w]; }
+        tc += wt[w];
+        ti += wt[16 + w];
+    }
+    uint32_t pc = bc + sc - lc, pw = bi + si - li;  // exclusive prefixes at this thread's first key
+    for (uint32_t j = 0; j < kpt; j++) {  // each thread rewrites only its own keys
+        const uint32_t k = k0 + j;
+        if (k >= key_cap) break;
+        const uint32_t c = cur[k];
+        cur[k] = pc;
+        ist[k] = pw;
+        pc += c;
+        pw += (c + per - 1) / per;
+    }
+    if (tid == 0) { cur[key_cap] = tc; ist[key_cap] = ti; *n_work = ti; }
+    __syncthreads();
+    for (uint32_t w = tid; w < ti; w += kPlanBlock) {
+        uint32_t lo = 0, hi = key_cap;  // largest k with ist[k] <= w (keys without items share a start)
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (ist[mid] <= w) lo = mid; else hi = mid;
+        }
+        const uint32_t i = w - ist[lo];
+        const uint32_t left = cur[lo + 1] - cur[lo] - i * per;
+        work[w] = WorkItem{lo, cur[lo] + i * per, left < per ? left : per, keys[lo].nr};
+    }
+    __syncthreads();  // the work items read the cursors' start values; the scatter advances them
+#pragma unroll
+    for (uint32_t j = 0; j < kPlanSmallMax / kPlanBlock; j++)
+        if (mine[j] != ~0u) perm[atomicAdd(&cur[mine[j]], 1u)] = tid + kPlanBlock * j;
+}
+
 }  // namespace
 
 uint32_t plan_max_work(uint32_t n, uint32_t key_cap, uint32_t per) {
@@ -130,6 +210,11 @@ uint32_t plan_max_work(uint32_t n, uint32_t key_cap, uint32_t per) {
 
 hipError_t launch_plan(const DevKey *keys, uint32_t key_cap, const qpp_pkt *descs, uint32_t n, PlanBuffers pb,
                        uint32_t per, hipStream_t s) {
+    if (n <= kPlanSmallMax && key_cap <= (uint32_t)kMaxPlanKeys) {
+        hipLaunchKernelGGL(plan_small, dim3(1), dim3(kPlanBlock), kPlanSmallLds, s, keys, key_cap, descs, n, pb.perm,
+                           pb.work, pb.n_work, per);
+        return hipGetLastError();
+    }
     hipError_t e = hipMemsetAsync(pb.counts, 0, sizeof(uint32_t) * key_cap, s);
     if (e != hipSuccess) return e;
     const dim3 grid((n + kPlanBlock - 1) / kPlanBlock);

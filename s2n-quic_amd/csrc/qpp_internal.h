@@ -123,8 +123,9 @@ hipError_t launch_aes_gcm_burst(bool seal, const DevKey *keys, const qpp_pkt *de
 hipError_t launch_aes_gcm(bool seal, const DevKey *keys, const qpp_pkt *descs, const PlanBuffers &pb, uint32_t n,
                           uint32_t key_cap, uint32_t per, uint8_t *arena, uint8_t *masks, int8_t *status,
                           uint32_t flags, uint32_t suites, hipStream_t s);
+// burst: one wave per packet (small batches) instead of one lane per packet
 hipError_t launch_chacha(bool seal, const DevKey *keys, const qpp_pkt *descs, uint32_t n, uint8_t *arena,
-                         uint8_t *masks, int8_t *status, uint32_t flags, hipStream_t s);
+                         uint8_t *masks, int8_t *status, uint32_t flags, bool burst, hipStream_t s);
 // receive side: remove header protection, expand the PN, choose the key by key phase -> descs_out (chacha.hip)
 hipError_t launch_unprotect(const DevKey *keys, const qpp_rx_pkt *rx, uint32_t n, uint8_t *arena, qpp_pkt *descs_out,
                             int8_t *status, hipStream_t s);

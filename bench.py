@@ -42,6 +42,24 @@ def open_bytes_per_packet(pt, aad):
     return aad + pt + 16 + 24 + pt + 1
 
 
+LDS_PEAK_CYCLES = 256 * 2.4e9  # LDS-array cycles per second: one array per CU, 256 CUs at the 2.4 GHz spec clock
+
+
+def aes_lds_cycles_per_packet(pt, aad, nr, hp=True):
+    """LDS-array cycles aes_gcm_kernel spends per packet (MI355X_MICROARCH.md §LDS: ds_read_b32 2, ds_read_b128 4,
+    ds_write_b128 8 cycles per wave instruction of 64 packets, so per packet 1/64 of that).  Per counter block: the
+    CTR AES with round caching (CtrPage) = 133 T-table lookups for AES-128, 197 for AES-256; counters are issued in
+    groups of NB = 4 from counter 0 (J0 = counter 1); each group block also crosses the staging area (2 ds_read_b128
+    + 2 ds_write_b128).  GHASH: 16 ds_read_b128 per product, one per AAD block, ciphertext block, the length block
+    and the final product.  HP: one uncached AES block.  At P = 1200 this gives 4.68e8 cycles per 1 Mi-packet launch
+    against SQ_LDS_IDX_ACTIVE 4.90e8 incl. 1.8e7 bank-conflict cycles (profiles/r01_prof_c2_summary.txt)."""
+    lookups = 133 if nr == 10 else 197
+    ctr_blocks = -(-((pt + 15) // 16 + 2) // 4) * 4
+    ghash = (aad + 15) // 16 + (pt + 15) // 16 + 2
+    per_wave = 2 * (ctr_blocks * lookups + (16 * nr if hp else 0)) + 4 * 16 * ghash + ctr_blocks * (2 * 4 + 2 * 8)
+    return per_wave / 64.0
+
+
 def cpu_baseline(suite, pt, aad, seconds):
     """The reference's per-packet CPU loop (OpenSSL EVP stand-in for aws-lc) on this host's cores."""
     path = os.path.join(ROOT, "oracle", "libcpubase.so")
@@ -184,6 +202,14 @@ def main():
             },
             "cpu_baseline": None,
         }
+        if suite != 3 and n > qpp.BURST_MAX_DEFAULT:
+            # the lane kernel's own bound: the CU's LDS array (T-table + GHASH-table lookups), not HBM
+            cyc = n * aes_lds_cycles_per_packet(pt, aad, 10 if suite == 1 else 14)
+            out["kernel_roofline"] = {
+                "bound": "lds", "achieved": round(cyc / (seal_avg / 1e3) / 1e9, 1), "peak": LDS_PEAK_CYCLES / 1e9,
+                "unit": "G LDS-array cycles/s", "frac": round(cyc / (seal_avg / 1e3) / LDS_PEAK_CYCLES, 4),
+                "model": "bench.aes_lds_cycles_per_packet, checked against SQ_LDS_IDX_ACTIVE; peak = 256 CUs x 2.4 GHz",
+            }
         if world == 1 and not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(suite, pt, aad, args.cpu_seconds)
         print(json.dumps(out), flush=True)

@@ -27,7 +27,11 @@ constexpr uint32_t kBurstAes = 0;
 constexpr uint32_t kBurstGh = 65536;
 constexpr uint32_t kBurstTab = 8192;
 constexpr uint32_t kBurstLds = kBurstGh + 7 * kBurstTab;  // 120 KiB: one workgroup per CU
-constexpr int kBurstWG = 256;                             // 4 waves = 4 packets in flight per CU
+#ifndef QPP_BURST_WAVES
+#define QPP_BURST_WAVES 8  // measured: 4 waves 34 / 80 / 137 us seal at 64 / 4096 / 8192 packets, 8 waves 30 / 56 / 93, 12 waves 29 / 62 / 91
+#endif
+constexpr int kBurstWaves = QPP_BURST_WAVES;              // packets in flight per CU (one workgroup per CU)
+constexpr int kBurstWG = 64 * kBurstWaves;
 static_assert(kBurstLds <= kLdsMax, "LDS budget");
 
 __device__ __forceinline__ uint32_t tab(int t) { return kBurstGh + (uint32_t)t * kBurstTab; }
@@ -210,10 +214,12 @@ void launch_burst(dim3 grid, hipStream_t s, const DevKey *keys, const qpp_pkt *d
 }  // namespace
 
 uint32_t burst_packets_per_item(uint32_t n, uint32_t n_cu) {
-    // whole waves (4 per workgroup), enough items to spread the batch over every CU, at most 64 packets per item
-    uint32_t per = n_cu ? (n + n_cu - 1) / n_cu : 64u;
-    per = (per + 3u) & ~3u;
-    return per < 4u ? 4u : per > 64u ? 64u : per;
+    // enough items to spread the batch over every CU; an item fills the workgroup's waves (or, for tiny batches,
+    // 4 of them, so more CUs take part); at most 8 packets per wave
+    const uint32_t w = (uint32_t)kBurstWaves;
+    uint32_t per = n_cu ? (n + n_cu - 1) / n_cu : 8u * w;
+    per = per <= w ? ((per + 3u) & ~3u) : (per + w - 1) / w * w;
+    return per < 4u ? 4u : per > 8u * w ? 8u * w : per;
 }
 
 hipError_t launch_aes_gcm_burst(bool seal, const DevKey *keys, const qpp_pkt *descs, const PlanBuffers &pb,

@@ -8,7 +8,7 @@ Multi-GPU (torchrun, one process per GPU): every rank seals/opens its own shard 
 gloo on CPU tensors carries only the barrier and the max-over-ranks time.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--suite aes128gcm|aes256gcm|chacha20poly1305]
-                    [--packets N] [--pt BYTES] [--keys K] [--mode device|e2e]
+                    [--packets N] [--pt BYTES] [--keys K] [--mode device|e2e|rx|keys|txq]
 """
 import argparse
 import ctypes
@@ -60,6 +60,16 @@ def aes_lds_cycles_per_packet(pt, aad, nr, hp=True):
     return per_wave / 64.0
 
 
+VALU_PEAK_PER_NS = 540.0  # wave-instructions/ns chip-wide for xor/add/alignbit/bitop3/perm/mul_lo (tools/ubench/issue.hip)
+
+
+def chacha_valu_per_packet(pt):
+    """VALU wave-instructions chacha_kernel issues per packet: 1386 per 64-byte chunk per wave of 64 packets (20-round
+    block, 4 Poly1305 blocks of 26-bit-limb products, staging), from SQ_INSTS_VALU = 4.315e8 per 1 Mi x 1200 B seal
+    launch (profiles/r01_prof_c3_chacha_summary.txt: 19 chunks x 1386 x 16384 waves)."""
+    return 1386.0 * ((pt + 63) // 64) / 64.0
+
+
 def cpu_baseline(suite, pt, aad, seconds):
     """The reference's per-packet CPU loop (OpenSSL EVP stand-in for aws-lc) on this host's cores."""
     path = os.path.join(ROOT, "oracle", "libcpubase.so")
@@ -96,7 +106,8 @@ def main():
     ap.add_argument("--keys", type=int, default=1)
     ap.add_argument("--mode", default="device", choices=["device", "e2e", "rx", "keys", "txq"],
                     help="device: seal+open in HBM (headline); e2e: pinned host -> HBM -> host; rx: receive path "
-                         "(unprotect -> PN expand -> open); keys: device key schedule (key-update churn)")
+                         "(unprotect -> PN expand -> open); keys: device key schedule (key-update churn); "
+                         "txq: 64-packet GSO-burst flush latency through the transmit queue")
     ap.add_argument("--cpu-seconds", type=float, default=1.5)
     ap.add_argument("--chunks", type=int, default=16, help="e2e: pipeline chunks (H2D / seal+open / D2H overlap)")
     ap.add_argument("--no-cpu", action="store_true")
@@ -197,11 +208,19 @@ def main():
             "roofline": {
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": "aes_gcm_kernel<seal> + plan (per seal call)" if suite != 3 else "chacha_kernel<seal>",
+                "kernel": (("chacha" if suite == 3 else "aes_gcm") + ("_burst" if n <= qpp.BURST_MAX_DEFAULT else "")
+                           + "_kernel<seal>" + ("" if suite == 3 else " + plan (per seal call)")),
                 "bytes_per_packet": seal_bytes_per_packet(pt, aad),
             },
             "cpu_baseline": None,
         }
+        if suite == 3 and n > qpp.BURST_MAX_DEFAULT:
+            ins = n * chacha_valu_per_packet(pt)
+            out["kernel_roofline"] = {
+                "bound": "valu", "achieved": round(ins / (seal_avg / 1e3) / 1e9, 1), "peak": VALU_PEAK_PER_NS,
+                "unit": "G wave-instructions/s", "frac": round(ins / (seal_avg / 1e3) / (VALU_PEAK_PER_NS * 1e9), 4),
+                "model": "bench.chacha_valu_per_packet (SQ_INSTS_VALU); peak measured by tools/ubench/issue.hip",
+            }
         if suite != 3 and n > qpp.BURST_MAX_DEFAULT:
             # the lane kernel's own bound: the CU's LDS array (T-table + GHASH-table lookups), not HBM
             cyc = n * aes_lds_cycles_per_packet(pt, aad, 10 if suite == 1 else 14)

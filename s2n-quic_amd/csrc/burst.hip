@@ -95,17 +95,25 @@ __device__ __forceinline__ void burst_packet(const AesLds &aes, const DevKey *__
     const uint32_t a = (p.aad_len + 15u) >> 4, c = (p.len + 15u) >> 4, m = a + c + 1;
     const uint32_t K = (m + 63u) >> 6, pad = 64u * K - m;
     uint4 acc = make_uint4(0, 0, 0, 0), ct0 = acc, ct1 = acc;  // ct0/ct1: ciphertext blocks 0/1 where owned
+    uint4 ek = acc;  // E_K(J0), computed in pass 0 by the idle lane pad - 1 inside the data lanes' AES stream
     for (uint32_t k = 0; k < K; k++) {
         const int i = (int)(lane + 64u * k) - (int)pad;  // block index in the GHASH sequence
+        const bool data = i >= (int)a && i < (int)(a + c);
+        const bool j0 = k == 0 && i == -1;
+        const uint32_t b = (uint32_t)i - a;  // data block b uses counter b + 2
+        uint4 in = make_uint4(0, 0, 0, 0), ks = in;
+        if (data || j0) {
+            if (data) in = ld16(pay + 16u * b);
+            ks = aes.encrypt<NR>(make_uint4(p.n0, p.n1, p.n2, bswap32(data ? b + 2u : 1u)), rk);
+        }
         uint4 x = make_uint4(0, 0, 0, 0);
+        if (j0) ek = ks;
         if (i >= 0 && i < (int)a) {
             const uint32_t off = 16u * (uint32_t)i;
             x = ld16(p.base + off);
             if (p.aad_len - off < 16u) x = keep_bytes(x, p.aad_len - off);
-        } else if (i >= (int)a && i < (int)(a + c)) {
-            const uint32_t b = (uint32_t)i - a, r = p.len - 16u * b;  // data block b uses counter b + 2
-            const uint4 ks = aes.encrypt<NR>(make_uint4(p.n0, p.n1, p.n2, bswap32(b + 2u)), rk);
-            uint4 in = ld16(pay + 16u * b);
+        } else if (data) {
+            const uint32_t r = p.len - 16u * b;
             uint4 out = in ^ ks;
             if (r >= 16u) {
                 st16(pay + 16u * b, out);
@@ -125,8 +133,9 @@ __device__ __forceinline__ void burst_packet(const AesLds &aes, const DevKey *__
     // lane tree: level t combines lanes l and l + 2^t (l a multiple of 2^(t+1)) as v_l * H^(2^t) ^ v_(l+2^t)
 #pragma unroll
     for (int t = 0; t < 6; t++) acc = gmul(tab(t), acc) ^ shfl4_down(acc, 1u << t);
-    const uint4 ek0 = aes.encrypt<NR>(make_uint4(p.n0, p.n1, p.n2, bswap32(1u)), rk);  // E_K(J0)
-    const uint4 tag = shfl4(gmul(tab(0), acc), 0) ^ ek0;                                 // Y = Q * H, from lane 0
+    const uint4 ek0 = pad ? shfl4(ek, (int)pad - 1)  // (pad == 0: no idle lane in pass 0)
+                          : aes.encrypt<NR>(make_uint4(p.n0, p.n1, p.n2, bswap32(1u)), rk);
+    const uint4 tag = shfl4(gmul(tab(0), acc), 0) ^ ek0;  // Y = Q * H, from lane 0
 
     if (SEAL) {
         if (lane == 0) st16(pay + p.len, tag);

@@ -342,22 +342,27 @@ __global__ __launch_bounds__(256) void chacha_burst_kernel(const DevKey *__restr
     const uint32_t aad_len = d.aad_len, len = d.pt_len;
     uint8_t *pay = base + aad_len;
 
-    uint32_t ks[16];
-    chacha_block(k, 0, n0, n1, n2, ks);  // one-time Poly1305 key (every lane: uniform)
-    Poly1305 key_r;
-    key_r.init(ks[0], ks[1], ks[2], ks[3]);
-    const uint32_t sw0 = ks[4], sw1 = ks[5], sw2 = ks[6], sw3 = ks[7];
-    P130 rp[7];  // r^(2^t)
-    rp[0] = P130{key_r.r0, key_r.r1, key_r.r2, key_r.r3, key_r.r4};
-#pragma unroll
-    for (int t = 1; t < 7; t++) rp[t] = p_mul(rp[t - 1], rp[t - 1]);
-
     const uint32_t a = (aad_len + 15u) >> 4, c = (len + 15u) >> 4, m = a + c + 1;
     const uint32_t K = (m + 63u) >> 6, pad = 64u * K - m;
     P130 acc{0, 0, 0, 0, 0};
     uint4 ct0 = make_uint4(0, 0, 0, 0), ct1 = ct0;  // ciphertext blocks 0/1 where this lane owns them (HP sample)
+    uint4 pk0 = ct0, pk1 = ct0;                       // the one-time Poly1305 key (r, s), in lane pad - 1
+    P130 rp[7];                                       // r^(2^t), from pass 1 on (pass 0 needs no power of r)
     for (uint32_t kk = 0; kk < K; kk++) {
         const int i = (int)(lane + 64u * kk) - (int)pad;
+        const bool data = i >= (int)a && i < (int)(a + c);
+        const bool key0 = kk == 0 && i == -1;  // ChaCha block 0 (the Poly1305 key) rides in an idle lane of pass 0
+        const uint32_t b = (uint32_t)i - a;
+        uint4 in = make_uint4(0, 0, 0, 0);
+        uint32_t ks[16];
+        if (data || key0) {
+            if (data) in = ld16(pay + 16u * b);
+            chacha_block(k, data ? 1u + (b >> 2) : 0u, n0, n1, n2, ks);
+        }
+        if (key0) {
+            pk0 = make_uint4(ks[0], ks[1], ks[2], ks[3]);
+            pk1 = make_uint4(ks[4], ks[5], ks[6], ks[7]);
+        }
         uint4 x = make_uint4(0, 0, 0, 0);
         uint32_t hib = 1u << 24;  // the 2^128 bit of every (padded, full) MAC block
         if (i < 0) {
@@ -366,14 +371,12 @@ __global__ __launch_bounds__(256) void chacha_burst_kernel(const DevKey *__restr
             const uint32_t off = 16u * (uint32_t)i;
             x = ld16(base + off);
             if (aad_len - off < 16u) x = keep_bytes(x, aad_len - off);
-        } else if (i < (int)(a + c)) {
-            const uint32_t b = (uint32_t)i - a, r = len - 16u * b, q = b & 3u;
-            chacha_block(k, 1u + (b >> 2), n0, n1, n2, ks);
+        } else if (data) {
+            const uint32_t r = len - 16u * b, q = b & 3u;
             const uint4 kq = make_uint4(q == 0 ? ks[0] : q == 1 ? ks[4] : q == 2 ? ks[8] : ks[12],
                                         q == 0 ? ks[1] : q == 1 ? ks[5] : q == 2 ? ks[9] : ks[13],
                                         q == 0 ? ks[2] : q == 1 ? ks[6] : q == 2 ? ks[10] : ks[14],
                                         q == 0 ? ks[3] : q == 1 ? ks[7] : q == 2 ? ks[11] : ks[15]);
-            uint4 in = ld16(pay + 16u * b);
             uint4 out = in ^ kq;
             if (r >= 16u) {
                 st16(pay + 16u * b, out);
@@ -389,8 +392,27 @@ __global__ __launch_bounds__(256) void chacha_burst_kernel(const DevKey *__restr
             x = make_uint4(aad_len, 0, len, 0);  // le64(aad_len) || le64(ct_len)
         }
         const P130 xb = p_block(x, hib);
-        acc = kk ? p_add(p_mul(acc, rp[6]), xb) : xb;
+        if (kk == 0) {
+            acc = xb;
+            // Poly1305 key to every lane (pad == 0: no idle lane in pass 0, so every lane computes block 0)
+            if (pad) {
+                pk0 = shfl4(pk0, (int)pad - 1);
+                pk1 = shfl4(pk1, (int)pad - 1);
+            } else {
+                chacha_block(k, 0, n0, n1, n2, ks);
+                pk0 = make_uint4(ks[0], ks[1], ks[2], ks[3]);
+                pk1 = make_uint4(ks[4], ks[5], ks[6], ks[7]);
+            }
+            Poly1305 key_r;
+            key_r.init(pk0.x, pk0.y, pk0.z, pk0.w);
+            rp[0] = P130{key_r.r0, key_r.r1, key_r.r2, key_r.r3, key_r.r4};
+#pragma unroll
+            for (int t = 1; t < 7; t++) rp[t] = p_mul(rp[t - 1], rp[t - 1]);
+        } else {
+            acc = p_add(p_mul(acc, rp[6]), xb);
+        }
     }
+    const uint32_t sw0 = pk1.x, sw1 = pk1.y, sw2 = pk1.z, sw3 = pk1.w;
 #pragma unroll
     for (int t = 0; t < 6; t++) acc = p_add(p_mul(acc, rp[t]), p_shfl_down(acc, 1u << t));
     const P130 y = p_mul(acc, rp[0]);

@@ -56,9 +56,9 @@ void qpp_ctx_destroy(qpp_ctx *ctx);
 /* Default stream used by the per-packet functions and by batch calls given stream == NULL. */
 void *qpp_ctx_stream(qpp_ctx *ctx);
 int qpp_ctx_synchronize(qpp_ctx *ctx);
-/* AES-GCM batches of at most max_packets packets (default 8192, env QPP_BURST_MAX) run one wave per packet
- * (latency: a 64-packet GSO burst); larger ones one lane per packet (throughput).  0 = always lane per packet.
- * Outputs are identical either way. */
+/* AES-GCM batches of at most max_packets packets (default 16384, env QPP_BURST_MAX) run one wave per packet
+ * (latency: a 64-packet GSO burst); larger ones one lane per packet (throughput).  ChaCha20-Poly1305 batches switch
+ * at max_packets / 4.  0 = always lane per packet.  Outputs are identical either way. */
 int qpp_ctx_set_burst_max(qpp_ctx *ctx, size_t max_packets);
 int qpp_abi_version(void);
 

@@ -537,7 +537,7 @@ int qpp_seal_batch(qpp_ctx *ctx, const qpp_pkt *descs, size_t n, uint8_t *arena,
     }
     if (!(flags & QPP_ONLY_AES))
         HIP_TRY(ctx, launch_chacha(true, ctx->d_keys, descs, (uint32_t)n, arena, masks, status, flags,
-                                   n <= ctx->burst_max, s));
+                                   n <= (ctx->burst_max >> kChachaBurstShift), s));
     return QPP_OK;
 }
 
@@ -563,7 +563,7 @@ int qpp_open_batch(qpp_ctx *ctx, const qpp_pkt *descs, size_t n, uint8_t *arena,
     }
     if (!(flags & QPP_ONLY_AES))
         HIP_TRY(ctx, launch_chacha(false, ctx->d_keys, descs, (uint32_t)n, arena, nullptr, status, 0,
-                                   n <= ctx->burst_max, s));
+                                   n <= (ctx->burst_max >> kChachaBurstShift), s));
     return QPP_OK;
 }
 

@@ -120,12 +120,12 @@ __global__ __launch_bounds__(kPlanBlock) void plan_scatter(const DevKey *__restr
     }
 }
 
-// Small batches (n <= kPlanSmallMax, key_cap <= kMaxPlanKeys): the three stages above in ONE workgroup and one
+// Small batches (n <= kPlanSmallMax = 8 Ki, key_cap <= kMaxPlanKeys): the three stages above in ONE workgroup and one
 // launch (a GSO burst pays ~4 us here instead of a memset + three launches, ~17 us).  Each thread keeps the keys
 // of its <= 8 packets in registers; keys are scanned 8 per thread with a wave scan + a 16-entry workgroup scan.
 // Dynamic LDS: cur[kMaxPlanKeys + 1] (counts, then scatter cursors), ist[kMaxPlanKeys + 1] (first work item),
 // wave totals.
-constexpr uint32_t kPlanSmallMax = 8 * kPlanBlock;
+constexpr uint32_t kPlanSmallMax = 8 * kPlanBlock;  // (at 16 Ki the one workgroup took ~18 us more than the 3 launches)
 constexpr uint32_t kPlanSmallLds = 4 * (2 * (kMaxPlanKeys + 1) + 64);
 
 __global__ __launch_bounds__(kPlanBlock) void plan_small(const DevKey *__restrict__ keys, uint32_t key_cap,

@@ -87,7 +87,9 @@ struct WorkItem {
 };
 
 constexpr int kMinPacketsPerItem = 4;    // smallest AES work item: burst kernel, one packet per wave (plan scratch)
-constexpr uint32_t kBurstMaxDefault = 8192;   // batches up to this many packets use the wave-per-packet kernel
+constexpr uint32_t kBurstMaxDefault = 16384;  // AES batches up to this many packets run one wave per packet
+constexpr uint32_t kChachaBurstShift = 2;     // ChaCha20-Poly1305 batches up to burst_max >> 2 do (its lane kernel
+                                              // fills the chip with fewer packets: crossover ~6 Ki vs ~20 Ki)
 constexpr uint32_t kTxqZeroCopyMax = 256;     // txq flushes up to this many packets run on the pinned ring in place
 constexpr int kDefaultAesVariant = 0;  // see aes_gcm.hip launch_variant
 constexpr int kMaxPlanKeys = 8192;      // keys binned in LDS by the plan kernels (larger tables: global bins)

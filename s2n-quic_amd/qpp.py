@@ -34,7 +34,7 @@ PKT_DTYPE = np.dtype([("pn", "<u8"), ("key_idx", "<u4"), ("off", "<u4"), ("aad_l
                       ("pn_len", "u1"), ("flags", "u1"), ("reserved", "<u2")])
 assert PKT_DTYPE.itemsize == 24
 PKT_SKIP = 0x1
-BURST_MAX_DEFAULT = 8192  # kBurstMaxDefault (qpp_internal.h): larger AES batches run one lane per packet
+BURST_MAX_DEFAULT = 16384  # kBurstMaxDefault (qpp_internal.h): larger AES batches run one lane per packet
 # qpp_rx_pkt (24 bytes): one received, still protected packet
 RX_DTYPE = np.dtype([("largest_pn", "<u8"), ("key_idx", "<u4", (2,)), ("off", "<u4"), ("header_len", "<u2"),
                      ("len", "<u2")])

@@ -28,7 +28,7 @@ def path(request, ctx):
     """AES-GCM kernel path: wave per packet (small batches) or lane per packet (large); same outputs."""
     ctx.set_burst_max(1 << 30 if request.param == "burst" else 0)
     yield request.param
-    ctx.set_burst_max(8192)
+    ctx.set_burst_max(16384)
 
 
 # ------------------------------------------------------------------ RFC 9001 Appendix A through the trait mirror

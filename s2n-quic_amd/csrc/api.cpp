@@ -30,11 +30,8 @@ struct qpp_ctx {
     uint32_t plan_n_cap = 0, plan_key_cap = 0;
     // per-packet staging
     uint8_t *d_stage = nullptr, *h_stage = nullptr;
+    uint8_t *v_stage = nullptr;  // device view of the pinned h_stage (zero-copy per-packet calls)
     size_t stage_cap = 0;
-    qpp_pkt *d_desc1 = nullptr;
-    int8_t *d_status1 = nullptr;
-    uint8_t *d_mask1 = nullptr;
-    PlanBuffers plan1{};  // host-built plan for a single AES packet
     std::string last_error;
 };
 
@@ -122,6 +119,9 @@ int ensure_stage(qpp_ctx *ctx, size_t bytes) {
     if (ctx->h_stage) hipHostFree(ctx->h_stage);
     HIP_TRY(ctx, hipMalloc(&ctx->d_stage, cap));
     HIP_TRY(ctx, hipHostMalloc(&ctx->h_stage, cap, hipHostMallocDefault));
+    void *v = nullptr;
+    HIP_TRY(ctx, hipHostGetDevicePointer(&v, ctx->h_stage, 0));
+    ctx->v_stage = (uint8_t *)v;
     ctx->stage_cap = cap;
     return QPP_OK;
 }
@@ -176,54 +176,52 @@ uint32_t suite_mask(const qpp_ctx *ctx) {
     return m;
 }
 
-// One packet through the batch kernels: stage = [pad4 | header | payload | tag].
+// One packet through the batch kernels, zero-copy: the kernel reads and writes the pinned stage directly (no DMA
+// copies; one launch, one wait).  Stage layout: descriptor @0 | perm @32 | n_work @36 | work item @48 | status @64
+// | mask @80 | packet @kOnePkt = [pad 16 | header | payload | tag].
+constexpr size_t kOnePkt = 128;
 int run_one(const qpp_key *k, bool seal, uint64_t pn, const uint8_t *header, size_t header_len, const uint8_t *payload,
             size_t payload_len, uint8_t *out, uint8_t *tag_out, int8_t *status_out) {
     qpp_ctx *ctx = k->ctx;
     if (header_len > 0xffff || payload_len > 0xffff) return QPP_INTERNAL_ERROR;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    const size_t total = 16 + header_len + payload_len + 16;
+    const size_t total = kOnePkt + 16 + header_len + payload_len + 16;
     int rc = ensure_stage(ctx, total);
     if (rc) return rc;
     rc = flush_keys(ctx, ctx->stream);
     if (rc) return rc;
-    uint8_t *h = ctx->h_stage;
+    uint8_t *h = ctx->h_stage, *v = ctx->v_stage;
     memset(h, 0, total);
-    memcpy(h + 16, header, header_len);
-    memcpy(h + 16 + header_len, payload, payload_len);
-    if (!seal) memcpy(h + 16 + header_len + payload_len, tag_out, 16);
-    qpp_pkt d{};
+    uint8_t *pkt = h + kOnePkt;
+    memcpy(pkt + 16, header, header_len);
+    memcpy(pkt + 16 + header_len, payload, payload_len);
+    if (!seal) memcpy(pkt + 16 + header_len + payload_len, tag_out, 16);
+    qpp_pkt &d = *(qpp_pkt *)h;
     d.pn = pn;
     d.key_idx = k->slot;
     d.off = 16;
     d.aad_len = (uint16_t)header_len;
     d.pt_len = (uint16_t)payload_len;
+    *(uint32_t *)(h + 32) = 0;  // perm = {0}
+    *(uint32_t *)(h + 36) = 1;  // one work item, on this key
+    *(WorkItem *)(h + 48) = WorkItem{k->slot, 0, 1, ctx->h_keys[k->slot].nr};
+    h[64] = (uint8_t)QPP_INTERNAL_ERROR;  // overwritten by the kernel
+    const PlanBuffers pb{nullptr, nullptr, nullptr, (uint32_t *)(v + 32), (WorkItem *)(v + 48), (uint32_t *)(v + 36)};
     hipStream_t s = ctx->stream;
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->d_stage, h, total, hipMemcpyHostToDevice, s));
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->d_desc1, &d, sizeof d, hipMemcpyHostToDevice, s));
+    const qpp_pkt *vd = (const qpp_pkt *)v;
+    int8_t *vst = (int8_t *)(v + 64);
     if (is_aes(k->suite)) {
-        // host-built plan for one packet: perm = {0}, one work item on this key
-        const uint32_t zero = 0, one = 1;
-        WorkItem w{k->slot, 0, 1, ctx->h_keys[k->slot].nr};
-        HIP_TRY(ctx, hipMemcpyAsync(ctx->plan1.perm, &zero, 4, hipMemcpyHostToDevice, s));
-        HIP_TRY(ctx, hipMemcpyAsync(ctx->plan1.work, &w, sizeof w, hipMemcpyHostToDevice, s));
-        HIP_TRY(ctx, hipMemcpyAsync(ctx->plan1.n_work, &one, 4, hipMemcpyHostToDevice, s));
         // key_cap = 0: grid = plan_max_work(1, 0, per) = 1; only work item 0 exists
-        HIP_TRY(ctx, (ctx->burst_max ? launch_aes_gcm_burst : launch_aes_gcm)(seal, ctx->d_keys, ctx->d_desc1,
-                                                                             ctx->plan1, 1, 0, 1, ctx->d_stage,
-                                                                             ctx->d_mask1, ctx->d_status1, 0,
+        HIP_TRY(ctx, (ctx->burst_max ? launch_aes_gcm_burst : launch_aes_gcm)(seal, ctx->d_keys, vd, pb, 1, 0, 1,
+                                                                             v + kOnePkt, v + 80, vst, 0,
                                                                              1u << k->suite, s));
     } else {
-        HIP_TRY(ctx, launch_chacha(seal, ctx->d_keys, ctx->d_desc1, 1, ctx->d_stage, ctx->d_mask1, ctx->d_status1, 0,
-                                   ctx->burst_max > 0, s));
+        HIP_TRY(ctx, launch_chacha(seal, ctx->d_keys, vd, 1, v + kOnePkt, v + 80, vst, 0, ctx->burst_max > 0, s));
     }
-    int8_t st = QPP_OK;
-    HIP_TRY(ctx, hipMemcpyAsync(h, ctx->d_stage, total, hipMemcpyDeviceToHost, s));
-    HIP_TRY(ctx, hipMemcpyAsync(&st, ctx->d_status1, 1, hipMemcpyDeviceToHost, s));
     HIP_TRY(ctx, hipStreamSynchronize(s));
-    memcpy(out, h + 16 + header_len, payload_len);
-    if (seal) memcpy(tag_out, h + 16 + header_len + payload_len, 16);
-    *status_out = st;
+    memcpy(out, pkt + 16 + header_len, payload_len);
+    if (seal) memcpy(tag_out, pkt + 16 + header_len + payload_len, 16);
+    *status_out = (int8_t)h[64];
     secure_zero(h, total);
     return QPP_OK;
 }
@@ -250,12 +248,6 @@ int qpp_ctx_create(int device, qpp_ctx **out) {
     do {
         if (fail(ctx, hipSetDevice(device), "hipSetDevice")) { rc = QPP_DEVICE_ERROR; break; }
         if (fail(ctx, hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking), "stream")) { rc = QPP_DEVICE_ERROR; break; }
-        if (fail(ctx, hipMalloc(&ctx->d_desc1, sizeof(qpp_pkt)), "alloc")) { rc = QPP_DEVICE_ERROR; break; }
-        if (fail(ctx, hipMalloc(&ctx->d_status1, 16), "alloc")) { rc = QPP_DEVICE_ERROR; break; }
-        if (fail(ctx, hipMalloc(&ctx->d_mask1, 16), "alloc")) { rc = QPP_DEVICE_ERROR; break; }
-        if (fail(ctx, hipMalloc(&ctx->plan1.perm, 16), "alloc")) { rc = QPP_DEVICE_ERROR; break; }
-        if (fail(ctx, hipMalloc(&ctx->plan1.work, sizeof(WorkItem) * 2), "alloc")) { rc = QPP_DEVICE_ERROR; break; }
-        if (fail(ctx, hipMalloc(&ctx->plan1.n_work, 16), "alloc")) { rc = QPP_DEVICE_ERROR; break; }
         rc = grow_keys(ctx, 64);
     } while (0);
     if (rc) {
@@ -280,10 +272,8 @@ void qpp_ctx_destroy(qpp_ctx *ctx) {
     secure_zero(ctx->h_keys.data(), sizeof(DevKey) * ctx->h_keys.size());
     PlanBuffers &p = ctx->plan;
     hipFree(p.counts); hipFree(p.cursor); hipFree(p.istart); hipFree(p.perm); hipFree(p.work); hipFree(p.n_work);
-    hipFree(ctx->plan1.perm); hipFree(ctx->plan1.work); hipFree(ctx->plan1.n_work);
     hipFree(ctx->d_stage);
     if (ctx->h_stage) hipHostFree(ctx->h_stage);
-    hipFree(ctx->d_desc1); hipFree(ctx->d_status1); hipFree(ctx->d_mask1);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -494,21 +484,20 @@ int qpp_hp_mask(const qpp_key *key, const uint8_t *sample, size_t sample_len, ui
     if (!key || !sample || !mask || sample_len < 16) return QPP_INTERNAL_ERROR;
     qpp_ctx *ctx = key->ctx;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    int rc = ensure_stage(ctx, 64);
+    int rc = ensure_stage(ctx, 128);
     if (rc) return rc;
     rc = flush_keys(ctx, ctx->stream);
     if (rc) return rc;
-    memset(ctx->h_stage, 0, 64);
-    memcpy(ctx->h_stage + 4, sample, 16);
-    qpp_pkt d{};
+    // zero-copy: descriptor @0, sample @64 (+4), mask @96 of the pinned stage, read and written by the kernel
+    uint8_t *h = ctx->h_stage;
+    memset(h, 0, 128);
+    memcpy(h + 64 + 4, sample, 16);
+    qpp_pkt &d = *(qpp_pkt *)h;
     d.key_idx = key->slot;  // off = aad_len = pn_len = 0: sample at offset 4
     hipStream_t s = ctx->stream;
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->d_stage, ctx->h_stage, 64, hipMemcpyHostToDevice, s));
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->d_desc1, &d, sizeof d, hipMemcpyHostToDevice, s));
-    HIP_TRY(ctx, launch_hp_mask(ctx->d_keys, ctx->d_desc1, 1, ctx->d_stage, ctx->d_mask1, s));
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->h_stage + 32, ctx->d_mask1, 5, hipMemcpyDeviceToHost, s));
+    HIP_TRY(ctx, launch_hp_mask(ctx->d_keys, (const qpp_pkt *)ctx->v_stage, 1, ctx->v_stage + 64, ctx->v_stage + 96, s));
     HIP_TRY(ctx, hipStreamSynchronize(s));
-    memcpy(mask, ctx->h_stage + 32, 5);
+    memcpy(mask, h + 96, 5);
     return QPP_OK;
 }
 

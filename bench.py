@@ -8,7 +8,7 @@ Multi-GPU (torchrun, one process per GPU): every rank seals/opens its own shard 
 gloo on CPU tensors carries only the barrier and the max-over-ranks time.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--suite aes128gcm|aes256gcm|chacha20poly1305]
-                    [--packets N] [--pt BYTES] [--keys K] [--mode device|e2e|rx|keys|txq]
+                    [--packets N] [--pt BYTES] [--keys K] [--mode device|e2e|rx|keys|txq|packet]
 """
 import argparse
 import ctypes
@@ -104,10 +104,11 @@ def main():
     ap.add_argument("--pt", type=int, default=1200, help="payload bytes per packet")
     ap.add_argument("--aad", type=int, default=21, help="short header: 0x43 || DCID16 || PN4")
     ap.add_argument("--keys", type=int, default=1)
-    ap.add_argument("--mode", default="device", choices=["device", "e2e", "rx", "keys", "txq"],
+    ap.add_argument("--mode", default="device", choices=["device", "e2e", "rx", "keys", "txq", "packet"],
                     help="device: seal+open in HBM (headline); e2e: pinned host -> HBM -> host; rx: receive path "
                          "(unprotect -> PN expand -> open); keys: device key schedule (key-update churn); "
-                         "txq: 64-packet GSO-burst flush latency through the transmit queue")
+                         "txq: 64-packet GSO-burst flush latency through the transmit queue; packet: per-packet trait-API "
+                         "latency")
     ap.add_argument("--cpu-seconds", type=float, default=1.5)
     ap.add_argument("--chunks", type=int, default=16, help="e2e: pipeline chunks (H2D / seal+open / D2H overlap)")
     ap.add_argument("--no-cpu", action="store_true")
@@ -139,6 +140,8 @@ def main():
         return keys_churn(args, ctx, suite, rank, world, barrier, max_over_ranks)
     if args.mode == "txq":
         return txq_bursts(args, ctx, keys, rank, world, max_over_ranks)
+    if args.mode == "packet":
+        return per_packet(args, ctx, keys, rank, world, max_over_ranks)
 
     d_arena = ctx.alloc(arena.nbytes)
     d_arena.upload(arena)
@@ -374,7 +377,8 @@ def keys_churn(args, ctx, suite, rank, world, barrier, max_over_ranks):
 
 def txq_bursts(args, ctx, keys, rank, world, max_over_ranks, burst=64):
     """GSO-style bursts (BASELINE configs[3]): the transport encodes `burst` packets into the pinned ring and flushes
-    (qpp_txq_flush = H2D + one seal/HP batch + D2H + wait).  Reports the per-flush latency and the burst rate."""
+    (qpp_txq_flush: bursts <= 256 packets are sealed in place on the pinned ring by the wave-per-packet kernels,
+    one launch + one wait).  Reports the per-flush latency and the burst rate."""
     pt, aad = args.pt, args.aad
     stride = ((aad + pt + 16 + 15) // 16) * 16
     q = qpp.TxQueue(ctx, burst * stride, burst)
@@ -393,11 +397,39 @@ def txq_bursts(args, ctx, keys, rank, world, max_over_ranks, burst=64):
     t = max_over_ranks(float(np.median(lat)))
     if rank == 0:
         print(json.dumps({
-            "metric": f"txq flush latency, {burst}-packet GSO burst of {pt} B (pinned ring -> HBM -> ring), median",
+            "metric": f"txq flush latency, {burst}-packet GSO burst of {pt} B (sealed in place on the pinned ring), median",
             "value": round(1e6 * t, 1), "unit": "us", "higher_is_better": False, "n_gpus": world,
             "burst_gib_s": round(burst * pt / t / GiB, 3), "suite": args.suite, "flushes": len(lat),
         }), flush=True)
     q.close()
+    ctx.close()
+
+
+def per_packet(args, ctx, keys, rank, world, max_over_ranks, calls=300):
+    """The trait-shaped per-packet face (Key::encrypt -> qpp_seal, Key::decrypt -> qpp_open): one packet per call,
+    as quic/s2n-quic-transport calls it today.  Reports the median call latency (zero-copy, one launch per call)."""
+    rng = np.random.default_rng(10)
+    hdr = bytes([0x43]) + bytes(args.aad - 1)
+    pt = rng.integers(0, 256, args.pt, dtype=np.uint8).tobytes()
+    k = keys[0]
+    ts, to = [], []
+    for i in range(args.warmup + calls):
+        t0 = time.perf_counter()
+        ct = k.encrypt(i, hdr, pt)
+        t1 = time.perf_counter()
+        if k.decrypt(i, hdr, ct) != pt:
+            raise SystemExit("per-packet round trip failed")
+        t2 = time.perf_counter()
+        if i >= args.warmup:
+            ts.append(t1 - t0)
+            to.append(t2 - t1)
+    t = max_over_ranks(float(np.median(ts)))
+    if rank == 0:
+        print(json.dumps({
+            "metric": f"per-packet Key::encrypt latency ({args.pt} B, qpp_seal), median", "value": round(1e6 * t, 1),
+            "unit": "us", "higher_is_better": False, "n_gpus": world, "suite": args.suite,
+            "decrypt_us": round(1e6 * float(np.median(to)), 1), "calls": calls,
+        }), flush=True)
     ctx.close()
 
 

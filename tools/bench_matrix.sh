@@ -17,5 +17,7 @@ run rx_chacha_64keys --mode rx --suite chacha20poly1305 --keys 64 && \
 run keys_4ki_aes128 --mode keys --keys 4096 && \
 run txq_aes128 --mode txq && \
 run txq_chacha --mode txq --suite chacha20poly1305 && \
+run packet_aes128 --mode packet && \
+run packet_chacha --mode packet --suite chacha20poly1305 && \
 run e2e_aes128 --mode e2e --steps 3 && \
 run e2e_c5_4ki_keys --mode e2e --keys 4096 --packets 2097152 --steps 3

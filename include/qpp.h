@@ -41,6 +41,7 @@ typedef enum qpp_status {
     QPP_INTERNAL_ERROR = 3, /* packet_protection::Error::INTERNAL_ERROR (seal failure, bad capacity) */
     QPP_UNSUPPORTED = 4,    /* NegotiatedCipherSuite::new returned None (cipher_suite/negotiated.rs:52-68) */
     QPP_DEVICE_ERROR = 5,   /* no MI355X / HIP runtime failure: the engine fails loudly, never falls back */
+    QPP_ROTATION_NOT_SUPPORTED = 6, /* dc open::Error::RotationNotSupported (dc/s2n-quic-dc/src/crypto.rs:59-66) */
 } qpp_status;
 
 typedef enum qpp_endpoint { QPP_ENDPOINT_CLIENT = 0, QPP_ENDPOINT_SERVER = 1 } qpp_endpoint;
@@ -121,6 +122,31 @@ int qpp_open(const qpp_key *key, uint64_t pn, const uint8_t *header, size_t head
              uint8_t *payload, size_t payload_len);
 /* HeaderKey::{sealing,opening}_header_protection_mask(sample) -> [u8; 5] (header_key.rs:10-30,52-56). */
 int qpp_hp_mask(const qpp_key *key, const uint8_t *sample, size_t sample_len, uint8_t mask[5]);
+
+/* ------------------------------------------------------------------ dc consumers
+ * dc/s2n-quic-dc's packet keys use the same AEAD, nonce (u64 PN -> 0u32 || be64, XOR iv; dc/s2n-quic-dc/src/crypto.rs:
+ * 178-185, crypto/awslc.rs:364-370) and AAD = header as the QUIC path, so they run on the same kernels.  dc packets
+ * in a device arena are plain qpp_pkt records (pn_len = 0, no HP flags) for qpp_seal_batch / qpp_open_batch. */
+
+/* seal::Application::new / open::Application::new(key, iv, algorithm) (crypto/awslc.rs:24-33,157-166): raw key and
+ * iv, no header key (the dc protocol has no header protection).  Any of the three suites. */
+int qpp_dc_key_new(qpp_ctx *ctx, int suite, const uint8_t *key, size_t key_len, const uint8_t iv[12], qpp_key **out);
+/* seal::Application::encrypt(pn, header, extra_payload, payload_and_tag) (crypto/awslc.rs:53-83):
+ * inline_len = len - 16 - extra_len plaintext bytes at payload_and_tag are sealed in place, the ciphertext of
+ * extra_payload follows them and the 16-byte tag ends the buffer (seal_in_place_scatter).  len < 16 + extra_len
+ * (the reference's `assume!`) is QPP_INTERNAL_ERROR. */
+int qpp_dc_seal(const qpp_key *key, uint64_t pn, const uint8_t *header, size_t header_len,
+                const uint8_t *extra_payload, size_t extra_len, uint8_t *payload_and_tag, size_t len);
+/* open::Application::decrypt(key_phase, pn, header, payload_in, tag, payload_out) (crypto/awslc.rs:176-204):
+ * open_separate_gather.  key_phase != 0 -> QPP_ROTATION_NOT_SUPPORTED; a tag that is not 16 bytes or does not
+ * verify -> QPP_DECRYPT_ERROR (open::Error::InvalidTag), payload_out zeroed. */
+int qpp_dc_open(const qpp_key *key, int key_phase, uint64_t pn, const uint8_t *header, size_t header_len,
+                const uint8_t *payload_in, const uint8_t *tag, size_t tag_len, uint8_t *payload_out,
+                size_t payload_len);
+/* open::Application::decrypt_in_place(key_phase, pn, header, payload, tag) (crypto/awslc.rs:207-227):
+ * open_in_place_separate_tag; errors as qpp_dc_open. */
+int qpp_dc_open_in_place(const qpp_key *key, int key_phase, uint64_t pn, const uint8_t *header, size_t header_len,
+                         uint8_t *payload, size_t payload_len, const uint8_t *tag, size_t tag_len);
 
 /* ------------------------------------------------------------------ batches (device-resident) */
 

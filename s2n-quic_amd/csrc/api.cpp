@@ -501,6 +501,65 @@ int qpp_hp_mask(const qpp_key *key, const uint8_t *sample, size_t sample_len, ui
     return QPP_OK;
 }
 
+// ---------------------------------------------------------------- dc consumers (dc/s2n-quic-dc/src/crypto/awslc.rs)
+
+int qpp_dc_key_new(qpp_ctx *ctx, int suite, const uint8_t *key, size_t key_len, const uint8_t iv[12], qpp_key **out) {
+    // awslc.rs:24-33,157-166: key + iv only; the unused header-key slot stays zero
+    static const uint8_t no_hp[32] = {0};
+    if (!valid_suite(suite)) return QPP_UNSUPPORTED;
+    return qpp_key_new_raw(ctx, suite, key, key_len, iv, no_hp, suite_key_len(suite), out);
+}
+
+int qpp_dc_seal(const qpp_key *key, uint64_t pn, const uint8_t *header, size_t header_len, const uint8_t *extra_payload,
+                size_t extra_len, uint8_t *payload_and_tag, size_t len) {
+    // awslc.rs:53-83: inline_len = len - tag - extra; seal_in_place_scatter(in_out = [0, inline), extra_out_and_tag)
+    if (!key || (!header && header_len) || (!extra_payload && extra_len) || !payload_and_tag) return QPP_INTERNAL_ERROR;
+    if (len < 16 || len - 16 < extra_len) return QPP_INTERNAL_ERROR;
+    const size_t msg = len - 16, inline_len = msg - extra_len;
+    int8_t st;
+    int rc;
+    if (!extra_len) {
+        rc = run_one(key, true, pn, header, header_len, payload_and_tag, msg, payload_and_tag, payload_and_tag + msg, &st);
+    } else {
+        std::vector<uint8_t> flat(msg);  // inline || extra as one message; the sealed bytes land in payload_and_tag
+        if (inline_len) memcpy(flat.data(), payload_and_tag, inline_len);
+        memcpy(flat.data() + inline_len, extra_payload, extra_len);
+        rc = run_one(key, true, pn, header, header_len, flat.data(), msg, payload_and_tag, payload_and_tag + msg, &st);
+        secure_zero(flat.data(), flat.size());
+    }
+    return rc ? rc : st;
+}
+
+int qpp_dc_open(const qpp_key *key, int key_phase, uint64_t pn, const uint8_t *header, size_t header_len,
+                const uint8_t *payload_in, const uint8_t *tag, size_t tag_len, uint8_t *payload_out, size_t payload_len) {
+    // awslc.rs:176-204: ensure!(key_phase == Zero, RotationNotSupported); open_separate_gather -> InvalidTag
+    if (!key || (!header && header_len) || ((!payload_in || !payload_out) && payload_len) || (!tag && tag_len))
+        return QPP_INTERNAL_ERROR;
+    if (key_phase != 0) return QPP_ROTATION_NOT_SUPPORTED;
+    if (tag_len != 16) {
+        if (payload_len) memset(payload_out, 0, payload_len);
+        return QPP_DECRYPT_ERROR;
+    }
+    uint8_t t[16];
+    memcpy(t, tag, 16);
+    int8_t st;
+    int rc = run_one(key, false, pn, header, header_len, payload_in, payload_len, payload_out, t, &st);
+    return rc ? rc : st;
+}
+
+int qpp_dc_open_in_place(const qpp_key *key, int key_phase, uint64_t pn, const uint8_t *header, size_t header_len,
+                         uint8_t *payload, size_t payload_len, const uint8_t *tag, size_t tag_len) {
+    // awslc.rs:207-227: open_in_place_separate_tag
+    if (!key || (!header && header_len) || (!payload && payload_len) || (!tag && tag_len)) return QPP_INTERNAL_ERROR;
+    if (key_phase != 0) return QPP_ROTATION_NOT_SUPPORTED;
+    if (tag_len != 16) return QPP_DECRYPT_ERROR;
+    uint8_t t[16];
+    memcpy(t, tag, 16);
+    int8_t st;
+    int rc = run_one(key, false, pn, header, header_len, payload, payload_len, payload, t, &st);
+    return rc ? rc : st;
+}
+
 // ---------------------------------------------------------------- batches
 
 int qpp_seal_batch(qpp_ctx *ctx, const qpp_pkt *descs, size_t n, uint8_t *arena, uint8_t *masks, int8_t *status,

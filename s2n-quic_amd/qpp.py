@@ -26,6 +26,7 @@ KEY_LEN = {1: 16, 2: 32, 3: 32}
 HASH_LEN = {1: 32, 2: 48, 3: 32}
 
 OK, DECODE_ERROR, DECRYPT_ERROR, INTERNAL_ERROR, UNSUPPORTED, DEVICE_ERROR = 0, 1, 2, 3, 4, 5
+ROTATION_NOT_SUPPORTED = 6  # dc open::Error::RotationNotSupported
 HP_MASK_OUT, HP_APPLY, ONLY_AES, ONLY_CHACHA = 0x1, 0x2, 0x10, 0x20
 ENDPOINT_CLIENT, ENDPOINT_SERVER = 0, 1
 
@@ -51,14 +52,16 @@ EXPORTS = [
     "qpp_stream_destroy", "qpp_stream_synchronize", "qpp_event_create", "qpp_event_destroy", "qpp_event_record",
     "qpp_event_elapsed_ms", "qpp_stream_wait_event", "qpp_unprotect_open_batch", "qpp_pn_truncate", "qpp_pn_expand",
     "qpp_key_new_batch", "qpp_txq_create", "qpp_txq_destroy", "qpp_txq_ring", "qpp_txq_push", "qpp_txq_flush",
-    "qpp_txq_pending", "qpp_memcpy_d2d", "qpp_ctx_set_burst_max",
+    "qpp_txq_pending", "qpp_memcpy_d2d", "qpp_ctx_set_burst_max", "qpp_dc_key_new", "qpp_dc_seal", "qpp_dc_open",
+    "qpp_dc_open_in_place",
 ]
 
 
 class QppError(RuntimeError):
     def __init__(self, code, what=""):
         self.code = code
-        names = {1: "DECODE_ERROR", 2: "DECRYPT_ERROR", 3: "INTERNAL_ERROR", 4: "UNSUPPORTED", 5: "DEVICE_ERROR"}
+        names = {1: "DECODE_ERROR", 2: "DECRYPT_ERROR", 3: "INTERNAL_ERROR", 4: "UNSUPPORTED", 5: "DEVICE_ERROR",
+                 6: "ROTATION_NOT_SUPPORTED"}
         super().__init__(f"{names.get(code, code)} {what}".strip())
 
 
@@ -129,6 +132,10 @@ def lib():
             "qpp_txq_pending": (sz, [vp]),
             "qpp_memcpy_d2d": (ctypes.c_int, [vp, vp, vp, sz, vp]),
             "qpp_ctx_set_burst_max": (ctypes.c_int, [vp, sz]),
+            "qpp_dc_key_new": (ctypes.c_int, [vp, ctypes.c_int, vp, sz, vp, ctypes.POINTER(vp)]),
+            "qpp_dc_seal": (ctypes.c_int, [vp, u64, vp, sz, vp, sz, vp, sz]),
+            "qpp_dc_open": (ctypes.c_int, [vp, ctypes.c_int, u64, vp, sz, vp, vp, sz, vp, sz]),
+            "qpp_dc_open_in_place": (ctypes.c_int, [vp, ctypes.c_int, u64, vp, sz, vp, sz, vp, sz]),
         }
         assert set(sig) == set(EXPORTS)
         for name, (res, args) in sig.items():
@@ -235,6 +242,14 @@ class Context:
         if rc != OK:
             raise QppError(rc, "qpp_key_new_raw")
         return Key(self, h.value)
+
+    def dc_key(self, suite, key, iv):
+        """dc seal/open::Application::new(key, iv, algorithm) (dc/s2n-quic-dc/src/crypto/awslc.rs:24-33)"""
+        h = vp()
+        rc = lib().qpp_dc_key_new(self.handle, suite, _bytes_ptr(key), len(key), _bytes_ptr(iv), ctypes.byref(h))
+        if rc != OK:
+            raise QppError(rc, "qpp_dc_key_new")
+        return DcKey(self, h.value)
 
     def initial_keys(self, endpoint, dcid):
         s, o = vp(), vp()
@@ -379,6 +394,38 @@ class Key:
 
 
 # ------------------------------------------------------------------ synthetic batches (bench + tests)
+
+class DcKey(Key):
+    """dc/s2n-quic-dc crypto::{seal,open}::Application over the same engine (crypto/awslc.rs:40-83,168-227)."""
+
+    def dc_encrypt(self, pn, header, extra_payload, payload_and_tag):
+        """seal::Application::encrypt: returns the sealed payload_and_tag buffer"""
+        extra = bytes(extra_payload or b"")
+        buf = ctypes.create_string_buffer(bytes(payload_and_tag), max(len(payload_and_tag), 1))
+        rc = lib().qpp_dc_seal(self.handle, pn, _bytes_ptr(header), len(header), _bytes_ptr(extra), len(extra), buf,
+                               len(payload_and_tag))
+        if rc != OK:
+            raise QppError(rc, "qpp_dc_seal")
+        return buf.raw[:len(payload_and_tag)]
+
+    def dc_decrypt(self, key_phase, pn, header, payload_in, tag):
+        """open::Application::decrypt (separate input, tag and output)"""
+        out = ctypes.create_string_buffer(max(len(payload_in), 1))
+        rc = lib().qpp_dc_open(self.handle, key_phase, pn, _bytes_ptr(header), len(header), _bytes_ptr(payload_in),
+                               _bytes_ptr(tag), len(tag), out, len(payload_in))
+        if rc == DECRYPT_ERROR:
+            raise DecryptError(rc, "qpp_dc_open")
+        if rc != OK:
+            raise QppError(rc, "qpp_dc_open")
+        return out.raw[:len(payload_in)]
+
+    def dc_decrypt_in_place(self, key_phase, pn, header, payload, tag):
+        """open::Application::decrypt_in_place; returns (status, buffer after the call)"""
+        buf = ctypes.create_string_buffer(bytes(payload), max(len(payload), 1))
+        rc = lib().qpp_dc_open_in_place(self.handle, key_phase, pn, _bytes_ptr(header), len(header), buf,
+                                        len(payload), _bytes_ptr(tag), len(tag))
+        return rc, buf.raw[:len(payload)]
+
 
 def xoshiro_bytes(seed, n):
     """Deterministic synthetic payload bytes (numpy PCG64 seeded from `seed`)."""

@@ -524,3 +524,43 @@ def test_txq_deferred_seal_matches_encode_packet(ctx, path, flush, monkeypatch):
     q.close()
     for k in keys:
         k.free()
+
+
+# ------------------------------------------------------------------ dc consumers
+
+@pytest.mark.parametrize("name,suite", [("aead_aes128gcm.json", 1), ("aead_aes256gcm.json", 2),
+                                        ("aead_chacha20poly1305.json", 3)])
+def test_dc_application_fixtures(ctx, name, suite):
+    """dc seal/open::Application (dc/s2n-quic-dc/src/crypto/awslc.rs:53-83,176-227) on the golden vectors:
+    the dc nonce (crypto.rs:178-185 into_nonce, awslc.rs:364-370 xor iv) is the QUIC one, so the same CT || tag."""
+    for c in load_golden(name)["cases"]:
+        k = ctx.dc_key(suite, H(c["key"]), H(c["iv"]))
+        pt, aad, want = H(c["pt"]), H(c["aad"]), H(c["ct"] + c["tag"])
+        assert k.dc_encrypt(c["pn"], aad, None, pt + bytes(16)) == want
+        cut = len(pt) // 3  # extra_payload: the tail of the message arrives separately
+        assert k.dc_encrypt(c["pn"], aad, pt[cut:], pt[:cut] + bytes(len(pt) - cut + 16)) == want
+        ct, tag = want[:-16], want[-16:]
+        assert k.dc_decrypt(0, c["pn"], aad, ct, tag) == pt
+        rc, buf = k.dc_decrypt_in_place(0, c["pn"], aad, ct, tag)
+        assert rc == qpp.OK and buf == pt
+        with pytest.raises(qpp.QppError) as e:  # ensure!(key_phase == Zero, RotationNotSupported)
+            k.dc_decrypt(1, c["pn"], aad, ct, tag)
+        assert e.value.code == qpp.ROTATION_NOT_SUPPORTED
+        bad = bytearray(tag)
+        bad[0] ^= 1
+        with pytest.raises(qpp.DecryptError):
+            k.dc_decrypt(0, c["pn"], aad, ct, bytes(bad))
+        rc, buf = k.dc_decrypt_in_place(0, c["pn"], aad, ct, bytes(bad))
+        assert rc == qpp.DECRYPT_ERROR and buf == bytes(len(ct))  # never releases unauthenticated plaintext
+        rc, _ = k.dc_decrypt_in_place(0, c["pn"], aad, ct, tag[:15])
+        assert rc == qpp.DECRYPT_ERROR
+        k.free()
+
+
+def test_dc_seal_capacity(ctx):
+    k = ctx.dc_key(1, bytes(16), bytes(12))
+    with pytest.raises(qpp.QppError) as e:  # payload_and_tag.len() >= tag_len + extra_in.len() (awslc.rs:65-67)
+        k.dc_encrypt(1, b"h", bytes(10), bytes(20))
+    assert e.value.code == qpp.INTERNAL_ERROR
+    assert len(k.dc_encrypt(1, b"h", bytes(4), bytes(20))) == 20
+    k.free()

@@ -13,6 +13,7 @@ namespace qpp {
 namespace {
 
 constexpr int kPlanBlock = 1024;
+constexpr uint32_t kPlanPerThread = 4;  // packets per thread in plan_hist / plan_scatter (amortises the per-block bins)
 
 __device__ __forceinline__ bool is_aes(const DevKey *keys, uint32_t k) {
     return keys[k].suite != QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256;
@@ -27,10 +28,23 @@ __global__ __launch_bounds__(kPlanBlock) void plan_hist(const DevKey *__restrict
     if (local)
         for (uint32_t i = threadIdx.x; i < key_cap; i += blockDim.x) bins[i] = 0;
     __syncthreads();
-    const uint32_t pi = blockIdx.x * blockDim.x + threadIdx.x;
-    if (pi < n) {
-        const uint32_t k = descs[pi].key_idx;
-        if (k < key_cap && is_aes(keys, k)) {
+#pragma unroll
+    for (uint32_t j = 0; j < kPlanPerThread; j++) {
+        const uint32_t pi = (blockIdx.x * kPlanPerThread + j) * blockDim.x + threadIdx.x;
+        uint32_t k = ~0u;
+        if (pi < n) {
+            k = descs[pi].key_idx;
+            if (k >= key_cap || !is_aes(keys, k)) k = ~0u;
+        }
+        // a run of same-key packets fills whole waves (one connection's burst; a single-key batch): one atomic per
+        // wave instead of 64 serialised same-address LDS atomics
+        const uint32_t k0 = __builtin_amdgcn_readfirstlane(k);
+        if (__all(k == k0)) {
+            if (k0 != ~0u && (threadIdx.x & 63u) == 0) {
+                if (local) atomicAdd(&bins[k0], 64u);
+                else atomicAdd(&counts[k0], 64u);
+            }
+        } else if (k != ~0u) {
             if (local) atomicAdd(&bins[k], 1u);
             else atomicAdd(&counts[k], 1u);
         }
@@ -102,13 +116,31 @@ __global__ __launch_bounds__(kPlanBlock) void plan_scatter(const DevKey *__restr
     if (local)
         for (uint32_t i = threadIdx.x; i < key_cap; i += blockDim.x) bins[i] = 0;
     __syncthreads();
-    const uint32_t pi = blockIdx.x * blockDim.x + threadIdx.x;
-    uint32_t k = 0xffffffffu, rank = 0;
-    if (pi < n) {
-        k = descs[pi].key_idx;
-        if (k >= key_cap || !is_aes(keys, k)) k = 0xffffffffu;
-        else if (local) rank = atomicAdd(&bins[k], 1u);
-        else perm[atomicAdd(&cursor[k], 1u)] = pi;
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t ks[kPlanPerThread], rank[kPlanPerThread];
+#pragma unroll
+    for (uint32_t j = 0; j < kPlanPerThread; j++) {
+        const uint32_t pi = (blockIdx.x * kPlanPerThread + j) * blockDim.x + threadIdx.x;
+        uint32_t k = 0xffffffffu;
+        rank[j] = 0;
+        if (pi < n) {
+            k = descs[pi].key_idx;
+            if (k >= key_cap || !is_aes(keys, k)) k = 0xffffffffu;
+        }
+        const uint32_t k0 = __builtin_amdgcn_readfirstlane(k);
+        if (__all(k == k0)) {  // whole wave on one key (see plan_hist): one reservation of 64 consecutive ranks
+            if (k0 != 0xffffffffu) {
+                uint32_t base = 0;
+                if (lane == 0) base = local ? atomicAdd(&bins[k0], 64u) : atomicAdd(&cursor[k0], 64u);
+                base = (uint32_t)__shfl((int)base, 0, 64) + lane;
+                if (local) rank[j] = base;
+                else perm[base] = pi;
+            }
+        } else if (k != 0xffffffffu) {
+            if (local) rank[j] = atomicAdd(&bins[k], 1u);
+            else perm[atomicAdd(&cursor[k], 1u)] = pi;
+        }
+        ks[j] = k;
     }
     __syncthreads();
     if (local) {
@@ -116,7 +148,9 @@ __global__ __launch_bounds__(kPlanBlock) void plan_scatter(const DevKey *__restr
         for (uint32_t i = threadIdx.x; i < key_cap; i += blockDim.x)
             if (bins[i]) bins[i] = atomicAdd(&cursor[i], bins[i]);
         __syncthreads();
-        if (k != 0xffffffffu) perm[bins[k] + rank] = pi;
+#pragma unroll
+        for (uint32_t j = 0; j < kPlanPerThread; j++)
+            if (ks[j] != 0xffffffffu) perm[bins[ks[j]] + rank[j]] = (blockIdx.x * kPlanPerThread + j) * blockDim.x + threadIdx.x;
     }
 }
 
@@ -217,7 +251,7 @@ hipError_t launch_plan(const DevKey *keys, uint32_t key_cap, const qpp_pkt *desc
     }
     hipError_t e = hipMemsetAsync(pb.counts, 0, sizeof(uint32_t) * key_cap, s);
     if (e != hipSuccess) return e;
-    const dim3 grid((n + kPlanBlock - 1) / kPlanBlock);
+    const dim3 grid((n + kPlanBlock * kPlanPerThread - 1) / (kPlanBlock * kPlanPerThread));
     hipLaunchKernelGGL(plan_hist, grid, dim3(kPlanBlock), 0, s, keys, key_cap, descs, n, pb.counts);
     hipLaunchKernelGGL(plan_scan, dim3(1), dim3(kPlanBlock), 0, s, keys, key_cap, pb.counts, pb.cursor, pb.istart, pb.work,
                        pb.n_work, per);

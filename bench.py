@@ -27,6 +27,7 @@ import qpp  # noqa: E402
 qpp.lib()  # load the engine (and its HIP runtime) before anything else touches the GPU
 
 SUITES = {"aes128gcm": 1, "aes256gcm": 2, "chacha20poly1305": 3}
+WARMUP_MIN_S = 0.25  # see the warmup loop in main()
 METRIC = "GiB/s AEAD seal+open, device-resident, 1200 B packets at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s; 6.29 measured copy)
 GiB = float(1 << 30)
@@ -121,7 +122,8 @@ def main():
     barrier, max_over_ranks = ctl.barrier, ctl.max
 
     suite = SUITES[args.suite]
-    ctx = qpp.Context(local_rank)
+    # QPP_SHARE_DEVICE=1: every rank on GPU 0 (rehearsing the torchrun path on a one-GPU box; never set by the driver)
+    ctx = qpp.Context(0 if os.environ.get("QPP_SHARE_DEVICE") == "1" else local_rank)
     rng = np.random.default_rng(0x5eed0000 + 1)
     keys = [ctx.key(suite, rng.integers(0, 256, qpp.HASH_LEN[suite], dtype=np.uint8).tobytes()) for _ in range(args.keys)]
     n, pt, aad = args.packets, args.pt, args.aad
@@ -166,6 +168,14 @@ def main():
 
     evs = [(ctx.event(), ctx.event(), ctx.event()) for _ in range(args.steps)]
     e0, e1 = ctx.event(), ctx.event()
+    # Clock ramp: with the host-side check above between warmup and the timed region, a 5-step run measured 12 %
+    # below a 20-step run on the same box (the kernels themselves ran slower, per HIP events: the GPU had idled).
+    # So the last untimed steps run right before the barrier, for at least WARMUP_MIN_S, queued without host syncs.
+    t_w = time.perf_counter()
+    while args.warmup and time.perf_counter() - t_w < WARMUP_MIN_S:
+        for _ in range(8):
+            step()
+        ctx.sync(s)
     barrier()
     ctx.sync(s)
     ctx.record(e0, s)

@@ -100,6 +100,7 @@ int ensure_plan(qpp_ctx *ctx, uint32_t n) {
     hipFree(p.counts); hipFree(p.cursor); hipFree(p.istart); hipFree(p.perm); hipFree(p.work); hipFree(p.n_work);
     const uint32_t ncap = std::max(n, ctx->plan_n_cap), kcap = ctx->key_cap;
     HIP_TRY(ctx, hipMalloc(&p.counts, sizeof(uint32_t) * kcap));
+    HIP_TRY(ctx, hipMemset(p.counts, 0, sizeof(uint32_t) * kcap));  // plan_scan re-zeroes it after every plan
     HIP_TRY(ctx, hipMalloc(&p.cursor, sizeof(uint32_t) * kcap));
     HIP_TRY(ctx, hipMalloc(&p.istart, sizeof(uint32_t) * (kcap + 1)));
     HIP_TRY(ctx, hipMalloc(&p.perm, sizeof(uint32_t) * std::max<uint32_t>(ncap, 1)));

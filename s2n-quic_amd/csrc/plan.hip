@@ -59,7 +59,7 @@ __global__ __launch_bounds__(kPlanBlock) void plan_hist(const DevKey *__restrict
 // (b) work items per key -> istart; then every thread emits work items w = tid, tid+1024, ... by a binary
 // search of istart (in LDS), so a single key with 16 Ki work items is not written by one lane.
 __global__ __launch_bounds__(kPlanBlock) void plan_scan(const DevKey *__restrict__ keys, uint32_t key_cap,
-                                                       const uint32_t *__restrict__ counts, uint32_t *__restrict__ cursor,
+                                                       uint32_t *__restrict__ counts, uint32_t *__restrict__ cursor,
                                                        uint32_t *__restrict__ istart_g, WorkItem *__restrict__ work,
                                                        uint32_t *__restrict__ n_work, uint32_t per) {
     __shared__ uint32_t sc[kPlanBlock], si[kPlanBlock];
@@ -106,6 +106,10 @@ __global__ __launch_bounds__(kPlanBlock) void plan_scan(const DevKey *__restrict
         // cursor[] still holds the key's first perm index: plan_scatter runs after this kernel
         work[w] = WorkItem{lo, cursor[lo] + i * per, left < per ? left : per, keys[lo].nr};
     }
+    // counts[] is all-zero between plans (zeroed once at allocation, then here after its last read), so the next
+    // plan_hist needs no memset launch
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < key_cap; k += kPlanBlock) counts[k] = 0;
 }
 
 __global__ __launch_bounds__(kPlanBlock) void plan_scatter(const DevKey *__restrict__ keys, uint32_t key_cap,
@@ -249,8 +253,6 @@ hipError_t launch_plan(const DevKey *keys, uint32_t key_cap, const qpp_pkt *desc
                            pb.work, pb.n_work, per);
         return hipGetLastError();
     }
-    hipError_t e = hipMemsetAsync(pb.counts, 0, sizeof(uint32_t) * key_cap, s);
-    if (e != hipSuccess) return e;
     const dim3 grid((n + kPlanBlock * kPlanPerThread - 1) / (kPlanBlock * kPlanPerThread));
     hipLaunchKernelGGL(plan_hist, grid, dim3(kPlanBlock), 0, s, keys, key_cap, descs, n, pb.counts);
     hipLaunchKernelGGL(plan_scan, dim3(1), dim3(kPlanBlock), 0, s, keys, key_cap, pb.counts, pb.cursor, pb.istart, pb.work,

@@ -525,7 +525,12 @@ __global__ __launch_bounds__(1024) void unprotect_kernel(const DevKey *__restric
         return;
     }
     const DevKey *__restrict__ hk = keys + r.key_idx[0];
+    // All three packet loads are issued before the mask is computed (no dependent byte loads after it): byte 0,
+    // the 4 bytes that may hold the PN (len >= hdr + 20 was checked above) and the sample.
     const uint4 smp = ld16(base + hdr + 4);
+    uint32_t pnw;
+    __builtin_memcpy(&pnw, base + hdr, 4);
+    uint8_t b0 = base[0];
     uint32_t m0, m1;
     if (hk->suite == QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256) {
         uint32_t k[8];
@@ -538,18 +543,15 @@ __global__ __launch_bounds__(1024) void unprotect_kernel(const DevKey *__restric
         m0 = m.x;
         m1 = m.y;
     }
-    uint8_t b0 = base[0];
     const bool is_long = (b0 & 0x80) != 0;
     b0 ^= (uint8_t)m0 & (is_long ? 0x0f : 0x1f);
     base[0] = b0;
     const uint32_t pn_len = (b0 & 3u) + 1u;
-    const uint32_t mm = (m0 >> 8) | (m1 << 24);
-    uint64_t trunc = 0;
-    for (uint32_t j = 0; j < pn_len; j++) {
-        const uint8_t x = base[hdr + j] ^ (uint8_t)(mm >> (8 * j));
-        base[hdr + j] = x;
-        trunc = (trunc << 8) | x;
-    }
+    const uint32_t mm = (m0 >> 8) | (m1 << 24);  // mask bytes 1..4, byte j of the PN at bits 8j
+    // unmask PN bytes [0, pn_len); bytes past pn_len are written back unchanged (this lane owns the packet)
+    pnw ^= pn_len == 4u ? mm : (mm & ((1u << (8u * pn_len)) - 1u));
+    __builtin_memcpy(base + hdr, &pnw, 4);
+    const uint64_t trunc = bswap32(pnw) >> (8u * (4u - pn_len));  // PN bytes big-endian
     d.pn = decode_packet_number(r.largest_pn & kPnMask, trunc, 8 * pn_len);
     d.key_idx = (!is_long && (b0 & 0x04)) ? r.key_idx[1] : r.key_idx[0];
     d.aad_len = (uint16_t)(hdr + pn_len);

@@ -117,12 +117,7 @@ __device__ __forceinline__ void apply_mask(uint8_t *base, uint32_t hdr_len, uint
         mask_out[0] = (uint8_t)m0; mask_out[1] = (uint8_t)(m0 >> 8); mask_out[2] = (uint8_t)(m0 >> 16);
         mask_out[3] = (uint8_t)(m0 >> 24); mask_out[4] = (uint8_t)m1;
     }
-    if (flags & QPP_HP_APPLY) {  // header_crypto.rs:80-95
-        uint8_t b0 = base[0];
-        base[0] = b0 ^ ((uint8_t)m0 & ((b0 & 0x80) ? 0x0f : 0x1f));
-        uint32_t mm = (m0 >> 8) | (m1 << 24);
-        for (uint32_t i = 0; i < pn_len; i++) base[hdr_len + i] ^= (uint8_t)(mm >> (8 * i));
-    }
+    if (flags & QPP_HP_APPLY) hdr_apply(base, hdr_len, pn_len, hdr_load(base, hdr_len), m0, m1);  // header_crypto.rs:80-95
 }
 
 // One lane per packet, software-pipelined over 64-byte chunks: the keystream of chunk c+1 is computed in the same
@@ -548,6 +543,7 @@ __global__ __launch_bounds__(1024) void unprotect_kernel(const DevKey *__restric
     base[0] = b0;
     const uint32_t pn_len = (b0 & 3u) + 1u;
     const uint32_t mm = (m0 >> 8) | (m1 << 24);  // mask bytes 1..4, byte j of the PN at bits 8j
+    if (hdr == 0) pnw = (pnw & 0xffffff00u) | b0;  // PN byte 0 is byte 0, already unmasked above
     // unmask PN bytes [0, pn_len); bytes past pn_len are written back unchanged (this lane owns the packet)
     pnw ^= pn_len == 4u ? mm : (mm & ((1u << (8u * pn_len)) - 1u));
     __builtin_memcpy(base + hdr, &pnw, 4);

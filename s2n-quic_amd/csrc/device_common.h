@@ -216,6 +216,32 @@ __device__ __forceinline__ PacketView load_packet(const qpp_pkt &d, const DevKey
     return p;
 }
 
+// apply_header_protection (header_crypto.rs:80-95) as two independent loads issued before the mask is known and
+// up to 5 independent byte stores: no dependent byte-load loop after the mask.  The dword at base + hdr_len may
+// run past the PN into the payload (callers checked payload >= 4 - pn_len); only bytes [0, pn_len) are stored.
+struct HdrBytes {
+    uint32_t b0, pnw;
+};
+__device__ __forceinline__ HdrBytes hdr_load(const uint8_t *base, uint32_t hdr_len) {
+    HdrBytes h;
+    h.b0 = base[0];
+    __builtin_memcpy(&h.pnw, base + hdr_len, 4);
+    return h;
+}
+__device__ __forceinline__ void hdr_apply(uint8_t *base, uint32_t hdr_len, uint32_t pn_len, HdrBytes h, uint32_t m0,
+                                          uint32_t m1) {
+    const uint32_t nb0 = h.b0 ^ (m0 & ((h.b0 & 0x80) ? 0x0fu : 0x1fu));
+    base[0] = (uint8_t)nb0;
+    // hdr_len == 0 (a header of PN bytes only): PN byte 0 is byte 0 after its first-byte masking, as in the
+    // reference's in-place order
+    const uint32_t pnw = hdr_len ? h.pnw : (h.pnw & 0xffffff00u) | (nb0 & 0xffu);
+    const uint32_t x = pnw ^ ((m0 >> 8) | (m1 << 24));
+    base[hdr_len] = (uint8_t)x;
+    if (pn_len > 1) base[hdr_len + 1] = (uint8_t)(x >> 8);
+    if (pn_len > 2) base[hdr_len + 2] = (uint8_t)(x >> 16);
+    if (pn_len > 3) base[hdr_len + 3] = (uint8_t)(x >> 24);
+}
+
 // Header protection mask from the 16-byte sample (first 5 bytes of AES_hp(sample)).  The HP round keys are read
 // here, once per packet, into VGPRs: hoisted into SGPRs for the whole kernel they pushed the packet round keys out
 // of SGPRs (measured: 36 SGPR spills and per-iteration round-key reloads, a slower seal).
@@ -233,17 +259,14 @@ __device__ __forceinline__ void hp_finish(const AesLds &aes, const uint32_t *hp_
         const uint4 v = src[i];
         hp_rk[4 * i] = v.x; hp_rk[4 * i + 1] = v.y; hp_rk[4 * i + 2] = v.z; hp_rk[4 * i + 3] = v.w;
     }
+    const HdrBytes h = (flags & QPP_HP_APPLY) ? hdr_load(base, hdr_len) : HdrBytes{0, 0};
     uint4 m = aes.encrypt<HNR>(sample, hp_rk);
     if (flags & QPP_HP_MASK_OUT) {
         mask_out[0] = (uint8_t)m.x; mask_out[1] = (uint8_t)(m.x >> 8); mask_out[2] = (uint8_t)(m.x >> 16);
         mask_out[3] = (uint8_t)(m.x >> 24); mask_out[4] = (uint8_t)m.y;
     }
     if (flags & QPP_HP_APPLY) {
-        // header_crypto.rs:80-95
-        uint8_t b0 = base[0];
-        base[0] = b0 ^ ((uint8_t)m.x & ((b0 & 0x80) ? 0x0f : 0x1f));
-        uint32_t mm = (m.x >> 8) | (m.y << 24);
-        for (uint32_t i = 0; i < pn_len; i++) base[hdr_len + i] ^= (uint8_t)(mm >> (8 * i));
+        hdr_apply(base, hdr_len, pn_len, h, m.x, m.y);  // header_crypto.rs:80-95
     }
 }
 

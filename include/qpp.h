@@ -13,6 +13,11 @@
  * Rules: no exceptions cross the ABI; plain pointers and sizes only; a qpp_ctx is used by one
  * host thread at a time and owns one GPU; a qpp_key may be used from one thread at a time
  * (the traits are Send, not Sync).  All memory passed in is owned by the caller.
+ *
+ * Asynchrony: batch calls are asynchronous on the stream they are given.  Freeing a key (or header key) is
+ * stream-ordered: its device record is zeroized after every batch already enqueued on any stream of the context,
+ * and its slot is reused only after that, so a key may be freed while batches that use it are still in flight.
+ * Each stream gets its own plan scratch, so batches on different streams of one context may overlap.
  */
 #ifndef QPP_H
 #define QPP_H
@@ -24,7 +29,7 @@
 extern "C" {
 #endif
 
-#define QPP_ABI_VERSION 1
+#define QPP_ABI_VERSION 2
 
 /* Cipher suites (quic/s2n-quic-crypto/src/cipher_suite.rs:250-301). */
 typedef enum qpp_suite {
@@ -48,6 +53,7 @@ typedef enum qpp_endpoint { QPP_ENDPOINT_CLIENT = 0, QPP_ENDPOINT_SERVER = 1 } q
 
 typedef struct qpp_ctx qpp_ctx;
 typedef struct qpp_key qpp_key;
+typedef struct qpp_header_key qpp_header_key;
 
 /* ------------------------------------------------------------------ context (one per GPU) */
 
@@ -62,6 +68,9 @@ int qpp_ctx_synchronize(qpp_ctx *ctx);
  * at max_packets / 4.  0 = always lane per packet.  Outputs are identical either way. */
 int qpp_ctx_set_burst_max(qpp_ctx *ctx, size_t max_packets);
 int qpp_abi_version(void);
+/* Key-table occupancy (diagnostics / tests): slots allocated, high-water slot index, slots retired but not yet
+ * reusable (their zeroization is still behind in-flight batches). */
+int qpp_ctx_key_slots(qpp_ctx *ctx, uint32_t *capacity, uint32_t *high_water, uint32_t *retired);
 
 /* ------------------------------------------------------------------ keys */
 
@@ -69,6 +78,11 @@ int qpp_abi_version(void);
  * (quic/s2n-quic-crypto/src/cipher_suite.rs:52-63,85-103; header_key.rs:33-49; iv.rs:14-24).
  * secret_len must equal the suite's hash length (32 for SHA-256 suites, 48 for SHA-384). */
 int qpp_key_new(qpp_ctx *ctx, int suite, const uint8_t *secret, size_t secret_len, qpp_key **out);
+/* TLS_*::new(secret) -> Option<(Self, HeaderKey)> (cipher_suite.rs:85-103; negotiated.rs:95-134) as two
+ * independently owned handles: the header key outlives every packet key derived from this one by updates
+ * (KeySet::rotate_phase drops old keys, keyset.rs:94-96, while the space keeps its header key, space/application.rs:70). */
+int qpp_key_new_pair(qpp_ctx *ctx, int suite, const uint8_t *secret, size_t secret_len, qpp_key **key,
+                     qpp_header_key **header_key);
 /* Raw key material (fixtures, Retry/other consumers).  A raw key has no secret: update fails. */
 int qpp_key_new_raw(qpp_ctx *ctx, int suite, const uint8_t *key, size_t key_len, const uint8_t iv[12],
                     const uint8_t *hp, size_t hp_len, qpp_key **out);
@@ -76,7 +90,11 @@ int qpp_key_new_raw(qpp_ctx *ctx, int suite, const uint8_t *key, size_t key_len,
  * key/iv re-derived; the header-protection key is carried over unchanged (RFC 9001 §6)
  * (cipher_suite.rs:68-83, one_rtt.rs:11-14). */
 int qpp_key_update(const qpp_key *key, qpp_key **out);
-/* Zeroizes host and device copies (cipher_suite.rs:106-114,189-193). */
+/* Batched OneRttKey::derive_next_key (one_rtt.rs:11-14, cipher_suite.rs:68-83): out[i] = update(keys[i]), all keys
+ * of one context (any suites), derived on the GPU in one pass per suite; each header key is carried over.  The
+ * KeySet rotation of many connections at once (keyset.rs:75-96). */
+int qpp_key_update_batch(qpp_key *const *keys, size_t n, qpp_key **out);
+/* Zeroizes host and device copies (cipher_suite.rs:106-114,189-193); stream-ordered (see Asynchrony above). */
 void qpp_key_free(qpp_key *key);
 /* Index of this key in its context's device key table: the value to put in qpp_pkt.key_idx. */
 uint32_t qpp_key_slot(const qpp_key *key);
@@ -101,6 +119,26 @@ int qpp_key_new_batch(qpp_ctx *ctx, int suite, const uint8_t *secrets, size_t n,
  * (quic/s2n-quic-crypto/src/initial.rs:29-80).  Returns the endpoint's sealer and opener. */
 int qpp_initial_keys(qpp_ctx *ctx, int endpoint, const uint8_t *dcid, size_t dcid_len,
                      qpp_key **sealer, qpp_key **opener);
+/* The same, plus the InitialHeaderKey pair (initial.rs:54-66: HeaderKeyPair { sealer, opener }) as independently
+ * owned header keys.  header_sealer and header_opener are both NULL or both non-NULL. */
+int qpp_initial_keys_pair(qpp_ctx *ctx, int endpoint, const uint8_t *dcid, size_t dcid_len, qpp_key **sealer,
+                          qpp_key **opener, qpp_header_key **header_sealer, qpp_header_key **header_opener);
+
+/* ------------------------------------------------------------------ header keys (header_key.rs:7-63) */
+
+/* HeaderKey::new(secret, "quic hp", alg) (header_key.rs:33-49).  Its own device slot: usable as key_idx of
+ * qpp_hp_mask_batch descriptors (never of seal/open batches, which refuse it with QPP_INTERNAL_ERROR). */
+int qpp_header_key_new(qpp_ctx *ctx, int suite, const uint8_t *secret, size_t secret_len, qpp_header_key **out);
+/* From the raw header-protection key (16 / 32 bytes). */
+int qpp_header_key_new_raw(qpp_ctx *ctx, int suite, const uint8_t *hp, size_t hp_len, qpp_header_key **out);
+/* Zeroizes host and device copies; stream-ordered like qpp_key_free. */
+void qpp_header_key_free(qpp_header_key *hk);
+uint32_t qpp_header_key_slot(const qpp_header_key *hk);
+int qpp_header_key_suite(const qpp_header_key *hk);
+/* HeaderKey::{sealing,opening}_sample_len (16) */
+size_t qpp_header_key_sample_len(const qpp_header_key *hk);
+/* HeaderKey::{sealing,opening}_header_protection_mask(sample) -> [u8; 5] (header_key.rs:10-30,52-56). */
+int qpp_header_key_mask(const qpp_header_key *hk, const uint8_t *sample, size_t sample_len, uint8_t mask[5]);
 
 /* ------------------------------------------------------------------ per packet (trait mirror) */
 
@@ -120,7 +158,8 @@ int qpp_seal_scatter(qpp_key *key, uint64_t pn, const uint8_t *header, size_t he
  * plaintext region is zeroed so unauthenticated plaintext is never released. */
 int qpp_open(const qpp_key *key, uint64_t pn, const uint8_t *header, size_t header_len,
              uint8_t *payload, size_t payload_len);
-/* HeaderKey::{sealing,opening}_header_protection_mask(sample) -> [u8; 5] (header_key.rs:10-30,52-56). */
+/* The mask of the header key a qpp_key was derived with (the key's own copy; a transport holding a separate
+ * HeaderKey uses qpp_header_key_mask). */
 int qpp_hp_mask(const qpp_key *key, const uint8_t *sample, size_t sample_len, uint8_t mask[5]);
 
 /* ------------------------------------------------------------------ dc consumers
@@ -188,6 +227,27 @@ int qpp_open_batch(qpp_ctx *ctx, const qpp_pkt *descs, size_t n, uint8_t *arena,
  * aad_len = header_len and pn_len = 0).  masks[5*i]. */
 int qpp_hp_mask_batch(qpp_ctx *ctx, const qpp_pkt *descs, size_t n, const uint8_t *arena, uint8_t *masks,
                       void *stream);
+
+/* ------------------------------------------------------------------ host pipeline (packets in host memory)
+
+ * The path starts and ends in host memory (the UDP socket buffer, platform socket/io/tx.rs:204-268, rx.rs).  A host
+ * batch is cut into chunks of consecutive packets; each chunk's span of the arena is copied H2D, sealed and/or
+ * opened on the GPU and copied back D2H, chunks overlapping on three streams over a fixed ring of device buffers
+ * (so a batch may be far larger than the ring).  descs / arena / masks / status are HOST pointers (arena: pinned,
+ * qpp_host_alloc, for full PCIe rate); descriptors must be in ascending, non-overlapping arena order and stay
+ * untouched until the ticket completes.  ops: QPP_OP_SEAL, QPP_OP_OPEN, or both (seal then open on the device:
+ * the round trip; QPP_HP_APPLY is refused there since the opener needs the unprotected header).  Returns when every
+ * chunk is enqueued; *ticket completes when the last chunk is back in host memory. */
+#define QPP_OP_SEAL 0x1u
+#define QPP_OP_OPEN 0x2u
+int qpp_host_batch_submit(qpp_ctx *ctx, const qpp_pkt *descs, size_t n, uint8_t *arena, uint8_t *masks,
+                          int8_t *status, uint32_t flags, uint32_t ops, uint64_t *ticket);
+/* *done = 1 once the ticket's batch is back in host memory (the ticket stays valid until waited on). */
+int qpp_host_batch_query(qpp_ctx *ctx, uint64_t ticket, int *done);
+/* Blocks until the ticket's batch is back in host memory, then releases the ticket. */
+int qpp_host_batch_wait(qpp_ctx *ctx, uint64_t ticket);
+/* Ring geometry: packets and bytes per chunk, chunk buffers (defaults 65536, 96 MiB, 4).  Waits for the device. */
+int qpp_ctx_set_host_pipe(qpp_ctx *ctx, size_t chunk_packets, size_t chunk_bytes, size_t slots);
 
 /* ------------------------------------------------------------------ deferred transmit queue */
 

@@ -12,8 +12,9 @@
  * the RFC 9001 vectors.  Without libcrypto the harness falls back to the (slow) oracle restatement and
  * says so via cpubase_impl().
  */
-#define _POSIX_C_SOURCE 200809L
+#define _GNU_SOURCE
 #include <pthread.h>
+#include <sched.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -31,6 +32,7 @@ typedef struct {
     double seconds;
     uint64_t bytes;  /* payload bytes processed (seal + open) */
     int ok;
+    int cpu;         /* pin the worker to this CPU (-1: no pinning) */
 } job_t;
 
 static double now_s(void) {
@@ -54,6 +56,12 @@ static const EVP_CIPHER *aead(int suite) {
 
 static void *worker(void *arg) {
     job_t *j = (job_t *)arg;
+    if (j->cpu >= 0) {
+        cpu_set_t set;
+        CPU_ZERO(&set);
+        CPU_SET(j->cpu, &set);
+        pthread_setaffinity_np(pthread_self(), sizeof set, &set);
+    }
     const int stride = j->aad_len + j->pt_len + 16;
     uint8_t *arena = malloc((size_t)stride * j->packets);
     uint8_t key[32], iv[12], hp[32];
@@ -125,13 +133,15 @@ const char *cpubase_impl(void) {
 #endif
 }
 
-/* Runs `threads` workers, each looping over its own `packets` x pt_len batch for >= `seconds`.
+/* Runs `threads` workers, each looping over its own `packets` x pt_len batch for >= `seconds`; worker t is pinned to
+ * cpus[t] when cpus is non-NULL (one worker per physical core: bench.py picks them).
  * Returns aggregate seal+open payload throughput in GiB/s (2^30 B/s); *ok = 1 if every open verified. */
-double cpubase_run(int suite, int threads, int packets, int pt_len, int aad_len, int with_hp, double seconds, int *ok) {
+double cpubase_run(int suite, int threads, int packets, int pt_len, int aad_len, int with_hp, double seconds, int *ok,
+                   const int *cpus) {
     pthread_t *tid = calloc((size_t)threads, sizeof *tid);
     job_t *jobs = calloc((size_t)threads, sizeof *jobs);
     for (int t = 0; t < threads; t++) {
-        jobs[t] = (job_t){suite, packets, pt_len, aad_len, with_hp, seconds, 0, 0};
+        jobs[t] = (job_t){suite, packets, pt_len, aad_len, with_hp, seconds, 0, 0, cpus ? cpus[t] : -1};
         pthread_create(&tid[t], NULL, worker, &jobs[t]);
     }
     double total = 0, tmax = 0;
@@ -146,4 +156,40 @@ double cpubase_run(int suite, int threads, int packets, int pt_len, int aad_len,
     free(jobs);
     if (ok) *ok = all_ok;
     return total / tmax / (double)(1ull << 30);
+}
+
+/* The CPU's raw AEAD seal rate on one thread: one `msg_len`-byte message sealed over and over (no per-packet
+ * nonce set-up, no HP, no open) -- the AES-NI/VAES + (V)PCLMULQDQ kernel alone, to separate it from the per-packet
+ * EVP overhead that the packet loop above pays (GiB/s). */
+double cpubase_bulk_seal(int suite, int msg_len, double seconds, int cpu) {
+    if (cpu >= 0) {
+        cpu_set_t set;
+        CPU_ZERO(&set);
+        CPU_SET(cpu, &set);
+        pthread_setaffinity_np(pthread_self(), sizeof set, &set);
+    }
+    uint8_t *buf = malloc((size_t)msg_len + 16), key[32], nonce[12] = {0};
+    fill(buf, (size_t)msg_len, 9);
+    fill(key, 32, 1);
+    uint64_t bytes = 0;
+    double t0 = now_s();
+#ifdef HAVE_OPENSSL
+    EVP_CIPHER_CTX *enc = EVP_CIPHER_CTX_new();
+    EVP_EncryptInit_ex(enc, aead(suite), NULL, key, nonce);
+    int outl;
+    do {
+        for (int r = 0; r < 64; r++) {
+            EVP_EncryptInit_ex(enc, NULL, NULL, NULL, nonce);
+            EVP_EncryptUpdate(enc, buf, &outl, buf, msg_len);
+            EVP_EncryptFinal_ex(enc, buf + msg_len, &outl);
+            bytes += (uint64_t)msg_len;
+        }
+    } while (now_s() - t0 < seconds);
+    EVP_CIPHER_CTX_free(enc);
+#else
+    (void)suite;
+#endif
+    double t = now_s() - t0;
+    free(buf);
+    return (double)bytes / t / (double)(1ull << 30);
 }

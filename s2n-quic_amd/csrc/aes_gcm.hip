@@ -216,21 +216,12 @@ __device__ __forceinline__ void process_packet(const AesLds &aes, const Ghash &g
 
         const uint32_t c = (uint32_t)(NB * g);
         if ((c >> 8) != pg.page) pg.build(aes, rk, p.n0, p.n1, p.n2, c >> 8);
-#ifdef QPP_DIAG_NOAES
-#pragma unroll
-        for (int j = 0; j < NB; j++) ks[j] = make_uint4(c + j, pg.k0, pg.l0, 0);
-#else
         ctr_keystream<NR, NB>(aes, pg, rk, c, ks);
-#endif
 #ifndef QPP_LEAN
         // GHASH of the previous group (independent of the keystream just issued)
 #pragma unroll
         for (int j = 0; j < NB; j++)
-#ifdef QPP_DIAG_NOGHASH
-            if (bprev + j >= 0 && bprev + j < nblk) z = z ^ cprev[j];
-#else
             if (bprev + j >= 0 && bprev + j < nblk) z = gh.mulx(z, cprev[j]);
-#endif
         if (g == 0) ek0 = ks[1];
 #endif
         const int b0 = NB * g - 2;  // data block of slot 0
@@ -286,20 +277,18 @@ __device__ __forceinline__ void process_packet(const AesLds &aes, const Ghash &g
         st16(pay + p.len, tag);
         int8_t st = QPP_OK;
         if (flags & (QPP_HP_MASK_OUT | QPP_HP_APPLY)) {
-            // sample = ciphertext||tag bytes [4 - pn_len, 20 - pn_len)  (payload.rs:151-169), read back: the lane
-            // wrote those bytes itself (same-lane store -> load ordering)
+            // sample = ciphertext||tag bytes [4 - pn_len, 20 - pn_len)  (payload.rs:151-169), read back from memory:
+            // full ciphertext blocks 0 and 1 were stored by OTHER lanes of this wave (cooperative co_store), the tail
+            // and the tag by this lane, so the wave's stores are ordered before this load by a wavefront fence
             const uint32_t s = 4 - p.pn_len;
             if (p.pn_len < 1 || p.pn_len > 4 || p.len < s) {
                 st = QPP_DECODE_ERROR;
             } else {
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
                 const uint4 smp = ld16(pay + s);
                 const uint32_t hdr_len = p.aad_len - p.pn_len;
-#ifndef QPP_DIAG_NOHP
                 hp_finish<NR == 10 ? 10 : 14>(aes, key->hp_rk, smp, p.base, hdr_len, p.pn_len,
                                               masks + 5 * (size_t)pkt_index, flags);
-#else
-                masks[pkt_index] = (uint8_t)(smp.x ^ hdr_len);
-#endif
             }
         }
         if (status) status[pkt_index] = st;
@@ -336,11 +325,7 @@ __global__ __launch_bounds__(WG) void aes_gcm_kernel(const DevKey *__restrict__ 
     for (int i = 0; i < 4 * (NR + 1); i++) rk[i] = __builtin_amdgcn_readfirstlane(key->rk[i]);
     Stage<NB> st;
     st.lane = threadIdx.x & 63u;
-#ifdef QPP_DIAG_ALIAS_STAGE  // diagnostic: waves share staging slots (wrong data) so any WG size fits in LDS
-    st.base = kLdsStage + ((threadIdx.x >> 6) % (8 / (NB / 2))) * (64u * 16u * NB);
-#else
     st.base = kLdsStage + (threadIdx.x >> 6) * (64u * 16u * NB);
-#endif
     for (uint32_t t0 = 0; t0 < w.count; t0 += WG) {  // WG < 1024: several passes over the work item
         const uint32_t t = t0 + threadIdx.x;
         const bool real = t < w.count;
@@ -375,11 +360,21 @@ __device__ void aes_bytewise(const uint32_t *rk, int nr, uint8_t s[16]) {
     }
 }
 
-__global__ void key_setup_kernel(DevKey *keys, uint32_t first, uint32_t count) {
+// Key install: record i (when records != nullptr) is copied into slot slots[i], then H = E_K(0) and V[m] = H * x^m are
+// derived for it.  A slot list (not a range) so that retired slots can be reused and a live slot next to a new one is
+// never rewritten while in-flight batches read it.  Header-key-only records (live == 2) and ChaCha keys need no GHASH
+// powers.
+__global__ void key_install_kernel(DevKey *keys, const uint32_t *__restrict__ slots,
+                                   const DevKey *__restrict__ records, uint32_t count) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= count) return;
-    DevKey *k = keys + first + i;
-    if (!k->live || k->suite == QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256) return;
+    DevKey *k = keys + slots[i];
+    if (records) {
+        const uint4 *src = (const uint4 *)(records + i);
+        uint4 *dst = (uint4 *)k;
+        for (uint32_t w = 0; w < sizeof(DevKey) / 16; w++) dst[w] = src[w];
+    }
+    if (k->live != 1 || k->suite == QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256) return;
     uint8_t v[16] = {0};
     aes_bytewise(k->rk, (int)k->nr, v);
     for (int m = 0; m < 128; m++) {
@@ -398,9 +393,10 @@ __global__ void key_setup_kernel(DevKey *keys, uint32_t first, uint32_t count) {
 
 }  // namespace
 
-hipError_t launch_key_setup(DevKey *keys, uint32_t first, uint32_t count, hipStream_t s) {
+hipError_t launch_key_install(DevKey *keys, const uint32_t *slots, const DevKey *records, uint32_t count,
+                              hipStream_t s) {
     if (!count) return hipSuccess;
-    hipLaunchKernelGGL(key_setup_kernel, dim3((count + 63) / 64), dim3(64), 0, s, keys, first, count);
+    hipLaunchKernelGGL(key_install_kernel, dim3((count + 63) / 64), dim3(64), 0, s, keys, slots, records, count);
     return hipGetLastError();
 }
 
@@ -411,19 +407,10 @@ namespace {
 struct Variant {
     int nb, wg, per;
 };
-#ifdef QPP_DIAG_ALIAS_STAGE
-constexpr Variant kVariants[] = {{4, 512, 1024}, {2, 1024, 1024}, {2, 512, 1024}, {4, 256, 1024}, {4, 768, 768}};
-#else
 constexpr Variant kVariants[] = {{4, 512, 1024}, {2, 1024, 1024}, {2, 512, 1024}, {4, 256, 1024}};
-#endif
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 constexpr uint32_t lds_bytes(int nb, int wg) {
-    const uint32_t b = kLdsStage + (uint32_t)(wg / 64) * 1024u * (uint32_t)nb;
-#ifdef QPP_DIAG_ALIAS_STAGE
-    return b > kLdsMax ? kLdsMax : b;
-#else
-    return b;
-#endif
+    return kLdsStage + (uint32_t)(wg / 64) * 1024u * (uint32_t)nb;
 }
 
 template <bool SEAL, int NR>
@@ -437,9 +424,6 @@ void launch_variant(int v, dim3 grid, hipStream_t s, const DevKey *keys, const q
         case 1: { QPP_AES_LAUNCH(2, 1024); break; }
         case 2: { QPP_AES_LAUNCH(2, 512); break; }
         case 3: { QPP_AES_LAUNCH(4, 256); break; }
-#ifdef QPP_DIAG_ALIAS_STAGE
-        case 4: { QPP_AES_LAUNCH(4, 768); break; }
-#endif
         default: { QPP_AES_LAUNCH(4, 512); break; }
     }
 #undef QPP_AES_LAUNCH

@@ -1,10 +1,21 @@
 // api.cpp — host runtime behind include/qpp.h: contexts (one per GPU), the device key table, per-packet
-// trait mirrors (a batch of one on the GPU) and the batch entry points.  No CPU fallback exists: every
-// byte of payload is sealed/opened by the HIP kernels; without a gfx950 device the calls fail with
-// QPP_DEVICE_ERROR.
+// trait mirrors (a batch of one on the GPU), the batch entry points and the host-memory pipeline.  No CPU
+// fallback exists: every byte of payload is sealed/opened by the HIP kernels; without a gfx950 device the
+// calls fail with QPP_DEVICE_ERROR.
+//
+// Asynchrony rules (DESIGN.md §2 "Key lifetime"):
+//   * every stream a batch is enqueued on gets a StreamState: its own plan scratch (two streams of one context never
+//     share counts/perm/work) and an event recorded after its latest batch;
+//   * key records reach HBM on the context's key stream (one install launch per flush, over a slot list, never a range
+//     that could rewrite a live neighbour) and a `keys_ready` event; a batch on any stream first waits (device side)
+//     for the latest install it has not yet waited for.  The host never blocks on data batches to install a key;
+//   * a freed key's slot is retired in stream order on the retire stream: it waits for every StreamState's last
+//     event, zeroes the device record and records a "retired" event; the slot is reused only once that completed.
 #include <string.h>
 
 #include <algorithm>
+#include <deque>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -12,26 +23,72 @@
 
 using namespace qpp;
 
+namespace {
+
+struct StreamState {
+    hipStream_t stream = nullptr;
+    PlanBuffers plan{};
+    uint32_t plan_n_cap = 0, plan_key_cap = 0;
+    hipEvent_t last = nullptr;  // after this stream's latest batch
+    bool used = false;          // `last` has been recorded at least once
+    uint64_t key_gen = 0;       // the latest key install this stream has waited for
+};
+
+struct Retired {
+    uint32_t slot;
+    hipEvent_t done;  // the zeroing of the device record (context stream) has completed
+};
+
+// One slot of the host pipeline: device buffers for one chunk in flight, and the events that order its reuse.
+struct PipeSlot {
+    uint8_t *arena = nullptr;  // chunk span of the arena
+    qpp_pkt *descs = nullptr;
+    uint8_t *masks = nullptr;
+    int8_t *status = nullptr;
+    hipEvent_t h2d = nullptr, comp = nullptr, d2h = nullptr;
+    bool busy = false;  // d2h has been recorded (the next user waits for it)
+};
+
+struct HostPipe {
+    size_t chunk_packets = 65536, chunk_bytes = 96u << 20, nslots = 4;
+    hipStream_t h2d = nullptr, comp = nullptr, d2h = nullptr;
+    std::vector<PipeSlot> slots;
+    size_t next = 0;
+    uint64_t next_ticket = 1;
+    std::map<uint64_t, hipEvent_t> tickets;
+};
+
+}  // namespace
+
 struct qpp_ctx {
     int device = 0;
     uint32_t n_cu = 0;  // compute units (AES work-item sizing)
     uint32_t burst_max = kBurstMaxDefault;  // AES batches up to this size take the wave-per-packet kernel
     hipStream_t stream = nullptr;
+    hipStream_t kstream = nullptr;  // key installs / derivations
+    hipStream_t rstream = nullptr;  // key retirements (zeroization behind in-flight batches)
+    hipEvent_t keys_ready = nullptr;
+    uint64_t key_gen = 0;           // installs so far (keys_ready marks the latest)
     // device key table + host mirror
     DevKey *d_keys = nullptr;
     uint32_t key_cap = 0;
     std::vector<DevKey> h_keys;
-    std::vector<uint32_t> free_slots;
-    uint32_t live_by_suite[4] = {0, 0, 0, 0};  // live keys per suite: which kernels a batch can need
+    std::vector<uint8_t> dirty_flag;
+    std::vector<uint32_t> dirty;          // slots whose host record must be installed before the next launch
+    std::vector<uint32_t> free_slots;     // reusable now
+    std::deque<Retired> retired;          // reusable once `done` has completed
+    uint32_t live_by_suite[4] = {0, 0, 0, 0};  // live packet keys per suite: which kernels a batch can need
     uint32_t next_slot = 0;
-    uint32_t dirty_lo = UINT32_MAX, dirty_hi = 0;
-    // plan scratch
-    PlanBuffers plan{};
-    uint32_t plan_n_cap = 0, plan_key_cap = 0;
-    // per-packet staging
+    // per-stream state (plan scratch, last-batch event); [0] is the context stream
+    std::vector<StreamState *> streams;
+    std::vector<hipEvent_t> event_pool;
+    // per-packet staging (pinned, zero-copy) and key staging (pinned + device)
     uint8_t *d_stage = nullptr, *h_stage = nullptr;
     uint8_t *v_stage = nullptr;  // device view of the pinned h_stage (zero-copy per-packet calls)
     size_t stage_cap = 0;
+    uint8_t *h_kstage = nullptr, *d_kstage = nullptr;
+    size_t kstage_cap = 0, kstage_pending = 0;
+    HostPipe *pipe = nullptr;
     std::string last_error;
 };
 
@@ -46,6 +103,15 @@ struct qpp_key {
     uint8_t hp[32] = {0};
 };
 
+// HeaderKey (header_key.rs:7-63): owned independently of any packet key; its own device slot (live = 2) holds only
+// the header-protection key schedule.
+struct qpp_header_key {
+    qpp_ctx *ctx = nullptr;
+    int suite = 0;
+    uint32_t slot = 0;
+    uint8_t hp[32] = {0};
+};
+
 namespace {
 
 bool fail(qpp_ctx *ctx, hipError_t e, const char *what) {
@@ -57,10 +123,73 @@ bool fail(qpp_ctx *ctx, hipError_t e, const char *what) {
     do {                                                        \
         if (fail((ctx), (expr), #expr)) return QPP_DEVICE_ERROR; \
     } while (0)
+#define RC_TRY(expr)          \
+    do {                      \
+        int rc_ = (expr);     \
+        if (rc_) return rc_;  \
+    } while (0)
 
 bool valid_suite(int s) {
     return s == QPP_SUITE_TLS_AES_128_GCM_SHA256 || s == QPP_SUITE_TLS_AES_256_GCM_SHA384 ||
            s == QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256;
+}
+bool is_aes(int suite) { return suite != QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256; }
+constexpr uint32_t kAesSuites = (1u << QPP_SUITE_TLS_AES_128_GCM_SHA256) | (1u << QPP_SUITE_TLS_AES_256_GCM_SHA384);
+
+hipEvent_t get_event(qpp_ctx *ctx) {
+    if (!ctx->event_pool.empty()) {
+        hipEvent_t e = ctx->event_pool.back();
+        ctx->event_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+    return e;
+}
+void put_event(qpp_ctx *ctx, hipEvent_t e) {
+    if (e) ctx->event_pool.push_back(e);
+}
+
+void free_plan(PlanBuffers &p) {
+    hipFree(p.counts); hipFree(p.cursor); hipFree(p.istart); hipFree(p.perm); hipFree(p.work); hipFree(p.n_work);
+    p = PlanBuffers{};
+}
+
+StreamState *stream_state(qpp_ctx *ctx, hipStream_t s) {
+    for (StreamState *st : ctx->streams)
+        if (st->stream == s) return st;
+    StreamState *st = new StreamState();
+    st->stream = s;
+    if (hipEventCreateWithFlags(&st->last, hipEventDisableTiming) != hipSuccess) {
+        delete st;
+        return nullptr;
+    }
+    ctx->streams.push_back(st);
+    return st;
+}
+
+// Before enqueueing a batch on st: its launches must see every key installed so far (device-side wait).
+int see_keys(qpp_ctx *ctx, StreamState *st) {
+    if (st->key_gen == ctx->key_gen) return QPP_OK;
+    HIP_TRY(ctx, hipStreamWaitEvent(st->stream, ctx->keys_ready, 0));
+    st->key_gen = ctx->key_gen;
+    return QPP_OK;
+}
+
+// After enqueueing a batch on st: remember where it ends (key retirement orders behind it).
+int note_work(qpp_ctx *ctx, StreamState *st) {
+    HIP_TRY(ctx, hipEventRecord(st->last, st->stream));
+    st->used = true;
+    return QPP_OK;
+}
+
+// The stream state of a batch call on `stream` (NULL: the context stream), ready for launches.
+int batch_stream(qpp_ctx *ctx, void *stream, StreamState **out) {
+    StreamState *st = stream_state(ctx, stream ? (hipStream_t)stream : ctx->stream);
+    if (!st) return QPP_DEVICE_ERROR;
+    RC_TRY(see_keys(ctx, st));
+    *out = st;
+    return QPP_OK;
 }
 
 int grow_keys(qpp_ctx *ctx, uint32_t need) {
@@ -68,37 +197,78 @@ int grow_keys(qpp_ctx *ctx, uint32_t need) {
     uint32_t cap = std::max<uint32_t>(64, ctx->key_cap);
     while (cap < need) cap *= 2;
     DevKey *nk = nullptr;
-    HIP_TRY(ctx, hipDeviceSynchronize());
+    HIP_TRY(ctx, hipDeviceSynchronize());  // no batch may still read the old table
     HIP_TRY(ctx, hipMalloc(&nk, sizeof(DevKey) * cap));
     HIP_TRY(ctx, hipMemset(nk, 0, sizeof(DevKey) * cap));
     if (ctx->d_keys) {
         HIP_TRY(ctx, hipMemcpy(nk, ctx->d_keys, sizeof(DevKey) * ctx->key_cap, hipMemcpyDeviceToDevice));
+        HIP_TRY(ctx, hipMemset(ctx->d_keys, 0, sizeof(DevKey) * ctx->key_cap));
         HIP_TRY(ctx, hipFree(ctx->d_keys));
     }
     ctx->d_keys = nk;
     ctx->h_keys.resize(cap);
+    ctx->dirty_flag.resize(cap, 0);
     ctx->key_cap = cap;
     return QPP_OK;
 }
 
-// Pushes pending key records to HBM and derives H / H*x^m on the GPU (key setup kernel).
-int flush_keys(qpp_ctx *ctx, hipStream_t s) {
-    if (ctx->dirty_lo >= ctx->dirty_hi) return QPP_OK;
-    const uint32_t lo = ctx->dirty_lo, cnt = ctx->dirty_hi - ctx->dirty_lo;
-    HIP_TRY(ctx, hipStreamSynchronize(s));
-    HIP_TRY(ctx, hipMemcpy(ctx->d_keys + lo, ctx->h_keys.data() + lo, sizeof(DevKey) * cnt, hipMemcpyHostToDevice));
-    HIP_TRY(ctx, launch_key_setup(ctx->d_keys, lo, cnt, s));
-    ctx->dirty_lo = UINT32_MAX;
-    ctx->dirty_hi = 0;
+int ensure_kstage(qpp_ctx *ctx, size_t bytes) {
+    if (bytes <= ctx->kstage_cap) return QPP_OK;
+    size_t cap = std::max<size_t>(1 << 16, ctx->kstage_cap);
+    while (cap < bytes) cap *= 2;
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->kstream));
+    if (ctx->d_kstage) hipFree(ctx->d_kstage);
+    if (ctx->h_kstage) { secure_zero(ctx->h_kstage, ctx->kstage_cap); hipHostFree(ctx->h_kstage); }
+    ctx->d_kstage = nullptr;
+    ctx->h_kstage = nullptr;
+    ctx->kstage_cap = 0;
+    HIP_TRY(ctx, hipMalloc(&ctx->d_kstage, cap));
+    HIP_TRY(ctx, hipHostMalloc(&ctx->h_kstage, cap, hipHostMallocDefault));
+    ctx->kstage_cap = cap;
     return QPP_OK;
 }
 
-int ensure_plan(qpp_ctx *ctx, uint32_t n) {
-    if (n <= ctx->plan_n_cap && ctx->key_cap <= ctx->plan_key_cap) return QPP_OK;
-    HIP_TRY(ctx, hipDeviceSynchronize());
-    PlanBuffers &p = ctx->plan;
-    hipFree(p.counts); hipFree(p.cursor); hipFree(p.istart); hipFree(p.perm); hipFree(p.work); hipFree(p.n_work);
-    const uint32_t ncap = std::max(n, ctx->plan_n_cap), kcap = ctx->key_cap;
+// Installs every pending host record on the device: one copy + one install launch on the key stream, then the
+// keys_ready event that the next batch on every stream waits for (device side; H and V[m] included).
+int flush_keys(qpp_ctx *ctx) {
+    if (ctx->dirty.empty()) return QPP_OK;
+    const uint32_t n = (uint32_t)ctx->dirty.size();
+    const size_t rec = sizeof(DevKey) * n, slots = 4 * (size_t)n;
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->kstream));  // the pinned key stage of the previous flush is free again
+    if (ctx->kstage_pending) secure_zero(ctx->h_kstage, ctx->kstage_pending);
+    ctx->kstage_pending = 0;
+    RC_TRY(ensure_kstage(ctx, rec + slots));
+    for (uint32_t i = 0; i < n; i++) {
+        memcpy(ctx->h_kstage + sizeof(DevKey) * i, &ctx->h_keys[ctx->dirty[i]], sizeof(DevKey));
+        ctx->dirty_flag[ctx->dirty[i]] = 0;
+    }
+    memcpy(ctx->h_kstage + rec, ctx->dirty.data(), slots);
+    hipStream_t s = ctx->kstream;
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->d_kstage, ctx->h_kstage, rec + slots, hipMemcpyHostToDevice, s));
+    HIP_TRY(ctx, launch_key_install(ctx->d_keys, (const uint32_t *)(ctx->d_kstage + rec),
+                                    (const DevKey *)ctx->d_kstage, n, s));
+    HIP_TRY(ctx, hipMemsetAsync(ctx->d_kstage, 0, rec, s));
+    HIP_TRY(ctx, hipEventRecord(ctx->keys_ready, s));
+    ctx->key_gen++;
+    ctx->dirty.clear();
+    ctx->kstage_pending = rec;  // the pinned copy of the records is zeroized once the copy is done (next key call)
+    return QPP_OK;
+}
+
+void mark_dirty(qpp_ctx *ctx, uint32_t slot) {
+    if (!ctx->dirty_flag[slot]) {
+        ctx->dirty_flag[slot] = 1;
+        ctx->dirty.push_back(slot);
+    }
+}
+
+int ensure_plan(qpp_ctx *ctx, StreamState *st, uint32_t n) {
+    if (n <= st->plan_n_cap && ctx->key_cap <= st->plan_key_cap) return QPP_OK;
+    HIP_TRY(ctx, hipStreamSynchronize(st->stream));  // the old scratch is no longer read
+    PlanBuffers &p = st->plan;
+    free_plan(p);
+    st->plan_n_cap = st->plan_key_cap = 0;
+    const uint32_t ncap = std::max(n, st->plan_n_cap), kcap = ctx->key_cap;
     HIP_TRY(ctx, hipMalloc(&p.counts, sizeof(uint32_t) * kcap));
     HIP_TRY(ctx, hipMemset(p.counts, 0, sizeof(uint32_t) * kcap));  // plan_scan re-zeroes it after every plan
     HIP_TRY(ctx, hipMalloc(&p.cursor, sizeof(uint32_t) * kcap));
@@ -106,8 +276,8 @@ int ensure_plan(qpp_ctx *ctx, uint32_t n) {
     HIP_TRY(ctx, hipMalloc(&p.perm, sizeof(uint32_t) * std::max<uint32_t>(ncap, 1)));
     HIP_TRY(ctx, hipMalloc(&p.work, sizeof(WorkItem) * (plan_max_work(ncap, kcap, kMinPacketsPerItem) + 1)));
     HIP_TRY(ctx, hipMalloc(&p.n_work, sizeof(uint32_t)));
-    ctx->plan_n_cap = ncap;
-    ctx->plan_key_cap = kcap;
+    st->plan_n_cap = ncap;
+    st->plan_key_cap = kcap;
     return QPP_OK;
 }
 
@@ -118,6 +288,8 @@ int ensure_stage(qpp_ctx *ctx, size_t bytes) {
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     if (ctx->d_stage) hipFree(ctx->d_stage);
     if (ctx->h_stage) hipHostFree(ctx->h_stage);
+    ctx->d_stage = ctx->h_stage = ctx->v_stage = nullptr;
+    ctx->stage_cap = 0;
     HIP_TRY(ctx, hipMalloc(&ctx->d_stage, cap));
     HIP_TRY(ctx, hipHostMalloc(&ctx->h_stage, cap, hipHostMallocDefault));
     void *v = nullptr;
@@ -127,21 +299,50 @@ int ensure_stage(qpp_ctx *ctx, size_t bytes) {
     return QPP_OK;
 }
 
-uint32_t alloc_slot(qpp_ctx *ctx) {
-    if (!ctx->free_slots.empty()) {
-        uint32_t s = ctx->free_slots.back();
-        ctx->free_slots.pop_back();
-        return s;
+// A slot for a new key: a retired slot whose zeroing has completed, else a fresh one.
+int alloc_slot(qpp_ctx *ctx, uint32_t *out) {
+    while (!ctx->retired.empty()) {
+        const hipError_t q = hipEventQuery(ctx->retired.front().done);
+        if (q == hipErrorNotReady) break;
+        if (fail(ctx, q, "retired slot event")) return QPP_DEVICE_ERROR;
+        ctx->free_slots.push_back(ctx->retired.front().slot);
+        put_event(ctx, ctx->retired.front().done);
+        ctx->retired.pop_front();
     }
-    return ctx->next_slot++;
+    if (!ctx->free_slots.empty()) {
+        *out = ctx->free_slots.back();
+        ctx->free_slots.pop_back();
+        return QPP_OK;
+    }
+    RC_TRY(grow_keys(ctx, ctx->next_slot + 1));
+    *out = ctx->next_slot++;
+    return QPP_OK;
 }
 
-// Fills the slot's host record from the key's material and marks it dirty.
+// Zeroizes a slot's device record behind every batch already enqueued on any stream of this context, then queues
+// the slot for reuse (cipher_suite.rs:106-114,189-193 zeroize on drop; here "drop" is stream-ordered).
+void retire_slot(qpp_ctx *ctx, uint32_t slot) {
+    secure_zero(&ctx->h_keys[slot], sizeof(DevKey));
+    hipSetDevice(ctx->device);
+    for (StreamState *st : ctx->streams)
+        if (st->used) hipStreamWaitEvent(ctx->rstream, st->last, 0);
+    hipStreamWaitEvent(ctx->rstream, ctx->keys_ready, 0);  // behind the slot's own install, if still pending
+    hipMemsetAsync(ctx->d_keys + slot, 0, sizeof(DevKey), ctx->rstream);
+    hipEvent_t e = get_event(ctx);
+    if (!e || hipEventRecord(e, ctx->rstream) != hipSuccess) {
+        // no event: wait here instead (the slot must never be reused while a batch may read it)
+        hipStreamSynchronize(ctx->rstream);
+        put_event(ctx, e);
+        ctx->free_slots.push_back(slot);
+        return;
+    }
+    ctx->retired.push_back(Retired{slot, e});
+}
+
+// Fills the slot's host record from the key's material and marks it for installation.
 int install(qpp_key *k) {
     qpp_ctx *ctx = k->ctx;
-    k->slot = alloc_slot(ctx);
-    int rc = grow_keys(ctx, k->slot + 1);
-    if (rc) return rc;
+    RC_TRY(alloc_slot(ctx, &k->slot));
     DevKey &d = ctx->h_keys[k->slot];
     memset(&d, 0, sizeof d);
     d.suite = (uint32_t)k->suite;
@@ -155,9 +356,21 @@ int install(qpp_key *k) {
         d.nr = (uint32_t)aes_expand_key(k->key, kl, d.rk);
         d.hp_nr = (uint32_t)aes_expand_key(k->hp, kl, d.hp_rk);
     }
-    ctx->dirty_lo = std::min(ctx->dirty_lo, k->slot);
-    ctx->dirty_hi = std::max(ctx->dirty_hi, k->slot + 1);
+    mark_dirty(ctx, k->slot);
     ctx->live_by_suite[k->suite]++;
+    return QPP_OK;
+}
+
+int install_header(qpp_header_key *h) {
+    qpp_ctx *ctx = h->ctx;
+    RC_TRY(alloc_slot(ctx, &h->slot));
+    DevKey &d = ctx->h_keys[h->slot];
+    memset(&d, 0, sizeof d);
+    d.suite = (uint32_t)h->suite;
+    d.live = 2;  // header key only: no packet key, never planned or sealed with
+    if (h->suite == QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256) memcpy(d.hp_rk, h->hp, 32);
+    else d.hp_nr = (uint32_t)aes_expand_key(h->hp, suite_key_len(h->suite), d.hp_rk);
+    mark_dirty(ctx, h->slot);
     return QPP_OK;
 }
 
@@ -168,13 +381,48 @@ void derive(qpp_key *k) {
     hkdf_expand_label(hl, k->secret, "quic hp", k->hp, kl);
 }
 
-bool is_aes(int suite) { return suite != QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256; }
-
 uint32_t suite_mask(const qpp_ctx *ctx) {
     uint32_t m = 0;
     for (int s = 1; s <= 3; s++)
         if (ctx->live_by_suite[s]) m |= 1u << s;
     return m;
+}
+
+// Batch bodies: plan (AES) + kernels on st's stream; keys already flushed.
+int enqueue_seal(qpp_ctx *ctx, StreamState *st, const qpp_pkt *descs, uint32_t n, uint8_t *arena, uint8_t *masks,
+                 int8_t *status, uint32_t flags) {
+    hipStream_t s = st->stream;
+    if (!(flags & QPP_ONLY_CHACHA) && (suite_mask(ctx) & kAesSuites)) {
+        RC_TRY(ensure_plan(ctx, st, n));
+        const bool burst = n <= ctx->burst_max;
+        const uint32_t per = burst ? burst_packets_per_item(n, ctx->n_cu) : aes_packets_per_item(n, ctx->n_cu);
+        HIP_TRY(ctx, launch_plan(ctx->d_keys, ctx->key_cap, descs, n, st->plan, per, s));
+        HIP_TRY(ctx, (burst ? launch_aes_gcm_burst : launch_aes_gcm)(true, ctx->d_keys, descs, st->plan, n,
+                                                                    ctx->key_cap, per, arena, masks, status, flags,
+                                                                    suite_mask(ctx), s));
+    }
+    if (!(flags & QPP_ONLY_AES))
+        HIP_TRY(ctx, launch_chacha(true, ctx->d_keys, ctx->key_cap, descs, n, arena, masks, status, flags,
+                                   n <= (ctx->burst_max >> kChachaBurstShift), s));
+    return QPP_OK;
+}
+
+int enqueue_open(qpp_ctx *ctx, StreamState *st, const qpp_pkt *descs, uint32_t n, uint8_t *arena, int8_t *status,
+                 uint32_t flags) {
+    hipStream_t s = st->stream;
+    if (!(flags & QPP_ONLY_CHACHA) && (suite_mask(ctx) & kAesSuites)) {
+        RC_TRY(ensure_plan(ctx, st, n));
+        const bool burst = n <= ctx->burst_max;
+        const uint32_t per = burst ? burst_packets_per_item(n, ctx->n_cu) : aes_packets_per_item(n, ctx->n_cu);
+        HIP_TRY(ctx, launch_plan(ctx->d_keys, ctx->key_cap, descs, n, st->plan, per, s));
+        HIP_TRY(ctx, (burst ? launch_aes_gcm_burst : launch_aes_gcm)(false, ctx->d_keys, descs, st->plan, n,
+                                                                    ctx->key_cap, per, arena, nullptr, status, 0,
+                                                                    suite_mask(ctx), s));
+    }
+    if (!(flags & QPP_ONLY_AES))
+        HIP_TRY(ctx, launch_chacha(false, ctx->d_keys, ctx->key_cap, descs, n, arena, nullptr, status, 0,
+                                   n <= (ctx->burst_max >> kChachaBurstShift), s));
+    return QPP_OK;
 }
 
 // One packet through the batch kernels, zero-copy: the kernel reads and writes the pinned stage directly (no DMA
@@ -187,10 +435,10 @@ int run_one(const qpp_key *k, bool seal, uint64_t pn, const uint8_t *header, siz
     if (header_len > 0xffff || payload_len > 0xffff) return QPP_INTERNAL_ERROR;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     const size_t total = kOnePkt + 16 + header_len + payload_len + 16;
-    int rc = ensure_stage(ctx, total);
-    if (rc) return rc;
-    rc = flush_keys(ctx, ctx->stream);
-    if (rc) return rc;
+    RC_TRY(ensure_stage(ctx, total));
+    RC_TRY(flush_keys(ctx));
+    StreamState *st = nullptr;
+    RC_TRY(batch_stream(ctx, nullptr, &st));
     uint8_t *h = ctx->h_stage, *v = ctx->v_stage;
     memset(h, 0, total);
     uint8_t *pkt = h + kOnePkt;
@@ -217,14 +465,128 @@ int run_one(const qpp_key *k, bool seal, uint64_t pn, const uint8_t *header, siz
                                                                              v + kOnePkt, v + 80, vst, 0,
                                                                              1u << k->suite, s));
     } else {
-        HIP_TRY(ctx, launch_chacha(seal, ctx->d_keys, vd, 1, v + kOnePkt, v + 80, vst, 0, ctx->burst_max > 0, s));
+        HIP_TRY(ctx, launch_chacha(seal, ctx->d_keys, ctx->key_cap, vd, 1, v + kOnePkt, v + 80, vst, 0,
+                                   ctx->burst_max > 0, s));
     }
+    RC_TRY(note_work(ctx, st));
     HIP_TRY(ctx, hipStreamSynchronize(s));
     memcpy(out, pkt + 16 + header_len, payload_len);
     if (seal) memcpy(tag_out, pkt + 16 + header_len + payload_len, 16);
     *status_out = (int8_t)h[64];
     secure_zero(h, total);
     return QPP_OK;
+}
+
+// HeaderKey::*_header_protection_mask for one sample through the hp_mask kernel, zero-copy on the pinned stage:
+// descriptor @0, sample @64 (+4), mask @96.
+int mask_one(qpp_ctx *ctx, uint32_t slot, const uint8_t *sample, uint8_t mask[5]) {
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    RC_TRY(ensure_stage(ctx, 128));
+    RC_TRY(flush_keys(ctx));
+    StreamState *st = nullptr;
+    RC_TRY(batch_stream(ctx, nullptr, &st));
+    uint8_t *h = ctx->h_stage;
+    memset(h, 0, 128);
+    memcpy(h + 64 + 4, sample, 16);
+    qpp_pkt &d = *(qpp_pkt *)h;
+    d.key_idx = slot;  // off = aad_len = pn_len = 0: sample at offset 4
+    hipStream_t s = ctx->stream;
+    HIP_TRY(ctx, launch_hp_mask(ctx->d_keys, ctx->key_cap, (const qpp_pkt *)ctx->v_stage, 1, ctx->v_stage + 64,
+                                ctx->v_stage + 96, s));
+    RC_TRY(note_work(ctx, st));
+    HIP_TRY(ctx, hipStreamSynchronize(s));
+    memcpy(mask, h + 96, 5);
+    return QPP_OK;
+}
+
+// n secrets (n * hash_len, host) [+ header keys hp_in, n * key_len, host] -> n device-derived keys in fresh or
+// recycled slots.  updates x "quic ku" on each; material copied back for the host handles.
+int derive_batch(qpp_ctx *ctx, int suite, const uint8_t *secrets, const uint8_t *hp_in, size_t n, uint32_t updates,
+                 qpp_key **out) {
+    const size_t hl = suite_hash_len(suite), kl = suite_key_len(suite), mb = key_material_bytes();
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    RC_TRY(flush_keys(ctx));  // pending host records first
+    std::vector<uint32_t> slots(n);
+    for (size_t i = 0; i < n; i++) RC_TRY(alloc_slot(ctx, &slots[i]));
+    // key stage: secrets | hp_in | slots | material
+    const size_t o_hp = n * hl, o_slot = o_hp + (hp_in ? n * kl : 0), o_mat = (o_slot + 4 * n + 15) & ~size_t(15);
+    const size_t total = o_mat + n * mb;
+    RC_TRY(ensure_kstage(ctx, total));
+    uint8_t *h = ctx->h_kstage, *d = ctx->d_kstage;
+    memcpy(h, secrets, n * hl);
+    if (hp_in) memcpy(h + o_hp, hp_in, n * kl);
+    memcpy(h + o_slot, slots.data(), 4 * n);
+    hipStream_t s = ctx->kstream;
+    HIP_TRY(ctx, hipMemcpyAsync(d, h, o_slot + 4 * n, hipMemcpyHostToDevice, s));
+    HIP_TRY(ctx, launch_key_derive(ctx->d_keys, (const uint32_t *)(d + o_slot), (uint32_t)n, suite, d,
+                                   hp_in ? d + o_hp : nullptr, updates, d + o_mat, s));
+    HIP_TRY(ctx, hipMemcpyAsync(h + o_mat, d + o_mat, n * mb, hipMemcpyDeviceToHost, s));
+    HIP_TRY(ctx, hipMemsetAsync(d, 0, total, s));
+    HIP_TRY(ctx, hipEventRecord(ctx->keys_ready, s));
+    ctx->key_gen++;
+    HIP_TRY(ctx, hipStreamSynchronize(s));  // the material comes back to the host handles
+    const uint32_t nr = suite == QPP_SUITE_TLS_AES_128_GCM_SHA256 ? 10 : suite == QPP_SUITE_TLS_AES_256_GCM_SHA384 ? 14 : 0;
+    for (size_t i = 0; i < n; i++) {
+        const uint8_t *m = h + o_mat + i * mb;
+        qpp_key *k = new qpp_key();
+        k->ctx = ctx;
+        k->suite = suite;
+        k->slot = slots[i];
+        k->has_secret = true;
+        memcpy(k->secret, m, hl);
+        memcpy(k->key, m + 48, kl);
+        memcpy(k->iv, m + 80, 12);
+        memcpy(k->hp, m + 96, kl);
+        // host mirror: what the host needs (suite, rounds, liveness); the record itself was written on the device
+        DevKey &r = ctx->h_keys[slots[i]];
+        memset(&r, 0, sizeof r);
+        r.suite = (uint32_t)suite;
+        r.nr = r.hp_nr = nr;
+        r.live = 1;
+        out[i] = k;
+    }
+    ctx->live_by_suite[suite] += (uint32_t)n;
+    secure_zero(h, total);
+    return QPP_OK;
+}
+
+// ---------------------------------------------------------------- host pipeline
+
+int pipe_init(qpp_ctx *ctx) {
+    HostPipe *p = ctx->pipe;
+    if (!p->h2d) {
+        HIP_TRY(ctx, hipStreamCreateWithFlags(&p->h2d, hipStreamNonBlocking));
+        HIP_TRY(ctx, hipStreamCreateWithFlags(&p->comp, hipStreamNonBlocking));
+        HIP_TRY(ctx, hipStreamCreateWithFlags(&p->d2h, hipStreamNonBlocking));
+    }
+    if (p->slots.size() == p->nslots && !p->slots.empty() && p->slots[0].arena) return QPP_OK;
+    p->slots.resize(p->nslots);
+    for (PipeSlot &sl : p->slots) {
+        HIP_TRY(ctx, hipMalloc(&sl.arena, p->chunk_bytes));
+        HIP_TRY(ctx, hipMalloc(&sl.descs, sizeof(qpp_pkt) * p->chunk_packets));
+        HIP_TRY(ctx, hipMalloc(&sl.masks, 5 * p->chunk_packets));
+        HIP_TRY(ctx, hipMalloc(&sl.status, p->chunk_packets));
+        HIP_TRY(ctx, hipEventCreateWithFlags(&sl.h2d, hipEventDisableTiming));
+        HIP_TRY(ctx, hipEventCreateWithFlags(&sl.comp, hipEventDisableTiming));
+        HIP_TRY(ctx, hipEventCreateWithFlags(&sl.d2h, hipEventDisableTiming));
+        sl.busy = false;
+    }
+    p->next = 0;
+    return QPP_OK;
+}
+
+void pipe_release(qpp_ctx *ctx) {
+    HostPipe *p = ctx->pipe;
+    if (!p) return;
+    for (PipeSlot &sl : p->slots) {
+        if (sl.arena) { hipMemset(sl.arena, 0, p->chunk_bytes); hipFree(sl.arena); }
+        hipFree(sl.descs); hipFree(sl.masks); hipFree(sl.status);
+        if (sl.h2d) hipEventDestroy(sl.h2d);
+        if (sl.comp) hipEventDestroy(sl.comp);
+        if (sl.d2h) hipEventDestroy(sl.d2h);
+        sl = PipeSlot{};
+    }
+    p->slots.clear();
 }
 
 }  // namespace
@@ -248,7 +610,14 @@ int qpp_ctx_create(int device, qpp_ctx **out) {
     int rc = QPP_OK;
     do {
         if (fail(ctx, hipSetDevice(device), "hipSetDevice")) { rc = QPP_DEVICE_ERROR; break; }
-        if (fail(ctx, hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking), "stream")) { rc = QPP_DEVICE_ERROR; break; }
+        if (fail(ctx, hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking), "stream") ||
+            fail(ctx, hipStreamCreateWithFlags(&ctx->kstream, hipStreamNonBlocking), "key stream") ||
+            fail(ctx, hipStreamCreateWithFlags(&ctx->rstream, hipStreamNonBlocking), "retire stream") ||
+            fail(ctx, hipEventCreateWithFlags(&ctx->keys_ready, hipEventDisableTiming), "key event")) {
+            rc = QPP_DEVICE_ERROR;
+            break;
+        }
+        if (!stream_state(ctx, ctx->stream)) { rc = QPP_DEVICE_ERROR; break; }
         rc = grow_keys(ctx, 64);
     } while (0);
     if (rc) {
@@ -271,11 +640,29 @@ void qpp_ctx_destroy(qpp_ctx *ctx) {
     hipDeviceSynchronize();
     if (ctx->d_keys) { hipMemset(ctx->d_keys, 0, sizeof(DevKey) * ctx->key_cap); hipFree(ctx->d_keys); }
     secure_zero(ctx->h_keys.data(), sizeof(DevKey) * ctx->h_keys.size());
-    PlanBuffers &p = ctx->plan;
-    hipFree(p.counts); hipFree(p.cursor); hipFree(p.istart); hipFree(p.perm); hipFree(p.work); hipFree(p.n_work);
+    for (StreamState *st : ctx->streams) {
+        free_plan(st->plan);
+        if (st->last) hipEventDestroy(st->last);
+        delete st;
+    }
+    for (Retired &r : ctx->retired) hipEventDestroy(r.done);
+    for (hipEvent_t e : ctx->event_pool) hipEventDestroy(e);
+    if (ctx->pipe) {
+        pipe_release(ctx);
+        for (auto &t : ctx->pipe->tickets) hipEventDestroy(t.second);
+        if (ctx->pipe->h2d) hipStreamDestroy(ctx->pipe->h2d);
+        if (ctx->pipe->comp) hipStreamDestroy(ctx->pipe->comp);
+        if (ctx->pipe->d2h) hipStreamDestroy(ctx->pipe->d2h);
+        delete ctx->pipe;
+    }
     hipFree(ctx->d_stage);
     if (ctx->h_stage) hipHostFree(ctx->h_stage);
+    hipFree(ctx->d_kstage);
+    if (ctx->h_kstage) { secure_zero(ctx->h_kstage, ctx->kstage_cap); hipHostFree(ctx->h_kstage); }
     if (ctx->stream) hipStreamDestroy(ctx->stream);
+    if (ctx->kstream) hipStreamDestroy(ctx->kstream);
+    if (ctx->rstream) hipStreamDestroy(ctx->rstream);
+    if (ctx->keys_ready) hipEventDestroy(ctx->keys_ready);
     delete ctx;
 }
 
@@ -288,6 +675,14 @@ int qpp_ctx_synchronize(qpp_ctx *ctx) {
 }
 
 const char *qpp_ctx_last_error(qpp_ctx *ctx) { return ctx ? ctx->last_error.c_str() : "no context"; }
+
+int qpp_ctx_key_slots(qpp_ctx *ctx, uint32_t *capacity, uint32_t *high_water, uint32_t *retired) {
+    if (!ctx) return QPP_INTERNAL_ERROR;
+    if (capacity) *capacity = ctx->key_cap;
+    if (high_water) *high_water = ctx->next_slot;
+    if (retired) *retired = (uint32_t)ctx->retired.size();
+    return QPP_OK;
+}
 
 // ---------------------------------------------------------------- keys
 
@@ -303,9 +698,19 @@ int qpp_key_new(qpp_ctx *ctx, int suite, const uint8_t *secret, size_t secret_le
     memcpy(k->secret, secret, secret_len);
     derive(k);
     int rc = install(k);
-    if (rc) { qpp_key_free(k); return rc; }
+    if (rc) { secure_zero(k, sizeof *k); delete k; return rc; }
     *out = k;
     return QPP_OK;
+}
+
+int qpp_key_new_pair(qpp_ctx *ctx, int suite, const uint8_t *secret, size_t secret_len, qpp_key **key,
+                     qpp_header_key **header_key) {
+    if (!key || !header_key) return QPP_INTERNAL_ERROR;
+    *header_key = nullptr;
+    RC_TRY(qpp_key_new(ctx, suite, secret, secret_len, key));
+    int rc = qpp_header_key_new(ctx, suite, secret, secret_len, header_key);
+    if (rc) { qpp_key_free(*key); *key = nullptr; }
+    return rc;
 }
 
 int qpp_key_new_batch(qpp_ctx *ctx, int suite, const uint8_t *secrets, size_t n, uint32_t updates, qpp_key **out) {
@@ -313,41 +718,44 @@ int qpp_key_new_batch(qpp_ctx *ctx, int suite, const uint8_t *secrets, size_t n,
     if (!valid_suite(suite)) return QPP_UNSUPPORTED;
     if (n > (1u << 24)) return QPP_INTERNAL_ERROR;
     if (!n) return QPP_OK;
-    const size_t hl = suite_hash_len(suite), kl = suite_key_len(suite), mb = key_material_bytes();
-    HIP_TRY(ctx, hipSetDevice(ctx->device));
-    hipStream_t s = ctx->stream;
-    int rc = flush_keys(ctx, s);  // pending host records first: a later flush never covers these device-made ones
-    if (rc) return rc;
-    const uint32_t first = ctx->next_slot;  // a contiguous range of fresh slots
-    rc = grow_keys(ctx, first + (uint32_t)n);
-    if (rc) return rc;
-    rc = ensure_stage(ctx, n * (hl + mb));
-    if (rc) return rc;
-    uint8_t *h = ctx->h_stage, *d = ctx->d_stage;
-    memcpy(h, secrets, n * hl);
-    HIP_TRY(ctx, hipMemcpyAsync(d, h, n * hl, hipMemcpyHostToDevice, s));
-    HIP_TRY(ctx, launch_key_derive(ctx->d_keys, first, (uint32_t)n, suite, d, updates, d + n * hl, s));
-    HIP_TRY(ctx, hipMemcpyAsync(h + n * hl, d + n * hl, n * mb, hipMemcpyDeviceToHost, s));
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->h_keys.data() + first, ctx->d_keys + first, sizeof(DevKey) * n,
-                                hipMemcpyDeviceToHost, s));  // host mirror of the records the device wrote
-    HIP_TRY(ctx, hipStreamSynchronize(s));
-    HIP_TRY(ctx, hipMemsetAsync(d, 0, n * (hl + mb), s));
-    ctx->next_slot = first + (uint32_t)n;
-    ctx->live_by_suite[suite] += (uint32_t)n;
-    for (size_t i = 0; i < n; i++) {
-        const uint8_t *m = h + n * hl + i * mb;
-        qpp_key *k = new qpp_key();
-        k->ctx = ctx;
-        k->suite = suite;
-        k->slot = first + (uint32_t)i;
-        k->has_secret = true;
-        memcpy(k->secret, m, hl);
-        memcpy(k->key, m + 48, kl);
-        memcpy(k->iv, m + 80, 12);
-        memcpy(k->hp, m + 96, kl);
-        out[i] = k;
+    return derive_batch(ctx, suite, secrets, nullptr, n, updates, out);
+}
+
+int qpp_key_update_batch(qpp_key *const *keys, size_t n, qpp_key **out) {
+    if (!out || (n && !keys)) return QPP_INTERNAL_ERROR;
+    if (!n) return QPP_OK;
+    if (n > (1u << 24)) return QPP_INTERNAL_ERROR;
+    qpp_ctx *ctx = keys[0] ? keys[0]->ctx : nullptr;
+    if (!ctx) return QPP_INTERNAL_ERROR;
+    for (size_t i = 0; i < n; i++)
+        if (!keys[i] || keys[i]->ctx != ctx || !keys[i]->has_secret) return QPP_INTERNAL_ERROR;
+    // one device pass per suite present, each key's secret through one "quic ku" step, its header key kept
+    std::vector<uint8_t> sec, hp;
+    std::vector<size_t> idx;
+    std::vector<qpp_key *> made;
+    for (int suite = 1; suite <= 3; suite++) {
+        idx.clear();
+        for (size_t i = 0; i < n; i++)
+            if (keys[i]->suite == suite) idx.push_back(i);
+        if (idx.empty()) continue;
+        const size_t hl = suite_hash_len(suite), kl = suite_key_len(suite);
+        sec.resize(idx.size() * hl);
+        hp.resize(idx.size() * kl);
+        for (size_t j = 0; j < idx.size(); j++) {
+            memcpy(sec.data() + j * hl, keys[idx[j]]->secret, hl);
+            memcpy(hp.data() + j * kl, keys[idx[j]]->hp, kl);
+        }
+        made.resize(idx.size());
+        int rc = derive_batch(ctx, suite, sec.data(), hp.data(), idx.size(), 1, made.data());
+        secure_zero(sec.data(), sec.size());
+        secure_zero(hp.data(), hp.size());
+        if (rc) {
+            for (size_t i = 0; i < n; i++)
+                if (out[i]) { qpp_key_free(out[i]); out[i] = nullptr; }
+            return rc;
+        }
+        for (size_t j = 0; j < idx.size(); j++) out[idx[j]] = made[j];
     }
-    secure_zero(h, n * (hl + mb));
     return QPP_OK;
 }
 
@@ -364,7 +772,7 @@ int qpp_key_new_raw(qpp_ctx *ctx, int suite, const uint8_t *key, size_t key_len,
     memcpy(k->iv, iv, 12);
     memcpy(k->hp, hp, hp_len);
     int rc = install(k);
-    if (rc) { qpp_key_free(k); return rc; }
+    if (rc) { secure_zero(k, sizeof *k); delete k; return rc; }
     *out = k;
     return QPP_OK;
 }
@@ -382,7 +790,7 @@ int qpp_key_update(const qpp_key *key, qpp_key **out) {
     derive(k);
     memcpy(k->hp, key->hp, sizeof k->hp);  // RFC 9001 §6: the header protection key is not updated
     int rc = install(k);
-    if (rc) { qpp_key_free(k); return rc; }
+    if (rc) { secure_zero(k, sizeof *k); delete k; return rc; }
     *out = k;
     return QPP_OK;
 }
@@ -390,12 +798,9 @@ int qpp_key_update(const qpp_key *key, qpp_key **out) {
 void qpp_key_free(qpp_key *key) {
     if (!key) return;
     qpp_ctx *ctx = key->ctx;
-    if (ctx && key->slot < ctx->key_cap && ctx->h_keys[key->slot].live) {
-        hipSetDevice(ctx->device);
+    if (ctx && key->slot < ctx->key_cap && ctx->h_keys[key->slot].live == 1) {
         ctx->live_by_suite[key->suite]--;
-        secure_zero(&ctx->h_keys[key->slot], sizeof(DevKey));
-        hipMemset(ctx->d_keys + key->slot, 0, sizeof(DevKey));  // synchronous: zeroize the device copy
-        ctx->free_slots.push_back(key->slot);
+        retire_slot(ctx, key->slot);
     }
     secure_zero(key, sizeof *key);
     delete key;
@@ -423,21 +828,86 @@ int qpp_key_material(const qpp_key *key, uint8_t *key_out, uint8_t iv_out[12], u
     return QPP_OK;
 }
 
+// ---------------------------------------------------------------- header keys (header_key.rs)
+
+int qpp_header_key_new_raw(qpp_ctx *ctx, int suite, const uint8_t *hp, size_t hp_len, qpp_header_key **out) {
+    if (!ctx || !out || !hp) return QPP_INTERNAL_ERROR;
+    *out = nullptr;
+    if (!valid_suite(suite)) return QPP_UNSUPPORTED;
+    if (hp_len != suite_key_len(suite)) return QPP_INTERNAL_ERROR;
+    qpp_header_key *h = new qpp_header_key();
+    h->ctx = ctx;
+    h->suite = suite;
+    memcpy(h->hp, hp, hp_len);
+    int rc = install_header(h);
+    if (rc) { secure_zero(h, sizeof *h); delete h; return rc; }
+    *out = h;
+    return QPP_OK;
+}
+
+int qpp_header_key_new(qpp_ctx *ctx, int suite, const uint8_t *secret, size_t secret_len, qpp_header_key **out) {
+    // HeaderKey::new(secret, "quic hp", alg) (header_key.rs:33-49), as TLS_*::new makes it (cipher_suite.rs:85-103)
+    if (!ctx || !out || !secret) return QPP_INTERNAL_ERROR;
+    *out = nullptr;
+    if (!valid_suite(suite)) return QPP_UNSUPPORTED;
+    if (secret_len != suite_hash_len(suite)) return QPP_INTERNAL_ERROR;
+    uint8_t hp[32];
+    const size_t kl = suite_key_len(suite);
+    hkdf_expand_label(secret_len, secret, "quic hp", hp, kl);
+    int rc = qpp_header_key_new_raw(ctx, suite, hp, kl, out);
+    secure_zero(hp, sizeof hp);
+    return rc;
+}
+
+void qpp_header_key_free(qpp_header_key *hk) {
+    if (!hk) return;
+    qpp_ctx *ctx = hk->ctx;
+    if (ctx && hk->slot < ctx->key_cap && ctx->h_keys[hk->slot].live == 2) retire_slot(ctx, hk->slot);
+    secure_zero(hk, sizeof *hk);
+    delete hk;
+}
+
+uint32_t qpp_header_key_slot(const qpp_header_key *hk) { return hk ? hk->slot : UINT32_MAX; }
+int qpp_header_key_suite(const qpp_header_key *hk) { return hk ? hk->suite : 0; }
+size_t qpp_header_key_sample_len(const qpp_header_key *) { return 16; }
+
+int qpp_header_key_mask(const qpp_header_key *hk, const uint8_t *sample, size_t sample_len, uint8_t mask[5]) {
+    if (!hk || !sample || !mask || sample_len < 16) return QPP_INTERNAL_ERROR;
+    return mask_one(hk->ctx, hk->slot, sample, mask);
+}
+
 int qpp_initial_keys(qpp_ctx *ctx, int endpoint, const uint8_t *dcid, size_t dcid_len, qpp_key **sealer,
                      qpp_key **opener) {
-    // quic/s2n-quic-crypto/src/initial.rs:29-68; salt quic/s2n-quic-core/src/crypto/initial.rs:29
+    return qpp_initial_keys_pair(ctx, endpoint, dcid, dcid_len, sealer, opener, nullptr, nullptr);
+}
+
+int qpp_initial_keys_pair(qpp_ctx *ctx, int endpoint, const uint8_t *dcid, size_t dcid_len, qpp_key **sealer,
+                          qpp_key **opener, qpp_header_key **header_sealer, qpp_header_key **header_opener) {
+    // quic/s2n-quic-crypto/src/initial.rs:29-68 -> (InitialKey, InitialHeaderKey); salt quic/s2n-quic-core/src/crypto/initial.rs:29
     static const uint8_t salt[20] = {0x38, 0x76, 0x2c, 0xf7, 0xf5, 0x59, 0x34, 0xb3, 0x4d, 0x17,
                                      0x9a, 0xe6, 0xa4, 0xc8, 0x0c, 0xad, 0xcc, 0xbb, 0x7f, 0x0a};
     if (!ctx || !sealer || !opener || (!dcid && dcid_len)) return QPP_INTERNAL_ERROR;
+    if (!header_sealer != !header_opener) return QPP_INTERNAL_ERROR;
+    *sealer = *opener = nullptr;
+    if (header_sealer) *header_sealer = *header_opener = nullptr;
     uint8_t prk[32], client[32], server[32];
     hkdf_extract(32, salt, sizeof salt, dcid, dcid_len, prk);
     hkdf_expand_label(32, prk, "client in", client, 32);
     hkdf_expand_label(32, prk, "server in", server, 32);
     const bool is_client = endpoint == QPP_ENDPOINT_CLIENT;
-    int rc = qpp_key_new(ctx, QPP_SUITE_TLS_AES_128_GCM_SHA256, is_client ? client : server, 32, sealer);
-    if (!rc) {
-        rc = qpp_key_new(ctx, QPP_SUITE_TLS_AES_128_GCM_SHA256, is_client ? server : client, 32, opener);
-        if (rc) { qpp_key_free(*sealer); *sealer = nullptr; }
+    const uint8_t *ss = is_client ? client : server, *os = is_client ? server : client;
+    const int suite = QPP_SUITE_TLS_AES_128_GCM_SHA256;
+    int rc = qpp_key_new(ctx, suite, ss, 32, sealer);
+    if (!rc) rc = qpp_key_new(ctx, suite, os, 32, opener);
+    if (!rc && header_sealer) rc = qpp_header_key_new(ctx, suite, ss, 32, header_sealer);
+    if (!rc && header_opener) rc = qpp_header_key_new(ctx, suite, os, 32, header_opener);
+    if (rc) {
+        qpp_key_free(*sealer); qpp_key_free(*opener);
+        *sealer = *opener = nullptr;
+        if (header_sealer) {
+            qpp_header_key_free(*header_sealer); qpp_header_key_free(*header_opener);
+            *header_sealer = *header_opener = nullptr;
+        }
     }
     secure_zero(prk, sizeof prk); secure_zero(client, sizeof client); secure_zero(server, sizeof server);
     return rc;
@@ -483,23 +953,7 @@ int qpp_open(const qpp_key *key, uint64_t pn, const uint8_t *header, size_t head
 
 int qpp_hp_mask(const qpp_key *key, const uint8_t *sample, size_t sample_len, uint8_t mask[5]) {
     if (!key || !sample || !mask || sample_len < 16) return QPP_INTERNAL_ERROR;
-    qpp_ctx *ctx = key->ctx;
-    HIP_TRY(ctx, hipSetDevice(ctx->device));
-    int rc = ensure_stage(ctx, 128);
-    if (rc) return rc;
-    rc = flush_keys(ctx, ctx->stream);
-    if (rc) return rc;
-    // zero-copy: descriptor @0, sample @64 (+4), mask @96 of the pinned stage, read and written by the kernel
-    uint8_t *h = ctx->h_stage;
-    memset(h, 0, 128);
-    memcpy(h + 64 + 4, sample, 16);
-    qpp_pkt &d = *(qpp_pkt *)h;
-    d.key_idx = key->slot;  // off = aad_len = pn_len = 0: sample at offset 4
-    hipStream_t s = ctx->stream;
-    HIP_TRY(ctx, launch_hp_mask(ctx->d_keys, (const qpp_pkt *)ctx->v_stage, 1, ctx->v_stage + 64, ctx->v_stage + 96, s));
-    HIP_TRY(ctx, hipStreamSynchronize(s));
-    memcpy(mask, h + 96, 5);
-    return QPP_OK;
+    return mask_one(key->ctx, key->slot, sample, mask);
 }
 
 // ---------------------------------------------------------------- dc consumers (dc/s2n-quic-dc/src/crypto/awslc.rs)
@@ -569,25 +1023,12 @@ int qpp_seal_batch(qpp_ctx *ctx, const qpp_pkt *descs, size_t n, uint8_t *arena,
     if ((flags & QPP_HP_MASK_OUT) && !masks) return QPP_INTERNAL_ERROR;
     if (n > UINT32_MAX) return QPP_INTERNAL_ERROR;
     if (!n) return QPP_OK;
-    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    int rc = flush_keys(ctx, s);
-    if (rc) return rc;
-    if (!(flags & QPP_ONLY_CHACHA)) {
-        rc = ensure_plan(ctx, (uint32_t)n);
-        if (rc) return rc;
-        const bool burst = n <= ctx->burst_max;
-        const uint32_t per = burst ? burst_packets_per_item((uint32_t)n, ctx->n_cu)
-                                   : aes_packets_per_item((uint32_t)n, ctx->n_cu);
-        HIP_TRY(ctx, launch_plan(ctx->d_keys, ctx->key_cap, descs, (uint32_t)n, ctx->plan, per, s));
-        HIP_TRY(ctx, (burst ? launch_aes_gcm_burst : launch_aes_gcm)(true, ctx->d_keys, descs, ctx->plan, (uint32_t)n,
-                                                                    ctx->key_cap, per, arena, masks, status, flags,
-                                                                    suite_mask(ctx), s));
-    }
-    if (!(flags & QPP_ONLY_AES))
-        HIP_TRY(ctx, launch_chacha(true, ctx->d_keys, descs, (uint32_t)n, arena, masks, status, flags,
-                                   n <= (ctx->burst_max >> kChachaBurstShift), s));
-    return QPP_OK;
+    RC_TRY(flush_keys(ctx));
+    StreamState *st = nullptr;
+    RC_TRY(batch_stream(ctx, stream, &st));
+    RC_TRY(enqueue_seal(ctx, st, descs, (uint32_t)n, arena, masks, status, flags));
+    return note_work(ctx, st);
 }
 
 int qpp_open_batch(qpp_ctx *ctx, const qpp_pkt *descs, size_t n, uint8_t *arena, int8_t *status, uint32_t flags,
@@ -595,25 +1036,12 @@ int qpp_open_batch(qpp_ctx *ctx, const qpp_pkt *descs, size_t n, uint8_t *arena,
     if (!ctx || (n && (!descs || !arena || !status))) return QPP_INTERNAL_ERROR;
     if (n > UINT32_MAX) return QPP_INTERNAL_ERROR;
     if (!n) return QPP_OK;
-    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    int rc = flush_keys(ctx, s);
-    if (rc) return rc;
-    if (!(flags & QPP_ONLY_CHACHA)) {
-        rc = ensure_plan(ctx, (uint32_t)n);
-        if (rc) return rc;
-        const bool burst = n <= ctx->burst_max;
-        const uint32_t per = burst ? burst_packets_per_item((uint32_t)n, ctx->n_cu)
-                                   : aes_packets_per_item((uint32_t)n, ctx->n_cu);
-        HIP_TRY(ctx, launch_plan(ctx->d_keys, ctx->key_cap, descs, (uint32_t)n, ctx->plan, per, s));
-        HIP_TRY(ctx, (burst ? launch_aes_gcm_burst : launch_aes_gcm)(false, ctx->d_keys, descs, ctx->plan, (uint32_t)n,
-                                                                    ctx->key_cap, per, arena, nullptr, status, 0,
-                                                                    suite_mask(ctx), s));
-    }
-    if (!(flags & QPP_ONLY_AES))
-        HIP_TRY(ctx, launch_chacha(false, ctx->d_keys, descs, (uint32_t)n, arena, nullptr, status, 0,
-                                   n <= (ctx->burst_max >> kChachaBurstShift), s));
-    return QPP_OK;
+    RC_TRY(flush_keys(ctx));
+    StreamState *st = nullptr;
+    RC_TRY(batch_stream(ctx, stream, &st));
+    RC_TRY(enqueue_open(ctx, st, descs, (uint32_t)n, arena, status, flags));
+    return note_work(ctx, st);
 }
 
 int qpp_unprotect_open_batch(qpp_ctx *ctx, const qpp_rx_pkt *rx, size_t n, uint8_t *arena, qpp_pkt *descs_out,
@@ -621,14 +1049,15 @@ int qpp_unprotect_open_batch(qpp_ctx *ctx, const qpp_rx_pkt *rx, size_t n, uint8
     if (!ctx || (n && (!rx || !arena || !descs_out || !status))) return QPP_INTERNAL_ERROR;
     if (n > UINT32_MAX) return QPP_INTERNAL_ERROR;
     if (!n) return QPP_OK;
-    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    int rc = flush_keys(ctx, s);
-    if (rc) return rc;
+    RC_TRY(flush_keys(ctx));
+    StreamState *st = nullptr;
+    RC_TRY(batch_stream(ctx, stream, &st));
     // 1. header unprotection + PN expansion + key-phase choice -> descs_out (device); 2. the open kernels on them,
     // grouped by the chosen key like any batch (skipped packets keep their DECODE_ERROR status)
-    HIP_TRY(ctx, launch_unprotect(ctx->d_keys, rx, (uint32_t)n, arena, descs_out, status, s));
-    return qpp_open_batch(ctx, descs_out, n, arena, status, flags, s);
+    HIP_TRY(ctx, launch_unprotect(ctx->d_keys, ctx->key_cap, rx, (uint32_t)n, arena, descs_out, status, st->stream));
+    RC_TRY(enqueue_open(ctx, st, descs_out, (uint32_t)n, arena, status, flags));
+    return note_work(ctx, st);
 }
 
 int qpp_pn_truncate(uint64_t pn, uint64_t largest_acked, uint64_t *truncated, size_t *pn_len) {
@@ -656,11 +1085,117 @@ int qpp_hp_mask_batch(qpp_ctx *ctx, const qpp_pkt *descs, size_t n, const uint8_
                       void *stream) {
     if (!ctx || (n && (!descs || !arena || !masks))) return QPP_INTERNAL_ERROR;
     if (!n) return QPP_OK;
-    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    int rc = flush_keys(ctx, s);
-    if (rc) return rc;
-    HIP_TRY(ctx, launch_hp_mask(ctx->d_keys, descs, (uint32_t)n, arena, masks, s));
+    RC_TRY(flush_keys(ctx));
+    StreamState *st = nullptr;
+    RC_TRY(batch_stream(ctx, stream, &st));
+    HIP_TRY(ctx, launch_hp_mask(ctx->d_keys, ctx->key_cap, descs, (uint32_t)n, arena, masks, st->stream));
+    return note_work(ctx, st);
+}
+
+// ---------------------------------------------------------------- host pipeline (packets start and end in host memory)
+
+int qpp_ctx_set_host_pipe(qpp_ctx *ctx, size_t chunk_packets, size_t chunk_bytes, size_t slots) {
+    if (!ctx || !chunk_packets || chunk_packets > UINT32_MAX || chunk_bytes < 4096 || slots < 2 || slots > 16)
+        return QPP_INTERNAL_ERROR;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    HIP_TRY(ctx, hipDeviceSynchronize());
+    if (!ctx->pipe) ctx->pipe = new HostPipe();
+    pipe_release(ctx);
+    ctx->pipe->chunk_packets = chunk_packets;
+    ctx->pipe->chunk_bytes = chunk_bytes;
+    ctx->pipe->nslots = slots;
+    return QPP_OK;
+}
+
+int qpp_host_batch_submit(qpp_ctx *ctx, const qpp_pkt *descs, size_t n, uint8_t *arena, uint8_t *masks,
+                          int8_t *status, uint32_t flags, uint32_t ops, uint64_t *ticket) {
+    if (!ctx || !ticket || (n && (!descs || !arena))) return QPP_INTERNAL_ERROR;
+    if (!(ops & (QPP_OP_SEAL | QPP_OP_OPEN)) || (ops & ~(QPP_OP_SEAL | QPP_OP_OPEN))) return QPP_INTERNAL_ERROR;
+    if ((flags & QPP_HP_MASK_OUT) && !(masks && (ops & QPP_OP_SEAL))) return QPP_INTERNAL_ERROR;
+    if ((ops & QPP_OP_OPEN) && n && !status) return QPP_INTERNAL_ERROR;
+    if ((ops & QPP_OP_SEAL) && (ops & QPP_OP_OPEN) && (flags & QPP_HP_APPLY)) return QPP_INTERNAL_ERROR;
+    *ticket = 0;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    if (!ctx->pipe) ctx->pipe = new HostPipe();
+    HostPipe *p = ctx->pipe;
+    RC_TRY(pipe_init(ctx));
+    RC_TRY(flush_keys(ctx));
+    StreamState *st = nullptr;
+    RC_TRY(batch_stream(ctx, p->comp, &st));
+    // chunks of consecutive packets: at most chunk_packets, span [lo, hi) of at most chunk_bytes; packets must be in
+    // ascending, non-overlapping arena order so that spans of different chunks never overlap
+    size_t i = 0;
+    uint64_t prev_end = 0;
+    while (i < n) {
+        const size_t first = i;
+        const uint64_t lo = descs[i].off;
+        uint64_t hi = lo;
+        while (i < n && i - first < p->chunk_packets) {
+            const qpp_pkt &d = descs[i];
+            const uint64_t end = (uint64_t)d.off + d.aad_len + d.pt_len + 16;
+            if (d.off < prev_end) return QPP_INTERNAL_ERROR;  // out of order or overlapping
+            if (end - lo > p->chunk_bytes) {
+                if (i == first) return QPP_INTERNAL_ERROR;  // one packet larger than a chunk buffer
+                break;
+            }
+            hi = std::max(hi, end);
+            prev_end = end;
+            i++;
+        }
+        const uint32_t cn = (uint32_t)(i - first);
+        PipeSlot &sl = p->slots[p->next];
+        p->next = (p->next + 1) % p->slots.size();
+        // the slot's previous chunk must be back in host memory before its buffers are overwritten (device-side wait)
+        if (sl.busy) HIP_TRY(ctx, hipStreamWaitEvent(p->h2d, sl.d2h, 0));
+        HIP_TRY(ctx, hipMemcpyAsync(sl.arena, arena + lo, hi - lo, hipMemcpyHostToDevice, p->h2d));
+        HIP_TRY(ctx, hipMemcpyAsync(sl.descs, descs + first, sizeof(qpp_pkt) * cn, hipMemcpyHostToDevice, p->h2d));
+        HIP_TRY(ctx, hipEventRecord(sl.h2d, p->h2d));
+        HIP_TRY(ctx, hipStreamWaitEvent(p->comp, sl.h2d, 0));
+        uint8_t *base = sl.arena - lo;  // descriptor offsets stay absolute: the kernels address base + off
+        if (ops & QPP_OP_SEAL)
+            RC_TRY(enqueue_seal(ctx, st, sl.descs, cn, base, sl.masks, (ops & QPP_OP_OPEN) ? nullptr : sl.status,
+                                flags));
+        if (ops & QPP_OP_OPEN)
+            RC_TRY(enqueue_open(ctx, st, sl.descs, cn, base, sl.status, flags & ~(QPP_HP_MASK_OUT | QPP_HP_APPLY)));
+        HIP_TRY(ctx, hipEventRecord(sl.comp, p->comp));
+        HIP_TRY(ctx, hipStreamWaitEvent(p->d2h, sl.comp, 0));
+        HIP_TRY(ctx, hipMemcpyAsync(arena + lo, sl.arena, hi - lo, hipMemcpyDeviceToHost, p->d2h));
+        if ((flags & QPP_HP_MASK_OUT) && masks)
+            HIP_TRY(ctx, hipMemcpyAsync(masks + 5 * first, sl.masks, 5 * (size_t)cn, hipMemcpyDeviceToHost, p->d2h));
+        if (status) HIP_TRY(ctx, hipMemcpyAsync(status + first, sl.status, cn, hipMemcpyDeviceToHost, p->d2h));
+        HIP_TRY(ctx, hipEventRecord(sl.d2h, p->d2h));
+        sl.busy = true;
+    }
+    RC_TRY(note_work(ctx, st));
+    hipEvent_t done = get_event(ctx);
+    if (!done) return QPP_DEVICE_ERROR;
+    HIP_TRY(ctx, hipEventRecord(done, p->d2h));
+    *ticket = p->next_ticket++;
+    p->tickets[*ticket] = done;
+    return QPP_OK;
+}
+
+int qpp_host_batch_query(qpp_ctx *ctx, uint64_t ticket, int *done) {
+    if (!ctx || !done || !ctx->pipe) return QPP_INTERNAL_ERROR;
+    auto it = ctx->pipe->tickets.find(ticket);
+    if (it == ctx->pipe->tickets.end()) return QPP_INTERNAL_ERROR;
+    const hipError_t q = hipEventQuery(it->second);
+    if (q == hipErrorNotReady) { *done = 0; return QPP_OK; }
+    HIP_TRY(ctx, q);
+    *done = 1;
+    return QPP_OK;
+}
+
+int qpp_host_batch_wait(qpp_ctx *ctx, uint64_t ticket) {
+    if (!ctx || !ctx->pipe) return QPP_INTERNAL_ERROR;
+    auto it = ctx->pipe->tickets.find(ticket);
+    if (it == ctx->pipe->tickets.end()) return QPP_INTERNAL_ERROR;
+    hipEvent_t e = it->second;
+    ctx->pipe->tickets.erase(it);
+    const hipError_t r = hipEventSynchronize(e);
+    put_event(ctx, e);
+    HIP_TRY(ctx, r);
     return QPP_OK;
 }
 
@@ -709,8 +1244,22 @@ int qpp_stream_create(qpp_ctx *ctx, void **out) {
     *out = (void *)s;
     return QPP_OK;
 }
-void qpp_stream_destroy(qpp_ctx *, void *stream) {
-    if (stream) hipStreamDestroy((hipStream_t)stream);
+void qpp_stream_destroy(qpp_ctx *ctx, void *stream) {
+    if (!stream) return;
+    hipStream_t s = (hipStream_t)stream;
+    if (ctx && s != ctx->stream) {
+        hipStreamSynchronize(s);  // its batches are done: its plan scratch and last-batch event can go
+        for (size_t i = 0; i < ctx->streams.size(); i++) {
+            StreamState *st = ctx->streams[i];
+            if (st->stream != s) continue;
+            free_plan(st->plan);
+            if (st->last) hipEventDestroy(st->last);
+            delete st;
+            ctx->streams.erase(ctx->streams.begin() + (long)i);
+            break;
+        }
+    }
+    hipStreamDestroy(s);
 }
 int qpp_stream_synchronize(qpp_ctx *ctx, void *stream) {
     HIP_TRY(ctx, hipStreamSynchronize(stream ? (hipStream_t)stream : ctx->stream));
@@ -843,9 +1392,8 @@ int qpp_txq_push(qpp_txq *q, const qpp_key *key, uint64_t pn, size_t off, size_t
 // burst kernel (AES) and the ChaCha kernel on the pinned ring itself; one launch per suite family, one sync.
 static int txq_flush_zero_copy(qpp_txq *q, hipStream_t s) {
     qpp_ctx *ctx = q->ctx;
-    const uint32_t aes = (1u << QPP_SUITE_TLS_AES_128_GCM_SHA256) | (1u << QPP_SUITE_TLS_AES_256_GCM_SHA384);
     const uint32_t n = (uint32_t)q->count;
-    if (q->suites & aes) {
+    if (q->suites & kAesSuites) {
         std::vector<uint32_t> &ord = q->order;
         ord.clear();
         for (uint32_t i = 0; i < n; i++)
@@ -866,10 +1414,11 @@ static int txq_flush_zero_copy(qpp_txq *q, hipStream_t s) {
         std::copy(ord.begin(), ord.end(), q->h_perm);
         *q->h_nwork = items;
         HIP_TRY(ctx, launch_aes_gcm_burst(true, ctx->d_keys, q->v_desc, q->v_plan, (uint32_t)ord.size(), keys, per,
-                                          q->v_ring, nullptr, nullptr, QPP_HP_APPLY, q->suites & aes, s));
+                                          q->v_ring, nullptr, nullptr, QPP_HP_APPLY, q->suites & kAesSuites, s));
     }
-    if (q->suites & ~aes)
-        HIP_TRY(ctx, launch_chacha(true, ctx->d_keys, q->v_desc, n, q->v_ring, nullptr, nullptr, QPP_HP_APPLY, true, s));
+    if (q->suites & ~kAesSuites)
+        HIP_TRY(ctx, launch_chacha(true, ctx->d_keys, ctx->key_cap, q->v_desc, n, q->v_ring, nullptr, nullptr,
+                                   QPP_HP_APPLY, true, s));
     HIP_TRY(ctx, hipStreamSynchronize(s));
     return QPP_OK;
 }
@@ -880,18 +1429,19 @@ int qpp_txq_flush(qpp_txq *q) {
     qpp_ctx *ctx = q->ctx;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream;
-    int rc = flush_keys(ctx, s);
-    if (rc) return rc;
+    RC_TRY(flush_keys(ctx));
+    int rc;
     if (q->count <= q->zc_max) {
+        StreamState *st = nullptr;
+        RC_TRY(batch_stream(ctx, nullptr, &st));  // sees the latest key install; synchronous, so no note_work
         rc = txq_flush_zero_copy(q, s);
     } else {
         const size_t span = q->hi - q->lo;
         HIP_TRY(ctx, hipMemcpyAsync(q->d_ring + q->lo, q->h_ring + q->lo, span, hipMemcpyHostToDevice, s));
         HIP_TRY(ctx, hipMemcpyAsync(q->d_desc, q->h_desc, sizeof(qpp_pkt) * q->count, hipMemcpyHostToDevice, s));
-        const uint32_t aes = (1u << QPP_SUITE_TLS_AES_128_GCM_SHA256) | (1u << QPP_SUITE_TLS_AES_256_GCM_SHA384);
         uint32_t flags = QPP_HP_APPLY;
-        if (!(q->suites & ~aes)) flags |= QPP_ONLY_AES;
-        else if (!(q->suites & aes)) flags |= QPP_ONLY_CHACHA;
+        if (!(q->suites & ~kAesSuites)) flags |= QPP_ONLY_AES;
+        else if (!(q->suites & kAesSuites)) flags |= QPP_ONLY_CHACHA;
         rc = qpp_seal_batch(ctx, q->d_desc, q->count, q->d_ring, nullptr, nullptr, flags, s);
         if (rc) return rc;
         HIP_TRY(ctx, hipMemcpyAsync(q->h_ring + q->lo, q->d_ring + q->lo, span, hipMemcpyDeviceToHost, s));

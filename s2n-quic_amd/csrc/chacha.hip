@@ -125,13 +125,20 @@ __device__ __forceinline__ void apply_mask(uint8_t *base, uint32_t hdr_len, uint
 // staging (Stage<4>, device_common.h): each wave instruction loads/stores 16 packets x 64 contiguous bytes instead
 // of 64 scattered 16-byte pieces, and chunk c+1's input is loaded one chunk ahead.
 template <bool SEAL>
-__global__ __launch_bounds__(256) void chacha_kernel(const DevKey *__restrict__ keys, const qpp_pkt *__restrict__ descs,
-                                                    uint32_t n, uint8_t *__restrict__ arena, uint8_t *masks,
-                                                    int8_t *status, uint32_t flags) {
+__global__ __launch_bounds__(256) void chacha_kernel(const DevKey *__restrict__ keys, uint32_t key_cap,
+                                                    const qpp_pkt *__restrict__ descs, uint32_t n,
+                                                    uint8_t *__restrict__ arena, uint8_t *masks, int8_t *status,
+                                                    uint32_t flags) {
     const uint32_t pi = blockIdx.x * blockDim.x + threadIdx.x;
     const qpp_pkt d = descs[pi < n ? pi : n - 1];  // (any valid descriptor for helper lanes)
-    const DevKey *__restrict__ key = keys + d.key_idx;
-    const bool has = pi < n && key->suite == QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256 && !(d.flags & QPP_PKT_SKIP);
+    const bool bad_slot = d.key_idx >= key_cap;    // never dereferenced: the packet is refused
+    const DevKey *__restrict__ key = keys + (bad_slot ? 0u : d.key_idx);
+    // a slot outside the table, a freed slot or a header-key-only slot holds no packet key: refused (no AES kernel
+    // takes such a packet either: the plan gives it no work item with a round count)
+    const bool refused = bad_slot || key->live != 1;
+    if (refused && pi < n && status && !(d.flags & QPP_PKT_SKIP)) status[pi] = QPP_INTERNAL_ERROR;
+    const bool has = pi < n && !refused && key->suite == QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256 &&
+                     !(d.flags & QPP_PKT_SKIP);
     if (!__any(has)) return;  // wave-uniform: AES packets go to aes_gcm_kernel
     Stage<4> st;
     st.lane = threadIdx.x & 63u;
@@ -319,7 +326,7 @@ __device__ __forceinline__ uint32_t byte_of(uint4 v, uint32_t i) {  // byte i (<
 }
 
 template <bool SEAL>
-__global__ __launch_bounds__(256) void chacha_burst_kernel(const DevKey *__restrict__ keys,
+__global__ __launch_bounds__(256) void chacha_burst_kernel(const DevKey *__restrict__ keys, uint32_t key_cap,
                                                           const qpp_pkt *__restrict__ descs, uint32_t n,
                                                           uint8_t *__restrict__ arena, uint8_t *masks, int8_t *status,
                                                           uint32_t flags) {
@@ -327,7 +334,15 @@ __global__ __launch_bounds__(256) void chacha_burst_kernel(const DevKey *__restr
     const uint32_t pi = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
     if (pi >= n) return;
     const qpp_pkt d = descs[pi];
+    if (d.key_idx >= key_cap) {  // wave-uniform: a slot outside the table is refused, never dereferenced
+        if (status && lane == 0 && !(d.flags & QPP_PKT_SKIP)) status[pi] = QPP_INTERNAL_ERROR;
+        return;
+    }
     const DevKey *__restrict__ key = keys + d.key_idx;
+    if (key->live != 1) {  // freed or header-key-only slot: refused
+        if (status && lane == 0 && !(d.flags & QPP_PKT_SKIP)) status[pi] = QPP_INTERNAL_ERROR;
+        return;
+    }
     if (key->suite != QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256 || (d.flags & QPP_PKT_SKIP)) return;  // wave-uniform
     uint32_t k[8];
 #pragma unroll
@@ -467,14 +482,20 @@ __global__ __launch_bounds__(256) void chacha_burst_kernel(const DevKey *__restr
 
 // Header-protection masks for any suite, one lane per packet; AES keys use the LDS T-tables with the
 // lane's own round keys.  Sample at off + aad_len - pn_len + 4.
-__global__ __launch_bounds__(1024) void hp_mask_kernel(const DevKey *__restrict__ keys, const qpp_pkt *__restrict__ descs,
-                                                      uint32_t n, const uint8_t *__restrict__ arena, uint8_t *masks) {
+__global__ __launch_bounds__(1024) void hp_mask_kernel(const DevKey *__restrict__ keys, uint32_t key_cap,
+                                                      const qpp_pkt *__restrict__ descs, uint32_t n,
+                                                      const uint8_t *__restrict__ arena, uint8_t *masks) {
     // 64 KiB of dynamic LDS (the launch reserves it), addressed by offset through lds_ld32/lds_st32
     build_aes_tables(0);
     __syncthreads();
     const uint32_t pi = blockIdx.x * blockDim.x + threadIdx.x;
     if (pi >= n) return;
     const qpp_pkt d = descs[pi];
+    uint8_t *o = masks + 5 * (size_t)pi;
+    if (d.key_idx >= key_cap) {  // no key: an all-zero mask (the caller's descriptor is wrong)
+        o[0] = o[1] = o[2] = o[3] = o[4] = 0;
+        return;
+    }
     const DevKey *__restrict__ key = keys + d.key_idx;
     const uint4 smp = ld16(arena + d.off + d.aad_len - d.pn_len + 4);
     uint32_t m0, m1;
@@ -488,7 +509,6 @@ __global__ __launch_bounds__(1024) void hp_mask_kernel(const DevKey *__restrict_
         uint4 m = key->hp_nr == 10 ? aes.encrypt<10>(smp, key->hp_rk) : aes.encrypt<14>(smp, key->hp_rk);
         m0 = m.x; m1 = m.y;
     }
-    uint8_t *o = masks + 5 * (size_t)pi;
     o[0] = (uint8_t)m0; o[1] = (uint8_t)(m0 >> 8); o[2] = (uint8_t)(m0 >> 16); o[3] = (uint8_t)(m0 >> 24); o[4] = (uint8_t)m1;
 }
 
@@ -498,8 +518,9 @@ __global__ __launch_bounds__(1024) void hp_mask_kernel(const DevKey *__restrict_
 //   largest acknowledged PN (packet/number/mod.rs:191-238) -> the packet key by the key-phase bit 0x04
 //   (key_phase.rs:12,46; KeySet::decrypt_packet, keyset.rs:113-143; long headers: key_idx[0]) -> the qpp_pkt the
 //   open kernels consume.  A packet too short for the sample is DECODE_ERROR and marked QPP_PKT_SKIP.
-__global__ __launch_bounds__(1024) void unprotect_kernel(const DevKey *__restrict__ keys, const qpp_rx_pkt *__restrict__ rx,
-                                                        uint32_t n, uint8_t *__restrict__ arena, qpp_pkt *descs_out,
+__global__ __launch_bounds__(1024) void unprotect_kernel(const DevKey *__restrict__ keys, uint32_t key_cap,
+                                                        const qpp_rx_pkt *__restrict__ rx, uint32_t n,
+                                                        uint8_t *__restrict__ arena, qpp_pkt *descs_out,
                                                         int8_t *status) {
     // 64 KiB of dynamic LDS: the AES T-tables for the AES header keys
     build_aes_tables(0);
@@ -517,6 +538,13 @@ __global__ __launch_bounds__(1024) void unprotect_kernel(const DevKey *__restric
         d.flags = QPP_PKT_SKIP;
         descs_out[i] = d;
         status[i] = QPP_DECODE_ERROR;
+        return;
+    }
+    if (r.key_idx[0] >= key_cap || r.key_idx[1] >= key_cap) {  // slots outside the key table: refused, never read
+        d.flags = QPP_PKT_SKIP;
+        d.key_idx = 0;
+        descs_out[i] = d;
+        status[i] = QPP_INTERNAL_ERROR;
         return;
     }
     const DevKey *__restrict__ hk = keys + r.key_idx[0];
@@ -558,39 +586,39 @@ __global__ __launch_bounds__(1024) void unprotect_kernel(const DevKey *__restric
 
 }  // namespace
 
-hipError_t launch_unprotect(const DevKey *keys, const qpp_rx_pkt *rx, uint32_t n, uint8_t *arena, qpp_pkt *descs_out,
-                            int8_t *status, hipStream_t s) {
+hipError_t launch_unprotect(const DevKey *keys, uint32_t key_cap, const qpp_rx_pkt *rx, uint32_t n, uint8_t *arena,
+                            qpp_pkt *descs_out, int8_t *status, hipStream_t s) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(unprotect_kernel, dim3((n + 1023) / 1024), dim3(1024), 65536, s, keys, rx, n, arena, descs_out,
-                       status);
+    hipLaunchKernelGGL(unprotect_kernel, dim3((n + 1023) / 1024), dim3(1024), 65536, s, keys, key_cap, rx, n, arena,
+                       descs_out, status);
     return hipGetLastError();
 }
 
-hipError_t launch_chacha(bool seal, const DevKey *keys, const qpp_pkt *descs, uint32_t n, uint8_t *arena,
-                         uint8_t *masks, int8_t *status, uint32_t flags, bool burst, hipStream_t s) {
+hipError_t launch_chacha(bool seal, const DevKey *keys, uint32_t key_cap, const qpp_pkt *descs, uint32_t n,
+                         uint8_t *arena, uint8_t *masks, int8_t *status, uint32_t flags, bool burst, hipStream_t s) {
     if (!n) return hipSuccess;
     if (burst) {  // one wave per packet, 4 per workgroup
         if (seal)
-            hipLaunchKernelGGL(chacha_burst_kernel<true>, dim3((n + 3) / 4), dim3(256), 0, s, keys, descs, n, arena,
+            hipLaunchKernelGGL(chacha_burst_kernel<true>, dim3((n + 3) / 4), dim3(256), 0, s, keys, key_cap, descs, n, arena,
                                masks, status, flags);
         else
-            hipLaunchKernelGGL(chacha_burst_kernel<false>, dim3((n + 3) / 4), dim3(256), 0, s, keys, descs, n, arena,
+            hipLaunchKernelGGL(chacha_burst_kernel<false>, dim3((n + 3) / 4), dim3(256), 0, s, keys, key_cap, descs, n, arena,
                                masks, status, flags);
         return hipGetLastError();
     }
     const dim3 grid((n + 255) / 256), block(256);
     const uint32_t lds = 4u * 64u * 16u * 4u;  // Stage<4> per wave, 4 waves
     if (seal)
-        hipLaunchKernelGGL(chacha_kernel<true>, grid, block, lds, s, keys, descs, n, arena, masks, status, flags);
+        hipLaunchKernelGGL(chacha_kernel<true>, grid, block, lds, s, keys, key_cap, descs, n, arena, masks, status, flags);
     else
-        hipLaunchKernelGGL(chacha_kernel<false>, grid, block, lds, s, keys, descs, n, arena, masks, status, flags);
+        hipLaunchKernelGGL(chacha_kernel<false>, grid, block, lds, s, keys, key_cap, descs, n, arena, masks, status, flags);
     return hipGetLastError();
 }
 
-hipError_t launch_hp_mask(const DevKey *keys, const qpp_pkt *descs, uint32_t n, const uint8_t *arena, uint8_t *masks,
-                          hipStream_t s) {
+hipError_t launch_hp_mask(const DevKey *keys, uint32_t key_cap, const qpp_pkt *descs, uint32_t n,
+                          const uint8_t *arena, uint8_t *masks, hipStream_t s) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(hp_mask_kernel, dim3((n + 1023) / 1024), dim3(1024), 65536, s, keys, descs, n,
+    hipLaunchKernelGGL(hp_mask_kernel, dim3((n + 1023) / 1024), dim3(1024), 65536, s, keys, key_cap, descs, n,
                        arena, masks);
     return hipGetLastError();
 }

@@ -168,8 +168,11 @@ __device__ int aes_expand(const uint8_t *key, int key_len, uint32_t *rk) {
 // material record per key (host handles are filled from it): secret' | key | iv | hp
 constexpr int kMatSecret = 0, kMatKey = 48, kMatIv = 80, kMatHp = 96, kMatBytes = 128;
 
-__global__ __launch_bounds__(64) void key_derive_kernel(DevKey *keys, uint32_t first, uint32_t n, int suite,
-                                                       const uint8_t *__restrict__ secrets, uint32_t updates,
+// hp_in == nullptr: the header key is derived from the given secret ("quic hp", TLS_*::new); otherwise it is taken
+// from hp_in (kl bytes per key): the header key of the key being updated (OneRttKey::derive_next_key keeps it).
+__global__ __launch_bounds__(64) void key_derive_kernel(DevKey *keys, const uint32_t *__restrict__ slots, uint32_t n,
+                                                       int suite, const uint8_t *__restrict__ secrets,
+                                                       const uint8_t *__restrict__ hp_in, uint32_t updates,
                                                        uint8_t *material) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -177,7 +180,11 @@ __global__ __launch_bounds__(64) void key_derive_kernel(DevKey *keys, uint32_t f
     const int kl = suite == QPP_SUITE_TLS_AES_128_GCM_SHA256 ? 16 : 32;
     uint8_t s[48], t[48], key[32], iv[12], hp[32];
     for (int j = 0; j < hl; j++) s[j] = secrets[(size_t)i * hl + j];
-    label_expand(hl, s, "quic hp", 7, hp, kl);  // header key of the first secret, kept by every update
+    if (hp_in) {
+        for (int j = 0; j < kl; j++) hp[j] = hp_in[(size_t)i * kl + j];
+    } else {
+        label_expand(hl, s, "quic hp", 7, hp, kl);  // header key of the first secret, kept by every update
+    }
     for (uint32_t u = 0; u < updates; u++) {
         label_expand(hl, s, "quic ku", 7, t, hl);
         for (int j = 0; j < hl; j++) s[j] = t[j];
@@ -185,7 +192,7 @@ __global__ __launch_bounds__(64) void key_derive_kernel(DevKey *keys, uint32_t f
     label_expand(hl, s, "quic key", 8, key, kl);
     label_expand(hl, s, "quic iv", 7, iv, 12);
 
-    DevKey *k = keys + first + i;
+    DevKey *k = keys + slots[i];
     k->suite = (uint32_t)suite;
     for (int w = 0; w < 3; w++)
         k->iv[w] = (uint32_t)iv[4 * w] | ((uint32_t)iv[4 * w + 1] << 8) | ((uint32_t)iv[4 * w + 2] << 16) |
@@ -217,14 +224,14 @@ __global__ __launch_bounds__(64) void key_derive_kernel(DevKey *keys, uint32_t f
 
 uint32_t key_material_bytes() { return kMatBytes; }
 
-hipError_t launch_key_derive(DevKey *keys, uint32_t first, uint32_t n, int suite, const uint8_t *secrets,
-                             uint32_t updates, uint8_t *material, hipStream_t s) {
+hipError_t launch_key_derive(DevKey *keys, const uint32_t *slots, uint32_t n, int suite, const uint8_t *secrets,
+                             const uint8_t *hp_in, uint32_t updates, uint8_t *material, hipStream_t s) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(key_derive_kernel, dim3((n + 63) / 64), dim3(64), 0, s, keys, first, n, suite, secrets, updates,
-                       material);
+    hipLaunchKernelGGL(key_derive_kernel, dim3((n + 63) / 64), dim3(64), 0, s, keys, slots, n, suite, secrets, hp_in,
+                       updates, material);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    return launch_key_setup(keys, first, n, s);
+    return launch_key_install(keys, slots, nullptr, n, s);
 }
 
 }  // namespace qpp

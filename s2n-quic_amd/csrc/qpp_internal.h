@@ -69,7 +69,7 @@ struct alignas(16) DevKey {
     uint32_t suite;      // qpp_suite
     uint32_t nr;         // AES rounds of the packet key (10/14), 0 for ChaCha
     uint32_t hp_nr;      // AES rounds of the HP key
-    uint32_t live;       // 1 while the slot holds a key
+    uint32_t live;       // 1 while the slot holds a packet key (+ its header key), 2: a header key only, 0: free
     uint32_t iv[4];      // 12-byte iv, iv[3] = 0
     uint32_t rk[60];     // AES round keys (11/15 x 4 words) | ChaCha key in rk[0..8)
     uint32_t hp_rk[60];  // AES HP round keys                | ChaCha HP key in hp_rk[0..8)
@@ -104,11 +104,14 @@ struct PlanBuffers {
     uint32_t *n_work;   // [1]
 };
 
-hipError_t launch_key_setup(DevKey *keys, uint32_t first, uint32_t count, hipStream_t s);
-// keysched.hip: n secrets -> updates x "quic ku" -> key/iv (+ hp of the first secret) -> DevKey records
-// keys[first .. first+n) and per-key material (secret' | key | iv | hp, key_material_bytes() each); then key setup
-hipError_t launch_key_derive(DevKey *keys, uint32_t first, uint32_t n, int suite, const uint8_t *secrets,
-                             uint32_t updates, uint8_t *material, hipStream_t s);
+// aes_gcm.hip: records[i] (device, may be nullptr = already in place) -> keys[slots[i]], then H / V[m] for AES keys
+hipError_t launch_key_install(DevKey *keys, const uint32_t *slots, const DevKey *records, uint32_t count,
+                              hipStream_t s);
+// keysched.hip: n secrets -> updates x "quic ku" -> key/iv -> DevKey records keys[slots[i]] and per-key material
+// (secret' | key | iv | hp, key_material_bytes() each); then key install.  The header key is derived from the given
+// secret ("quic hp") when hp_in is nullptr, else taken from hp_in (suite key length per key: update batches).
+hipError_t launch_key_derive(DevKey *keys, const uint32_t *slots, uint32_t n, int suite, const uint8_t *secrets,
+                             const uint8_t *hp_in, uint32_t updates, uint8_t *material, hipStream_t s);
 uint32_t key_material_bytes();
 hipError_t launch_plan(const DevKey *keys, uint32_t key_cap, const qpp_pkt *descs, uint32_t n, PlanBuffers pb,
                        uint32_t per, hipStream_t s);
@@ -126,13 +129,14 @@ hipError_t launch_aes_gcm(bool seal, const DevKey *keys, const qpp_pkt *descs, c
                           uint32_t key_cap, uint32_t per, uint8_t *arena, uint8_t *masks, int8_t *status,
                           uint32_t flags, uint32_t suites, hipStream_t s);
 // burst: one wave per packet (small batches) instead of one lane per packet
-hipError_t launch_chacha(bool seal, const DevKey *keys, const qpp_pkt *descs, uint32_t n, uint8_t *arena,
-                         uint8_t *masks, int8_t *status, uint32_t flags, bool burst, hipStream_t s);
+// key_cap: slots in the key table; a packet naming a slot >= key_cap is never dereferenced (status INTERNAL_ERROR)
+hipError_t launch_chacha(bool seal, const DevKey *keys, uint32_t key_cap, const qpp_pkt *descs, uint32_t n,
+                         uint8_t *arena, uint8_t *masks, int8_t *status, uint32_t flags, bool burst, hipStream_t s);
 // receive side: remove header protection, expand the PN, choose the key by key phase -> descs_out (chacha.hip)
-hipError_t launch_unprotect(const DevKey *keys, const qpp_rx_pkt *rx, uint32_t n, uint8_t *arena, qpp_pkt *descs_out,
-                            int8_t *status, hipStream_t s);
-hipError_t launch_hp_mask(const DevKey *keys, const qpp_pkt *descs, uint32_t n, const uint8_t *arena,
-                          uint8_t *masks, hipStream_t s);
+hipError_t launch_unprotect(const DevKey *keys, uint32_t key_cap, const qpp_rx_pkt *rx, uint32_t n, uint8_t *arena,
+                            qpp_pkt *descs_out, int8_t *status, hipStream_t s);
+hipError_t launch_hp_mask(const DevKey *keys, uint32_t key_cap, const qpp_pkt *descs, uint32_t n,
+                          const uint8_t *arena, uint8_t *masks, hipStream_t s);
 
 // ---------------------------------------------------------------- host key schedule (kdf.cpp)
 size_t suite_key_len(int suite);

@@ -53,8 +53,12 @@ EXPORTS = [
     "qpp_event_elapsed_ms", "qpp_stream_wait_event", "qpp_unprotect_open_batch", "qpp_pn_truncate", "qpp_pn_expand",
     "qpp_key_new_batch", "qpp_txq_create", "qpp_txq_destroy", "qpp_txq_ring", "qpp_txq_push", "qpp_txq_flush",
     "qpp_txq_pending", "qpp_memcpy_d2d", "qpp_ctx_set_burst_max", "qpp_dc_key_new", "qpp_dc_seal", "qpp_dc_open",
-    "qpp_dc_open_in_place",
+    "qpp_dc_open_in_place", "qpp_ctx_key_slots", "qpp_key_new_pair", "qpp_key_update_batch", "qpp_initial_keys_pair",
+    "qpp_header_key_new", "qpp_header_key_new_raw", "qpp_header_key_free", "qpp_header_key_slot",
+    "qpp_header_key_suite", "qpp_header_key_sample_len", "qpp_header_key_mask", "qpp_host_batch_submit",
+    "qpp_host_batch_query", "qpp_host_batch_wait", "qpp_ctx_set_host_pipe",
 ]
+OP_SEAL, OP_OPEN = 0x1, 0x2
 
 
 class QppError(RuntimeError):
@@ -136,6 +140,21 @@ def lib():
             "qpp_dc_seal": (ctypes.c_int, [vp, u64, vp, sz, vp, sz, vp, sz]),
             "qpp_dc_open": (ctypes.c_int, [vp, ctypes.c_int, u64, vp, sz, vp, vp, sz, vp, sz]),
             "qpp_dc_open_in_place": (ctypes.c_int, [vp, ctypes.c_int, u64, vp, sz, vp, sz, vp, sz]),
+            "qpp_ctx_key_slots": (ctypes.c_int, [vp, ctypes.POINTER(u32), ctypes.POINTER(u32), ctypes.POINTER(u32)]),
+            "qpp_key_new_pair": (ctypes.c_int, [vp, ctypes.c_int, vp, sz, ctypes.POINTER(vp), ctypes.POINTER(vp)]),
+            "qpp_key_update_batch": (ctypes.c_int, [vp, sz, vp]),
+            "qpp_initial_keys_pair": (ctypes.c_int, [vp, ctypes.c_int, vp, sz] + [ctypes.POINTER(vp)] * 4),
+            "qpp_header_key_new": (ctypes.c_int, [vp, ctypes.c_int, vp, sz, ctypes.POINTER(vp)]),
+            "qpp_header_key_new_raw": (ctypes.c_int, [vp, ctypes.c_int, vp, sz, ctypes.POINTER(vp)]),
+            "qpp_header_key_free": (None, [vp]),
+            "qpp_header_key_slot": (u32, [vp]),
+            "qpp_header_key_suite": (ctypes.c_int, [vp]),
+            "qpp_header_key_sample_len": (sz, [vp]),
+            "qpp_header_key_mask": (ctypes.c_int, [vp, vp, sz, vp]),
+            "qpp_host_batch_submit": (ctypes.c_int, [vp, vp, sz, vp, vp, vp, u32, u32, ctypes.POINTER(u64)]),
+            "qpp_host_batch_query": (ctypes.c_int, [vp, u64, ctypes.POINTER(ctypes.c_int)]),
+            "qpp_host_batch_wait": (ctypes.c_int, [vp, u64]),
+            "qpp_ctx_set_host_pipe": (ctypes.c_int, [vp, sz, sz, sz]),
         }
         assert set(sig) == set(EXPORTS)
         for name, (res, args) in sig.items():
@@ -225,6 +244,63 @@ class Context:
             raise QppError(rc, "qpp_key_new")
         return Key(self, h.value)
 
+    def key_pair(self, suite, secret):
+        """TLS_*::new(secret) -> (Key, HeaderKey), independently owned (qpp_key_new_pair)."""
+        k, h = vp(), vp()
+        rc = lib().qpp_key_new_pair(self.handle, suite, _bytes_ptr(secret), len(secret), ctypes.byref(k),
+                                    ctypes.byref(h))
+        if rc != OK:
+            raise QppError(rc, "qpp_key_new_pair")
+        return Key(self, k.value), HeaderKey(self, h.value)
+
+    def header_key(self, suite, secret=None, hp=None):
+        """HeaderKey::new(secret, "quic hp") or from the raw header-protection key."""
+        h = vp()
+        if hp is not None:
+            rc = lib().qpp_header_key_new_raw(self.handle, suite, _bytes_ptr(hp), len(hp), ctypes.byref(h))
+        else:
+            rc = lib().qpp_header_key_new(self.handle, suite, _bytes_ptr(secret), len(secret), ctypes.byref(h))
+        if rc != OK:
+            raise QppError(rc, "qpp_header_key_new")
+        return HeaderKey(self, h.value)
+
+    def update_keys(self, keys):
+        """qpp_key_update_batch: [k.derive_next_key() for k in keys] in one device pass per suite."""
+        n = len(keys)
+        arr_in = (vp * max(n, 1))(*[k.handle for k in keys])
+        arr = (vp * max(n, 1))()
+        rc = lib().qpp_key_update_batch(arr_in, n, arr)
+        if rc != OK:
+            raise QppError(rc, "qpp_key_update_batch")
+        return [Key(self, arr[i]) for i in range(n)]
+
+    def key_slots(self):
+        """(capacity, high-water slot, retired-not-yet-reusable) of the device key table."""
+        c, h, r = u32(), u32(), u32()
+        self._check(lib().qpp_ctx_key_slots(self.handle, ctypes.byref(c), ctypes.byref(h), ctypes.byref(r)), "slots")
+        return c.value, h.value, r.value
+
+    def set_host_pipe(self, chunk_packets, chunk_bytes, slots):
+        self._check(lib().qpp_ctx_set_host_pipe(self.handle, chunk_packets, chunk_bytes, slots), "set_host_pipe")
+
+    def host_submit(self, descs, arena, masks=None, status=None, flags=0, ops=OP_SEAL | OP_OPEN):
+        """qpp_host_batch_submit over host numpy arrays (arena ideally from host_alloc); returns the ticket.
+        The arrays must stay alive and untouched until host_wait(ticket)."""
+        t = u64()
+        self._check(lib().qpp_host_batch_submit(self.handle, descs.ctypes.data, len(descs), arena.ctypes.data,
+                                                None if masks is None else masks.ctypes.data,
+                                                None if status is None else status.ctypes.data, flags, ops,
+                                                ctypes.byref(t)), "host_batch_submit")
+        return t.value
+
+    def host_done(self, ticket):
+        d = ctypes.c_int()
+        self._check(lib().qpp_host_batch_query(self.handle, ticket, ctypes.byref(d)), "host_batch_query")
+        return bool(d.value)
+
+    def host_wait(self, ticket):
+        self._check(lib().qpp_host_batch_wait(self.handle, ticket), "host_batch_wait")
+
     def keys_batch(self, suite, secrets, updates=0):
         """qpp_key_new_batch: every secret -> `updates` x derive_next_key, derived on the GPU in one pass."""
         secrets = [bytes(x) for x in secrets]
@@ -250,6 +326,14 @@ class Context:
         if rc != OK:
             raise QppError(rc, "qpp_dc_key_new")
         return DcKey(self, h.value)
+
+    def initial_keys_pair(self, endpoint, dcid):
+        """InitialKey::new_* -> (sealer, opener, header sealer, header opener)"""
+        hs = [vp() for _ in range(4)]
+        rc = lib().qpp_initial_keys_pair(self.handle, endpoint, _bytes_ptr(dcid), len(dcid), *[ctypes.byref(h) for h in hs])
+        if rc != OK:
+            raise QppError(rc, "qpp_initial_keys_pair")
+        return Key(self, hs[0].value), Key(self, hs[1].value), HeaderKey(self, hs[2].value), HeaderKey(self, hs[3].value)
 
     def initial_keys(self, endpoint, dcid):
         s, o = vp(), vp()
@@ -293,14 +377,25 @@ class Context:
         self._check(lib().qpp_stream_create(self.handle, ctypes.byref(st)), "stream")
         return st.value
 
+    def stream_destroy(self, stream):
+        lib().qpp_stream_destroy(self.handle, stream)
+
+    def synchronize(self):
+        """whole device (qpp_ctx_synchronize): every stream, key installs and retirements included"""
+        self._check(lib().qpp_ctx_synchronize(self.handle), "synchronize")
+
     def wait(self, stream, ev):
         self._check(lib().qpp_stream_wait_event(self.handle, stream, ev), "wait_event")
 
     def host_alloc(self, nbytes):
-        """pinned host memory as a numpy uint8 array (freed with the context)"""
+        """pinned host memory as a numpy uint8 array (host_free it, or it lives until the process ends)"""
         p = vp()
         self._check(lib().qpp_host_alloc(self.handle, int(nbytes), ctypes.byref(p)), "host_alloc")
         return np.ctypeslib.as_array((ctypes.c_uint8 * int(nbytes)).from_address(p.value))
+
+    def host_free(self, arr):
+        """release a host_alloc array (no view of it may be used afterwards)"""
+        lib().qpp_host_free(self.handle, arr.ctypes.data)
 
     def elapsed_ms(self, e0, e1):
         ms = ctypes.c_float()
@@ -391,6 +486,39 @@ class Key:
         if rc != OK:
             raise QppError(rc, "qpp_hp_mask")
         return bytes(out)
+
+
+class HeaderKey:
+    """HeaderKey (header_key.rs:7-63): owned independently of the packet keys it was born with."""
+
+    def __init__(self, ctx, handle):
+        self.ctx, self.handle = ctx, handle
+
+    def free(self):
+        if self.handle:
+            lib().qpp_header_key_free(self.handle)
+            self.handle = None
+
+    @property
+    def slot(self):
+        return lib().qpp_header_key_slot(self.handle)
+
+    @property
+    def suite(self):
+        return lib().qpp_header_key_suite(self.handle)
+
+    def sample_len(self):
+        return lib().qpp_header_key_sample_len(self.handle)
+
+    def header_protection_mask(self, sample):
+        out = (ctypes.c_uint8 * 5)()
+        rc = lib().qpp_header_key_mask(self.handle, _bytes_ptr(sample), len(sample), out)
+        if rc != OK:
+            raise QppError(rc, "qpp_header_key_mask")
+        return bytes(out)
+
+    sealing_header_protection_mask = header_protection_mask
+    opening_header_protection_mask = header_protection_mask
 
 
 # ------------------------------------------------------------------ synthetic batches (bench + tests)

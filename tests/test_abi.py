@@ -28,7 +28,7 @@ def test_library_exports_every_symbol():
     L = ctypes.CDLL(qpp.LIB_PATH)
     for name in declared_functions():
         assert hasattr(L, name), name
-    assert qpp.lib().qpp_abi_version() == 1
+    assert qpp.lib().qpp_abi_version() == 2
 
 
 def test_pkt_layout_matches_oracle():

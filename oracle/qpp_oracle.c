@@ -272,14 +272,14 @@ static void chacha_poly_core(const uint8_t key[32], const uint8_t nonce[12], con
         mac = heap;
     }
     memset(mac, 0, mlen);
-    memcpy(mac, aad, aad_len);
-    if (!encrypt) memcpy(mac + aad_len + pa, buf, len);
+    if (aad_len) memcpy(mac, aad, aad_len);  /* (aad / buf may be NULL at length 0) */
+    if (!encrypt && len) memcpy(mac + aad_len + pa, buf, len);
     for (size_t off = 0; off < len; off += 64) {
         orc_chacha20_block(key, (uint32_t)(1 + off / 64), nonce, blk);
         size_t n = len - off < 64 ? len - off : 64;
         for (size_t k = 0; k < n; k++) buf[off + k] ^= blk[k];
     }
-    if (encrypt) memcpy(mac + aad_len + pa, buf, len);
+    if (encrypt && len) memcpy(mac + aad_len + pa, buf, len);
     uint8_t *lens = mac + aad_len + pa + len + pc;
     for (int i = 0; i < 8; i++) {
         lens[i] = (uint8_t)((uint64_t)aad_len >> (8 * i));
@@ -326,7 +326,7 @@ void orc_sha256(const uint8_t *msg, size_t len, uint8_t out[32]) {
     for (size_t i = 0; i < full; i++) sha256_block(st, msg + 64 * i);
     uint8_t tail[128] = {0};
     size_t rem = len % 64;
-    memcpy(tail, msg + 64 * full, rem);
+    if (rem) memcpy(tail, msg + 64 * full, rem);
     tail[rem] = 0x80;
     size_t tl = rem < 56 ? 64 : 128;
     put_be64(tail + tl - 8, (uint64_t)len * 8);
@@ -385,7 +385,7 @@ void orc_sha384(const uint8_t *msg, size_t len, uint8_t out[48]) {
     for (size_t i = 0; i < full; i++) sha512_block(st, msg + 128 * i);
     uint8_t tail[256] = {0};
     size_t rem = len % 128;
-    memcpy(tail, msg + 128 * full, rem);
+    if (rem) memcpy(tail, msg + 128 * full, rem);
     tail[rem] = 0x80;
     size_t tl = rem < 112 ? 128 : 256;
     put_be64(tail + tl - 8, (uint64_t)len * 8); /* high 64 bits of the 128-bit length stay 0 */
@@ -406,7 +406,8 @@ void orc_hmac(size_t hash_len, const uint8_t *key, size_t key_len, const uint8_t
     /* inner = H(ipad || msg) — assemble into one buffer (messages here are small) */
     uint8_t tmp[128 + 512];
     if (len > 512) return; /* not needed for this path */
-    memcpy(tmp, ipad, bs); memcpy(tmp + bs, msg, len);
+    memcpy(tmp, ipad, bs);
+    if (len) memcpy(tmp + bs, msg, len);
     hash_any(hash_len, tmp, bs + len, inner);
     memcpy(tmp, opad, bs); memcpy(tmp + bs, inner, hash_len);
     hash_any(hash_len, tmp, bs + hash_len, out);
@@ -421,7 +422,7 @@ void orc_hkdf_expand(size_t hash_len, const uint8_t *prk, const uint8_t *info, s
     size_t tlen = 0, done = 0;
     for (uint8_t i = 1; done < out_len; i++) {
         memcpy(msg, t, tlen);
-        memcpy(msg + tlen, info, info_len);
+        if (info_len) memcpy(msg + tlen, info, info_len);
         msg[tlen + info_len] = i;
         orc_hmac(hash_len, prk, hash_len, msg, tlen + info_len + 1, t);
         tlen = hash_len;
@@ -505,7 +506,7 @@ int orc_open(int suite, const uint8_t *key, const uint8_t nonce[12],
     uint8_t diff = 0;
     for (int i = 0; i < 16; i++) diff |= (uint8_t)(tag[i] ^ buf[len + i]);
     if (diff) {
-        memset(buf, 0, len); /* never release unauthenticated plaintext */
+        if (len) memset(buf, 0, len); /* never release unauthenticated plaintext */
         return ORC_DECRYPT_ERROR;
     }
     return ORC_OK;

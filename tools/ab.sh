@@ -1,6 +1,9 @@
 #!/bin/bash
-# Same-box A/B: alternate benches of two library builds (QPP_LIB) and variants; usage: A=<so> B=<so> bash tools/ab.sh tag
+# Same-box A/B: alternate benches of library builds (QPP_LIB) and AES variants (QPP_AES_VARIANT), 3 rounds.
+# usage: CFGS="ab/a.so:0 ab/b.so:0 s2n-quic_amd/libqpp.so:1" [BENCH_ARGS="--suite aes256gcm --keys 64"] bash tools/ab.sh tag
+#   CFGS: space-separated <library path>:<variant index> pairs; BENCH_ARGS: extra bench.py arguments
 set -o pipefail
+[ -n "$CFGS" ] || { echo "CFGS is empty: nothing to compare (see the usage line)"; exit 2; }
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 tag=${1:-ab}; mkdir -p gpurun_out/$tag

@@ -163,6 +163,8 @@ def main():
     ap.add_argument("--pt", type=int, default=1200, help="payload bytes per packet")
     ap.add_argument("--aad", type=int, default=21, help="short header: 0x43 || DCID16 || PN4")
     ap.add_argument("--keys", type=int, default=1)
+    ap.add_argument("--key-run", type=int, default=1,
+                    help="consecutive packets per key run (1: every packet's key drawn independently; 64: GSO bursts)")
     ap.add_argument("--mode", default="device", choices=["device", "e2e", "rx", "keys", "txq", "packet"],
                     help="device: seal+open in HBM (headline); e2e: pinned host -> HBM -> host; rx: receive path "
                          "(unprotect -> PN expand -> open); keys: device key schedule (key-update churn); "
@@ -196,7 +198,8 @@ def main():
     n, pt, aad = args.packets, args.pt, args.aad
     sh = multigpu.shard(rank, world, n, seed_base=0x5eed0000 + 1)
     sh["pn_base"] = args.pn_first
-    descs, arena = qpp.make_batch(n, pt, [k.slot for k in keys], seed=sh["seed"], aad_len=aad, pn_base=sh["pn_base"])
+    descs, arena = qpp.make_batch(n, pt, [k.slot for k in keys], seed=sh["seed"], aad_len=aad, pn_base=sh["pn_base"],
+                                  run=args.key_run)
     flags = (0 if args.no_hp else qpp.HP_MASK_OUT) | (qpp.ONLY_CHACHA if suite == 3 else qpp.ONLY_AES)
     d_desc, d_mask, d_status = ctx.alloc(descs.nbytes), ctx.alloc(5 * n), ctx.alloc(n)
     d_desc.upload(descs)

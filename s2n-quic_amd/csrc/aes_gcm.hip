@@ -220,8 +220,17 @@ __device__ __forceinline__ void process_packet(const AesLds &aes, const Ghash &g
 #ifndef QPP_LEAN
         // GHASH of the previous group (independent of the keystream just issued)
 #pragma unroll
-        for (int j = 0; j < NB; j++)
+        for (int j = 0; j < NB; j++) {
+#ifdef QPP_GHASH_SELECT
+            // unconditional product + select: the steps stay in the keystream's basic block (no branch), so the
+            // scheduler can interleave their LDS reads with the AES rounds; invalid slots (counter 0/1 of group 0,
+            // past the last block) compute a product that is discarded
+            const uint4 zn = gh.mulx(z, cprev[j]);
+            if (bprev + j >= 0 && bprev + j < nblk) z = zn;
+#else
             if (bprev + j >= 0 && bprev + j < nblk) z = gh.mulx(z, cprev[j]);
+#endif
+        }
         if (g == 0) ek0 = ks[1];
 #endif
         const int b0 = NB * g - 2;  // data block of slot 0
@@ -407,7 +416,7 @@ namespace {
 struct Variant {
     int nb, wg, per;
 };
-constexpr Variant kVariants[] = {{4, 512, 1024}, {2, 1024, 1024}, {2, 512, 1024}, {4, 256, 1024}};
+constexpr Variant kVariants[] = {{4, 512, 1024}, {2, 1024, 1024}, {2, 512, 1024}, {4, 256, 1024}, {2, 768, 1536}};
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 constexpr uint32_t lds_bytes(int nb, int wg) {
     return kLdsStage + (uint32_t)(wg / 64) * 1024u * (uint32_t)nb;
@@ -424,6 +433,7 @@ void launch_variant(int v, dim3 grid, hipStream_t s, const DevKey *keys, const q
         case 1: { QPP_AES_LAUNCH(2, 1024); break; }
         case 2: { QPP_AES_LAUNCH(2, 512); break; }
         case 3: { QPP_AES_LAUNCH(4, 256); break; }
+        case 4: { QPP_AES_LAUNCH(2, 768); break; }
         default: { QPP_AES_LAUNCH(4, 512); break; }
     }
 #undef QPP_AES_LAUNCH

@@ -9,8 +9,12 @@
 //   * key records reach HBM on the context's key stream (one install launch per flush, over a slot list, never a range
 //     that could rewrite a live neighbour) and a `keys_ready` event; a batch on any stream first waits (device side)
 //     for the latest install it has not yet waited for.  The host never blocks on data batches to install a key;
-//   * a freed key's slot is retired in stream order on the retire stream: it waits for every StreamState's last
-//     event, zeroes the device record and records a "retired" event; the slot is reused only once that completed.
+//   * a freed key's slot is retired in stream order on the retire stream: freed slots collect in a pending list that
+//     is flushed before the next batch, key install or synchronisation (or once it holds kRetireFlush slots): the
+//     retire stream waits for every StreamState's last event, one memset per run of consecutive slots zeroes their
+//     device records, and one
+//     "retired" event marks them; the slots are reused only once that completed.  (A rotation of 4096 keys used to
+//     cost 4096 memset launches.)
 #include <string.h>
 
 #include <algorithm>
@@ -35,9 +39,10 @@ struct StreamState {
 };
 
 struct Retired {
-    uint32_t slot;
-    hipEvent_t done;  // the zeroing of the device record (context stream) has completed
+    std::vector<uint32_t> slots;
+    hipEvent_t done;  // the zeroing of these device records (retire stream) has completed
 };
+constexpr size_t kRetireFlush = 4096;  // pending retirements that force a flush from qpp_key_free itself
 
 // One slot of the host pipeline: device buffers for one chunk in flight, and the events that order its reuse.
 struct PipeSlot {
@@ -77,6 +82,8 @@ struct qpp_ctx {
     std::vector<uint32_t> dirty;          // slots whose host record must be installed before the next launch
     std::vector<uint32_t> free_slots;     // reusable now
     std::deque<Retired> retired;          // reusable once `done` has completed
+    std::vector<uint32_t> retire_pending; // freed, host copy zeroized, device zeroing not yet enqueued
+    uint32_t retired_slots = 0;           // slots in `retired`
     uint32_t live_by_suite[4] = {0, 0, 0, 0};  // live packet keys per suite: which kernels a batch can need
     uint32_t next_slot = 0;
     // per-stream state (plan scratch, last-batch event); [0] is the context stream
@@ -199,12 +206,16 @@ int grow_keys(qpp_ctx *ctx, uint32_t need) {
     DevKey *nk = nullptr;
     HIP_TRY(ctx, hipDeviceSynchronize());  // no batch may still read the old table
     HIP_TRY(ctx, hipMalloc(&nk, sizeof(DevKey) * cap));
-    HIP_TRY(ctx, hipMemset(nk, 0, sizeof(DevKey) * cap));
+    // Stream-ordered and waited for: a plain hipMemset runs on the null stream, which does not order against the
+    // context's non-blocking streams (a batch could read the table before it is zeroed).
+    HIP_TRY(ctx, hipMemsetAsync(nk, 0, sizeof(DevKey) * cap, ctx->kstream));
     if (ctx->d_keys) {
-        HIP_TRY(ctx, hipMemcpy(nk, ctx->d_keys, sizeof(DevKey) * ctx->key_cap, hipMemcpyDeviceToDevice));
-        HIP_TRY(ctx, hipMemset(ctx->d_keys, 0, sizeof(DevKey) * ctx->key_cap));
-        HIP_TRY(ctx, hipFree(ctx->d_keys));
+        HIP_TRY(ctx, hipMemcpyAsync(nk, ctx->d_keys, sizeof(DevKey) * ctx->key_cap, hipMemcpyDeviceToDevice,
+                                    ctx->kstream));
+        HIP_TRY(ctx, hipMemsetAsync(ctx->d_keys, 0, sizeof(DevKey) * ctx->key_cap, ctx->kstream));
     }
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->kstream));
+    if (ctx->d_keys) HIP_TRY(ctx, hipFree(ctx->d_keys));
     ctx->d_keys = nk;
     ctx->h_keys.resize(cap);
     ctx->dirty_flag.resize(cap, 0);
@@ -228,9 +239,12 @@ int ensure_kstage(qpp_ctx *ctx, size_t bytes) {
     return QPP_OK;
 }
 
+int flush_retire(qpp_ctx *ctx);
+
 // Installs every pending host record on the device: one copy + one install launch on the key stream, then the
 // keys_ready event that the next batch on every stream waits for (device side; H and V[m] included).
 int flush_keys(qpp_ctx *ctx) {
+    RC_TRY(flush_retire(ctx));
     if (ctx->dirty.empty()) return QPP_OK;
     const uint32_t n = (uint32_t)ctx->dirty.size();
     const size_t rec = sizeof(DevKey) * n, slots = 4 * (size_t)n;
@@ -270,7 +284,10 @@ int ensure_plan(qpp_ctx *ctx, StreamState *st, uint32_t n) {
     st->plan_n_cap = st->plan_key_cap = 0;
     const uint32_t ncap = std::max(n, st->plan_n_cap), kcap = ctx->key_cap;
     HIP_TRY(ctx, hipMalloc(&p.counts, sizeof(uint32_t) * kcap));
-    HIP_TRY(ctx, hipMemset(p.counts, 0, sizeof(uint32_t) * kcap));  // plan_scan re-zeroes it after every plan
+    // zeroed on the batch's own stream: plan_hist on this stream follows it.  (A plain hipMemset goes to the null
+    // stream, which does not order against non-blocking streams: with recycled device memory plan_hist then counted
+    // on top of stale words and the scatter wrote past perm[] -- an illegal address under two concurrent streams.)
+    HIP_TRY(ctx, hipMemsetAsync(p.counts, 0, sizeof(uint32_t) * kcap, st->stream));  // plan_scan re-zeroes it after each plan
     HIP_TRY(ctx, hipMalloc(&p.cursor, sizeof(uint32_t) * kcap));
     HIP_TRY(ctx, hipMalloc(&p.istart, sizeof(uint32_t) * (kcap + 1)));
     HIP_TRY(ctx, hipMalloc(&p.perm, sizeof(uint32_t) * std::max<uint32_t>(ncap, 1)));
@@ -301,12 +318,15 @@ int ensure_stage(qpp_ctx *ctx, size_t bytes) {
 
 // A slot for a new key: a retired slot whose zeroing has completed, else a fresh one.
 int alloc_slot(qpp_ctx *ctx, uint32_t *out) {
+    RC_TRY(flush_retire(ctx));
     while (!ctx->retired.empty()) {
         const hipError_t q = hipEventQuery(ctx->retired.front().done);
         if (q == hipErrorNotReady) break;
         if (fail(ctx, q, "retired slot event")) return QPP_DEVICE_ERROR;
-        ctx->free_slots.push_back(ctx->retired.front().slot);
-        put_event(ctx, ctx->retired.front().done);
+        Retired &r = ctx->retired.front();
+        ctx->free_slots.insert(ctx->free_slots.end(), r.slots.rbegin(), r.slots.rend());
+        ctx->retired_slots -= (uint32_t)r.slots.size();
+        put_event(ctx, r.done);
         ctx->retired.pop_front();
     }
     if (!ctx->free_slots.empty()) {
@@ -319,24 +339,45 @@ int alloc_slot(qpp_ctx *ctx, uint32_t *out) {
     return QPP_OK;
 }
 
-// Zeroizes a slot's device record behind every batch already enqueued on any stream of this context, then queues
-// the slot for reuse (cipher_suite.rs:106-114,189-193 zeroize on drop; here "drop" is stream-ordered).
-void retire_slot(qpp_ctx *ctx, uint32_t slot) {
-    secure_zero(&ctx->h_keys[slot], sizeof(DevKey));
-    hipSetDevice(ctx->device);
+// Zeroizes the slots' device records behind every batch already enqueued on any stream of this context (one launch
+// for all pending slots), then queues the slots for reuse (cipher_suite.rs:106-114,189-193 zeroize on drop; here
+// "drop" is stream-ordered).  Called before anything new is enqueued, so the retire stream waits only for batches
+// enqueued before the keys were freed (and possibly a few after: never too early).
+int flush_retire(qpp_ctx *ctx) {
+    if (ctx->retire_pending.empty()) return QPP_OK;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
     for (StreamState *st : ctx->streams)
-        if (st->used) hipStreamWaitEvent(ctx->rstream, st->last, 0);
-    hipStreamWaitEvent(ctx->rstream, ctx->keys_ready, 0);  // behind the slot's own install, if still pending
-    hipMemsetAsync(ctx->d_keys + slot, 0, sizeof(DevKey), ctx->rstream);
+        if (st->used) HIP_TRY(ctx, hipStreamWaitEvent(ctx->rstream, st->last, 0));
+    HIP_TRY(ctx, hipStreamWaitEvent(ctx->rstream, ctx->keys_ready, 0));  // behind the slots' own installs
+    // one memset per run of consecutive slots (a rotation frees whole batches of keys that were allocated together)
+    std::vector<uint32_t> sorted(ctx->retire_pending);
+    std::sort(sorted.begin(), sorted.end());
+    for (size_t i = 0; i < sorted.size();) {
+        size_t j = i + 1;
+        while (j < sorted.size() && sorted[j] == sorted[j - 1] + 1) j++;
+        HIP_TRY(ctx, hipMemsetAsync(ctx->d_keys + sorted[i], 0, sizeof(DevKey) * (j - i), ctx->rstream));
+        i = j;
+    }
     hipEvent_t e = get_event(ctx);
     if (!e || hipEventRecord(e, ctx->rstream) != hipSuccess) {
-        // no event: wait here instead (the slot must never be reused while a batch may read it)
-        hipStreamSynchronize(ctx->rstream);
+        // no event: wait here instead (a slot must never be reused while a batch may read it)
         put_event(ctx, e);
-        ctx->free_slots.push_back(slot);
-        return;
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->rstream));
+        ctx->free_slots.insert(ctx->free_slots.end(), ctx->retire_pending.begin(), ctx->retire_pending.end());
+        ctx->retire_pending.clear();
+        return QPP_OK;
     }
-    ctx->retired.push_back(Retired{slot, e});
+    ctx->retired_slots += (uint32_t)ctx->retire_pending.size();
+    ctx->retired.push_back(Retired{std::move(ctx->retire_pending), e});
+    ctx->retire_pending.clear();
+    return QPP_OK;
+}
+
+// Frees a slot: the host copy is zeroized now, the device record behind in-flight work (flush_retire).
+void retire_slot(qpp_ctx *ctx, uint32_t slot) {
+    secure_zero(&ctx->h_keys[slot], sizeof(DevKey));
+    ctx->retire_pending.push_back(slot);
+    if (ctx->retire_pending.size() >= kRetireFlush) flush_retire(ctx);
 }
 
 // Fills the slot's host record from the key's material and marks it for installation.
@@ -579,7 +620,11 @@ void pipe_release(qpp_ctx *ctx) {
     HostPipe *p = ctx->pipe;
     if (!p) return;
     for (PipeSlot &sl : p->slots) {
-        if (sl.arena) { hipMemset(sl.arena, 0, p->chunk_bytes); hipFree(sl.arena); }
+        if (sl.arena) {
+            hipMemsetAsync(sl.arena, 0, p->chunk_bytes, ctx->stream);
+            hipStreamSynchronize(ctx->stream);
+            hipFree(sl.arena);
+        }
         hipFree(sl.descs); hipFree(sl.masks); hipFree(sl.status);
         if (sl.h2d) hipEventDestroy(sl.h2d);
         if (sl.comp) hipEventDestroy(sl.comp);
@@ -637,8 +682,13 @@ int qpp_ctx_set_burst_max(qpp_ctx *ctx, size_t max_packets) {
 void qpp_ctx_destroy(qpp_ctx *ctx) {
     if (!ctx) return;
     hipSetDevice(ctx->device);
+    if (ctx->d_keys) flush_retire(ctx);  // pending zeroizations, while the table and the stream states still exist
     hipDeviceSynchronize();
-    if (ctx->d_keys) { hipMemset(ctx->d_keys, 0, sizeof(DevKey) * ctx->key_cap); hipFree(ctx->d_keys); }
+    if (ctx->d_keys) {
+        hipMemsetAsync(ctx->d_keys, 0, sizeof(DevKey) * ctx->key_cap, ctx->stream);
+        hipStreamSynchronize(ctx->stream);
+        hipFree(ctx->d_keys);
+    }
     secure_zero(ctx->h_keys.data(), sizeof(DevKey) * ctx->h_keys.size());
     for (StreamState *st : ctx->streams) {
         free_plan(st->plan);
@@ -670,6 +720,7 @@ void *qpp_ctx_stream(qpp_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr;
 
 int qpp_ctx_synchronize(qpp_ctx *ctx) {
     HIP_TRY(ctx, hipSetDevice(ctx->device));
+    RC_TRY(flush_retire(ctx));
     HIP_TRY(ctx, hipDeviceSynchronize());
     return QPP_OK;
 }
@@ -680,7 +731,7 @@ int qpp_ctx_key_slots(qpp_ctx *ctx, uint32_t *capacity, uint32_t *high_water, ui
     if (!ctx) return QPP_INTERNAL_ERROR;
     if (capacity) *capacity = ctx->key_cap;
     if (high_water) *high_water = ctx->next_slot;
-    if (retired) *retired = (uint32_t)ctx->retired.size();
+    if (retired) *retired = ctx->retired_slots + (uint32_t)ctx->retire_pending.size();
     return QPP_OK;
 }
 
@@ -1356,7 +1407,11 @@ void qpp_txq_destroy(qpp_txq *q) {
     hipSetDevice(q->ctx->device);
     hipStreamSynchronize(q->ctx->stream);
     if (q->h_ring) { secure_zero(q->h_ring, q->ring_bytes); hipHostFree(q->h_ring); }
-    if (q->d_ring) { hipMemset(q->d_ring, 0, q->ring_bytes); hipFree(q->d_ring); }
+    if (q->d_ring) {
+        hipMemsetAsync(q->d_ring, 0, q->ring_bytes, q->ctx->stream);
+        hipStreamSynchronize(q->ctx->stream);
+        hipFree(q->d_ring);
+    }
     if (q->h_desc) hipHostFree(q->h_desc);
     if (q->d_desc) hipFree(q->d_desc);
     if (q->h_perm) hipHostFree(q->h_perm);

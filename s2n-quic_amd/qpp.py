@@ -560,11 +560,12 @@ def xoshiro_bytes(seed, n):
     return np.random.Generator(np.random.PCG64(seed)).integers(0, 256, size=n, dtype=np.uint8)
 
 
-def make_batch(n, pt_len, key_slots, seed, aad_len=21, pn_len=4, pn_base=0, stride=None, mixed=True):
+def make_batch(n, pt_len, key_slots, seed, aad_len=21, pn_len=4, pn_base=0, stride=None, mixed=True, run=1):
     """Packets back to back in an arena: [AAD aad_len | payload pt_len | tag 16] per `stride` bytes.
 
-    AAD = 1-RTT short header 0x43 || DCID(16) || PN(4).  key_idx = splitmix64(i) % len(key_slots)
-    when mixed, else key_slots[0].  Returns (descs, arena).
+    AAD = 1-RTT short header 0x43 || DCID(16) || PN(4) (SURVEY §8d).  key_idx = splitmix64(i // run) % len(key_slots)
+    when mixed (run > 1: runs of `run` consecutive packets of one connection, a GSO burst), else key_slots[0].
+    Returns (descs, arena).
     """
     stride = stride or ((aad_len + pt_len + 16 + 15) // 16) * 16
     if n * stride > 1 << 32:
@@ -580,7 +581,7 @@ def make_batch(n, pt_len, key_slots, seed, aad_len=21, pn_len=4, pn_base=0, stri
     descs["pn_len"] = pn_len
     slots = np.asarray(key_slots, dtype=np.uint32)
     if mixed and len(slots) > 1:
-        z = (idx + np.uint64(0x9E3779B97F4A7C15)) * np.uint64(1)
+        z = (idx // np.uint64(max(1, run)) + np.uint64(0x9E3779B97F4A7C15)) * np.uint64(1)
         z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
         z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
         z = z ^ (z >> np.uint64(31))

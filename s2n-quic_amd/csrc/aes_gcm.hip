@@ -216,21 +216,16 @@ __device__ __forceinline__ void process_packet(const AesLds &aes, const Ghash &g
 
         const uint32_t c = (uint32_t)(NB * g);
         if ((c >> 8) != pg.page) pg.build(aes, rk, p.n0, p.n1, p.n2, c >> 8);
+#ifdef QPP_AES_NOPIPE
         ctr_keystream<NR, NB>(aes, pg, rk, c, ks);
+#else
+        ctr_keystream_pipe<NR, NB>(aes, pg, rk, c, ks);  // +3-4 % over the scheduler's own order
+#endif
 #ifndef QPP_LEAN
         // GHASH of the previous group (independent of the keystream just issued)
 #pragma unroll
-        for (int j = 0; j < NB; j++) {
-#ifdef QPP_GHASH_SELECT
-            // unconditional product + select: the steps stay in the keystream's basic block (no branch), so the
-            // scheduler can interleave their LDS reads with the AES rounds; invalid slots (counter 0/1 of group 0,
-            // past the last block) compute a product that is discarded
-            const uint4 zn = gh.mulx(z, cprev[j]);
-            if (bprev + j >= 0 && bprev + j < nblk) z = zn;
-#else
+        for (int j = 0; j < NB; j++)
             if (bprev + j >= 0 && bprev + j < nblk) z = gh.mulx(z, cprev[j]);
-#endif
-        }
         if (g == 0) ek0 = ks[1];
 #endif
         const int b0 = NB * g - 2;  // data block of slot 0

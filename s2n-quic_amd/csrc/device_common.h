@@ -176,6 +176,58 @@ __device__ __forceinline__ void ctr_keystream(const AesLds &a, const CtrPage &pg
     for (int j = 0; j < NB; j++) ks[j] = a.final(s[j], rk + 4 * NR);
 }
 
+// The same keystream, software-pipelined by hand.  Left to itself the scheduler issues 2-8 T-table reads and then
+// waits for them (lgkmcnt 0..4 every few instructions): each wave has little LDS work in flight and the SIMD idles
+// whenever both of its waves wait.  Here the rounds 3..NR of the NB blocks are cut into "units" (round r, block j,
+// column c: 4 lookups + the column's combine), ordered column-major over the blocks, and the lookups of unit t + D
+// are issued before unit t is combined (D = NB - 1: unit t + NB is the first that needs the round unit t finishes).
+// So 4 (NB - 1) = 12 reads stay in flight (lgkmcnt(12) before each combine; the counter holds 15), and
+// sched_barrier(0) pins that order against the scheduler's clustering.
+template <int NR, int NB>
+__device__ __forceinline__ void ctr_keystream_pipe(const AesLds &a, const CtrPage &pg, const uint32_t *__restrict__ rk,
+                                                   uint32_t c0, uint4 (&ks)[NB]) {
+    static_assert(NB >= 2 && NB <= 4, "pipeline depth NB - 1 lookups groups of 4 within the 15-read counter");
+    constexpr int D = NB - 1;
+    constexpr int U = (NR - 2) * 4 * NB;  // units of rounds 3..NR
+    uint32_t st[2][NB][4];                 // round states, ping-pong by round parity
+    uint32_t ld[D + 1][4];                 // lookups of the units in flight (ring)
+    uint32_t out[NB][4];
+#pragma unroll
+    for (int j = 0; j < NB; j++) pg.two_rounds(a, c0 + j, st[0][j]);  // round-2 state (round 2 is even)
+    auto issue = [&](const int u) {
+        const int r = 3 + u / (4 * NB), c = (u / NB) & 3, j = u % NB;
+        const uint32_t *s = st[(r - 1) & 1][j];
+        uint32_t *l = ld[u % (D + 1)];
+        l[0] = a.t0<0>(s[c]);
+        l[1] = a.t1<1>(s[(c + 1) & 3]);
+        l[2] = a.t0<2>(s[(c + 2) & 3]);
+        l[3] = a.t1<3>(s[(c + 3) & 3]);
+    };
+    auto combine = [&](const int u) {
+        const int r = 3 + u / (4 * NB), c = (u / NB) & 3, j = u % NB;
+        const uint32_t *l = ld[u % (D + 1)];
+        const uint32_t k = rk[4 * r + c];
+        if (r < NR) {
+            st[r & 1][j][c] = xor3(l[0], l[1], k) ^ rotl16(l[2] ^ l[3]);
+        } else {  // final round: S-box bytes only (AesLds::last)
+            const uint32_t lo = __builtin_amdgcn_perm(l[1], l[0], 0x0c0c0601u);
+            const uint32_t hi = __builtin_amdgcn_perm(l[3], l[2], 0x07020c0cu);
+            out[j][c] = xor3(lo, hi, k);
+        }
+    };
+#pragma unroll
+    for (int u = 0; u < D; u++) issue(u);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        if (u + D < U) issue(u + D);
+        __builtin_amdgcn_sched_barrier(0);
+        combine(u);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int j = 0; j < NB; j++) ks[j] = make_uint4(out[j][0], out[j][1], out[j][2], out[j][3]);
+}
+
 // AES T0/T1 bank-replicated tables for the AesLds view: row x = 256 B, dword slot 0..31 = T0[x], 32..63 =
 // T1[x] = rotl8 T0[x].  Thread t owns S-box value x = t % 256 (one S-box load) and writes its row's slots in an
 // order rotated by x, so a wave's 64 stores of one step go to 32 distinct banks per 32-lane group.  Needs

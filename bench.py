@@ -384,8 +384,7 @@ def e2e(args, rank, world, local_rank):
         nonlocal keys, slots
         if args.rotate:
             new = ctx.update_keys(keys)
-            for k in keys:
-                k.free()
+            ctx.free_keys(keys)
             keys = new
             slots = np.array([k.slot for k in keys], dtype=np.uint32)
             descs["key_idx"] = slots[conn]

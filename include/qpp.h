@@ -96,6 +96,9 @@ int qpp_key_update(const qpp_key *key, qpp_key **out);
 int qpp_key_update_batch(qpp_key *const *keys, size_t n, qpp_key **out);
 /* Zeroizes host and device copies (cipher_suite.rs:106-114,189-193); stream-ordered (see Asynchrony above). */
 void qpp_key_free(qpp_key *key);
+/* qpp_key_free over n keys (the old keys of a KeySet rotation across many connections, keyset.rs:94-96); the device
+ * records are zeroized by one pass per run of consecutive slots.  NULL entries are skipped. */
+void qpp_key_free_batch(qpp_key *const *keys, size_t n);
 /* Index of this key in its context's device key table: the value to put in qpp_pkt.key_idx. */
 uint32_t qpp_key_slot(const qpp_key *key);
 int qpp_key_suite(const qpp_key *key);

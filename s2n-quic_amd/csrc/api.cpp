@@ -857,6 +857,11 @@ void qpp_key_free(qpp_key *key) {
     delete key;
 }
 
+void qpp_key_free_batch(qpp_key *const *keys, size_t n) {
+    if (!keys) return;
+    for (size_t i = 0; i < n; i++) qpp_key_free(keys[i]);  // retirements only collect; one flush before the next use
+}
+
 uint32_t qpp_key_slot(const qpp_key *key) { return key ? key->slot : UINT32_MAX; }
 int qpp_key_suite(const qpp_key *key) { return key ? key->suite : 0; }
 size_t qpp_tag_len(const qpp_key *) { return 16; }

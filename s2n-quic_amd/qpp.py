@@ -44,7 +44,7 @@ assert RX_DTYPE.itemsize == 24
 # every symbol include/qpp.h declares (tests/test_abi.py checks the library exports them all)
 EXPORTS = [
     "qpp_abi_version", "qpp_ctx_create", "qpp_ctx_destroy", "qpp_ctx_stream", "qpp_ctx_synchronize",
-    "qpp_ctx_last_error", "qpp_key_new", "qpp_key_new_raw", "qpp_key_update", "qpp_key_free", "qpp_key_slot",
+    "qpp_ctx_last_error", "qpp_key_new", "qpp_key_new_raw", "qpp_key_update", "qpp_key_free", "qpp_key_free_batch", "qpp_key_slot",
     "qpp_key_suite", "qpp_tag_len", "qpp_sample_len", "qpp_confidentiality_limit", "qpp_integrity_limit",
     "qpp_key_material", "qpp_initial_keys", "qpp_seal", "qpp_seal_scatter", "qpp_open", "qpp_hp_mask",
     "qpp_seal_batch", "qpp_open_batch", "qpp_hp_mask_batch", "qpp_dev_alloc", "qpp_dev_free", "qpp_host_alloc",
@@ -94,6 +94,7 @@ def lib():
             "qpp_key_new_raw": (ctypes.c_int, [vp, ctypes.c_int, vp, sz, vp, vp, sz, ctypes.POINTER(vp)]),
             "qpp_key_update": (ctypes.c_int, [vp, ctypes.POINTER(vp)]),
             "qpp_key_free": (None, [vp]),
+            "qpp_key_free_batch": (None, [vp, sz]),
             "qpp_key_slot": (u32, [vp]),
             "qpp_key_suite": (ctypes.c_int, [vp]),
             "qpp_tag_len": (sz, [vp]),
@@ -273,6 +274,14 @@ class Context:
         if rc != OK:
             raise QppError(rc, "qpp_key_update_batch")
         return [Key(self, arr[i]) for i in range(n)]
+
+    def free_keys(self, keys):
+        """qpp_key_free_batch: frees every key of the list (the old keys of a rotation) in one call."""
+        live = [k for k in keys if k.handle]
+        arr = (vp * max(len(live), 1))(*[k.handle for k in live])
+        lib().qpp_key_free_batch(arr, len(live))
+        for k in live:
+            k.handle = None
 
     def key_slots(self):
         """(capacity, high-water slot, retired-not-yet-reusable) of the device key table."""

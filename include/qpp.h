@@ -67,6 +67,14 @@ int qpp_ctx_synchronize(qpp_ctx *ctx);
  * (latency: a 64-packet GSO burst); larger ones one lane per packet (throughput).  ChaCha20-Poly1305 batches switch
  * at max_packets / 4.  0 = always lane per packet.  Outputs are identical either way. */
 int qpp_ctx_set_burst_max(qpp_ctx *ctx, size_t max_packets);
+/* AES-GCM batches larger than burst_max: the lane kernel (one key per 1024-packet workgroup) serves batches with at
+ * least 1024 packets per live AES key, the wave-item kernel (one key per 64-packet wave) batches with fewer (many
+ * keys, few packets each: key-update churn).  This forces one of them (env QPP_AES_KERNEL=lane|wave); outputs are
+ * identical. */
+#define QPP_AES_KERNEL_AUTO 0
+#define QPP_AES_KERNEL_LANE 1
+#define QPP_AES_KERNEL_WAVE 2
+int qpp_ctx_set_aes_kernel(qpp_ctx *ctx, int kernel);
 int qpp_abi_version(void);
 /* Key-table occupancy (diagnostics / tests): slots allocated, high-water slot index, slots retired but not yet
  * reusable (their zeroization is still behind in-flight batches). */

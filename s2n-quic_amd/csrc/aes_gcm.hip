@@ -128,8 +128,68 @@ __device__ void build_tables(const DevKey *__restrict__ key) {
     __syncthreads();
 }
 
+// ---------------------------------------------------------------- GHASH with per-wave 4-bit tables (many keys)
+// X * H = xor_b (Thi_b[x_b >> 4] ^ Tlo_b[x_b & 15]): 32 reads of 16 B per product instead of 16, but the tables of
+// one key are 8 KiB, so each of the 8 waves of a workgroup holds its own key's tables in [0, 64 KiB): wave w at
+// w * 8 KiB, high-nibble table at +0, low-nibble table at +4 KiB, entry (b, n) at n * 256 + b * 16.  That is the
+// byte layout of Ghash with a 16-entry "x", so the same lane rotation keeps every ds_read_b128 conflict-free and
+// the address is still ONE v_perm: the nibbles are split into bytes whose upper nibble carries (wave, half), i.e.
+// address bits 12-15.
+struct Ghash4 {
+    Ghash g;            // lane rotation, per-lane selectors (byte positions)
+    uint32_t hi_or, lo_or;  // 0x10101010 * (2 wave + half): the upper nibble of every split byte
+    __device__ __forceinline__ static Ghash4 make(uint32_t wave) {
+        Ghash4 h;
+        h.g = Ghash::make();
+        h.hi_or = 0x01010101u * ((2u * wave + 0u) << 4);
+        h.lo_or = 0x01010101u * ((2u * wave + 1u) << 4);
+        return h;
+    }
+    __device__ __forceinline__ uint4 rot(uint4 z) const { return g.rot(z); }
+    template <int K, int I>
+    __device__ __forceinline__ uint4 look(uint32_t wk) const {
+        return lds_ld128(kLdsGhash + __builtin_amdgcn_perm(wk, g.lc[K], g.sel[I]));
+    }
+    template <int K>
+    __device__ __forceinline__ uint4 word(uint32_t wk) const {  // the 8 reads of word K of W
+        const uint32_t h = __builtin_amdgcn_bitop3_b32(wk >> 4, 0x0f0f0f0fu, hi_or, 0xea);  // (a & b) | c
+        const uint32_t l = __builtin_amdgcn_bitop3_b32(wk, 0x0f0f0f0fu, lo_or, 0xea);
+        return xor3(xor3(look<K, 0>(h), look<K, 1>(h), look<K, 2>(h)), xor3(look<K, 3>(h), look<K, 0>(l), look<K, 1>(l)),
+                    look<K, 2>(l) ^ look<K, 3>(l));
+    }
+    __device__ __forceinline__ uint4 prod(const uint4 &w, uint4 c) const {
+        return xor3(xor3(word<0>(w.x), word<1>(w.y), c), word<2>(w.z), word<3>(w.w));
+    }
+    __device__ __forceinline__ uint4 mulx(const uint4 &w, uint4 c) const { return rot(prod(w, c)); }
+};
+
+// The calling wave's Ghash4 tables for `key` (from its V[m] = H * x^m): lane l fills byte b = l >> 2, half
+// h = (l >> 1) & 1, nibbles n = 8 (l & 1) .. + 7; T[n] = xor of V[8 b + 4 h + i] over the set bits (bit 3 - i) of n.
+// Ends with a wave-level LDS sync (the caller must have synced before overwriting a previous key's tables).
+__device__ __forceinline__ void build_gh4(const DevKey *__restrict__ key, uint32_t wave, uint32_t lane) {
+    const uint32_t b = lane >> 2, h = (lane >> 1) & 1u, n0 = 8u * (lane & 1u);
+    uint4 v[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const uint32_t *p = key->V[8 * b + 4 * h + i];
+        v[i] = make_uint4(p[0], p[1], p[2], p[3]);
+    }
+    const uint32_t base = kLdsGhash + wave * 8192u + h * 4096u + b * 16u;
+#pragma unroll
+    for (uint32_t k = 0; k < 8; k++) {
+        const uint32_t n = n0 + k;
+        uint4 e = make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+            if ((n >> (3 - i)) & 1u) e = e ^ v[i];
+        lds_st128(base + n * 256u, e);
+    }
+    wave_lds_sync();
+}
+
 // GHASH over the AAD (zero-padded to 16 bytes), as the pending (rotated) Z of the chain.
-__device__ __forceinline__ uint4 ghash_aad_w(const Ghash &gh, const uint8_t *aad, uint32_t aad_len) {
+template <typename GH>
+__device__ __forceinline__ uint4 ghash_aad_w(const GH &gh, const uint8_t *aad, uint32_t aad_len) {
     uint4 w = make_uint4(0, 0, 0, 0);
     for (uint32_t off = 0; off < aad_len; off += 16) {
         uint4 a = ld16(aad + off);
@@ -147,8 +207,8 @@ __device__ __forceinline__ uint4 ghash_aad_w(const Ghash &gh, const uint8_t *aad
 //   counter b + 2: data block b.
 // The GHASH steps of group g-1 are issued in the same basic block as the keystream of group g, so the two
 // independent dependency chains overlap.
-template <int NR, int NB, bool SEAL>
-__device__ __forceinline__ void process_packet(const AesLds &aes, const Ghash &gh, const Stage<NB> &st,
+template <int NR, int NB, bool SEAL, typename GH>
+__device__ __forceinline__ void process_packet(const AesLds &aes, const GH &gh, const Stage<NB> &st,
                                                const DevKey *__restrict__ key, const uint32_t *__restrict__ rk,
                                                bool has, const qpp_pkt &d, uint32_t pkt_index, uint8_t *arena,
                                                uint8_t *masks, int8_t *status, uint32_t flags) {
@@ -340,6 +400,45 @@ __global__ __launch_bounds__(WG) void aes_gcm_kernel(const DevKey *__restrict__ 
     }
 }
 
+// Many keys, few packets per key (key churn, a chunk of a host batch): work items of <= 64 packets of one key (a
+// wave), each wave with its own key's Ghash4 tables and round keys, the AES T-tables shared by the workgroup.  A
+// workgroup loops over items (grid-stride over waves), so every lane has a packet whenever its key has >= 64 packets
+// in the batch (aes_gcm_kernel needs 1024 per workgroup).
+template <bool SEAL, int NB, int NR>
+__global__ __launch_bounds__(512) void aes_gcm_wave_kernel(const DevKey *__restrict__ keys,
+                                                           const qpp_pkt *__restrict__ descs,
+                                                           const uint32_t *__restrict__ perm,
+                                                           const WorkItem *__restrict__ work,
+                                                           const uint32_t *__restrict__ n_work,
+                                                           uint8_t *__restrict__ arena, uint8_t *masks, int8_t *status,
+                                                           uint32_t flags) {
+    const uint32_t nw = *n_work;
+    if (blockIdx.x * 8u >= nw) return;  // uniform
+    build_aes_tables(kLdsAes);
+    __syncthreads();
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const AesLds aes = make_aes(kLdsAes);
+    const Ghash4 gh = Ghash4::make(wave);
+    Stage<NB> st;
+    st.lane = lane;
+    st.base = kLdsStage + wave * (64u * 16u * NB);
+    for (uint32_t it = blockIdx.x * 8u + wave; it < nw; it += gridDim.x * 8u) {  // wave-uniform
+        const WorkItem w = work[it];
+        if (w.nr != NR) continue;  // the other AES size's launch serves it
+        const DevKey *__restrict__ key = keys + w.key;
+        build_gh4(key, wave, lane);
+        uint32_t rk[4 * (NR + 1)];
+#pragma unroll
+        for (int i = 0; i < 4 * (NR + 1); i++) rk[i] = __builtin_amdgcn_readfirstlane(key->rk[i]);
+        const bool real = lane < w.count;
+        const uint32_t pi = real ? perm[w.begin + lane] : perm[w.begin];
+        const qpp_pkt d = descs[pi];
+        const bool has = real && !(d.flags & QPP_PKT_SKIP);
+        process_packet<NR, NB, SEAL>(aes, gh, st, key, rk, has, d, pi, arena, masks, status, flags);
+        wave_lds_sync();  // the next item rebuilds this wave's tables
+    }
+}
+
 // ---------------------------------------------------------------- key setup: H = E_K(0), V[m] = H * x^m
 __device__ void aes_bytewise(const uint32_t *rk, int nr, uint8_t s[16]) {
     auto rkb = [rk](int i) { return (uint8_t)(rk[i >> 2] >> (8 * (i & 3))); };
@@ -456,6 +555,31 @@ uint32_t aes_packets_per_item(uint32_t n, uint32_t n_cu) {
     per = (per + 63) & ~uint64_t(63);
     if (per < (uint64_t)kMinPacketsPerItem) per = kMinPacketsPerItem;
     return per > full ? full : (uint32_t)per;
+}
+
+hipError_t launch_aes_gcm_wave(bool seal, const DevKey *keys, const qpp_pkt *descs, const PlanBuffers &pb, uint32_t n,
+                               uint32_t key_cap, uint32_t n_cu, uint8_t *arena, uint8_t *masks, int8_t *status,
+                               uint32_t flags, uint32_t suites, hipStream_t s) {
+    if (!n) return hipSuccess;
+    // one 160-KiB workgroup per CU: a grid of 2 rounds of the chip (the second round's workgroups start as the
+    // first finish), each wave looping over the work items
+    const uint32_t items = plan_max_work(n, key_cap, kWavePacketsPerItem);
+    const uint32_t wgs = (items + 7) / 8;
+    const dim3 grid(wgs < 2 * n_cu ? wgs : 2 * n_cu), block(512);
+    const uint32_t lds = kLdsMax;
+#define QPP_WAVE_LAUNCH(S, NR)                                                                                  \
+    hipLaunchKernelGGL((aes_gcm_wave_kernel<S, 4, NR>), grid, block, lds, s, keys, descs, pb.perm, pb.work,      \
+                       pb.n_work, arena, masks, status, flags)
+    if (suites & (1u << QPP_SUITE_TLS_AES_128_GCM_SHA256)) {
+        if (seal) QPP_WAVE_LAUNCH(true, 10);
+        else QPP_WAVE_LAUNCH(false, 10);
+    }
+    if (suites & (1u << QPP_SUITE_TLS_AES_256_GCM_SHA384)) {
+        if (seal) QPP_WAVE_LAUNCH(true, 14);
+        else QPP_WAVE_LAUNCH(false, 14);
+    }
+#undef QPP_WAVE_LAUNCH
+    return hipGetLastError();
 }
 
 hipError_t launch_aes_gcm(bool seal, const DevKey *keys, const qpp_pkt *descs, const PlanBuffers &pb, uint32_t n,

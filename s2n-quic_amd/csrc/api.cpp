@@ -15,6 +15,7 @@
 //     device records, and one
 //     "retired" event marks them; the slots are reused only once that completed.  (A rotation of 4096 keys used to
 //     cost 4096 memset launches.)
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -69,6 +70,7 @@ struct qpp_ctx {
     int device = 0;
     uint32_t n_cu = 0;  // compute units (AES work-item sizing)
     uint32_t burst_max = kBurstMaxDefault;  // AES batches up to this size take the wave-per-packet kernel
+    int aes_kernel = 0;  // QPP_AES_KERNEL_*: 0 = chosen per batch (aes_path)
     hipStream_t stream = nullptr;
     hipStream_t kstream = nullptr;  // key installs / derivations
     hipStream_t rstream = nullptr;  // key retirements (zeroization behind in-flight batches)
@@ -429,18 +431,48 @@ uint32_t suite_mask(const qpp_ctx *ctx) {
     return m;
 }
 
+// Which AES-GCM kernel serves an n-packet batch: the wave-per-packet burst kernel for small batches; the lane kernel
+// (one key per 1024-packet workgroup, 8-bit GHASH tables) when the batch has >= kWaveKernelPacketsPerKey packets per
+// live AES key; else the wave-item kernel (one key per 64-packet wave, 4-bit tables).  QPP_AES_KERNEL=lane|wave
+// forces one of the two throughput kernels (A/B).
+enum class AesPath { burst, lane, wave };
+AesPath aes_path(const qpp_ctx *ctx, uint32_t n) {
+    if (n <= ctx->burst_max) return AesPath::burst;
+    if (ctx->aes_kernel) return ctx->aes_kernel == QPP_AES_KERNEL_LANE ? AesPath::lane : AesPath::wave;
+    const uint64_t aes_keys = (uint64_t)ctx->live_by_suite[QPP_SUITE_TLS_AES_128_GCM_SHA256] +
+                              ctx->live_by_suite[QPP_SUITE_TLS_AES_256_GCM_SHA384];
+    return (uint64_t)n < kWaveKernelPacketsPerKey * aes_keys ? AesPath::wave : AesPath::lane;
+}
+uint32_t aes_per_item(const qpp_ctx *ctx, AesPath p, uint32_t n) {
+    return p == AesPath::burst ? burst_packets_per_item(n, ctx->n_cu)
+           : p == AesPath::wave ? kWavePacketsPerItem
+                                : aes_packets_per_item(n, ctx->n_cu);
+}
+hipError_t launch_aes(const qpp_ctx *ctx, AesPath p, bool seal, const qpp_pkt *descs, const PlanBuffers &pb, uint32_t n,
+                      uint8_t *arena, uint8_t *masks, int8_t *status, uint32_t flags, hipStream_t s) {
+    const uint32_t per = aes_per_item(ctx, p, n);
+    switch (p) {
+        case AesPath::burst:
+            return launch_aes_gcm_burst(seal, ctx->d_keys, descs, pb, n, ctx->key_cap, per, arena, masks, status, flags,
+                                        suite_mask(ctx), s);
+        case AesPath::wave:
+            return launch_aes_gcm_wave(seal, ctx->d_keys, descs, pb, n, ctx->key_cap, ctx->n_cu, arena, masks, status,
+                                       flags, suite_mask(ctx), s);
+        default:
+            return launch_aes_gcm(seal, ctx->d_keys, descs, pb, n, ctx->key_cap, per, arena, masks, status, flags,
+                                  suite_mask(ctx), s);
+    }
+}
+
 // Batch bodies: plan (AES) + kernels on st's stream; keys already flushed.
 int enqueue_seal(qpp_ctx *ctx, StreamState *st, const qpp_pkt *descs, uint32_t n, uint8_t *arena, uint8_t *masks,
                  int8_t *status, uint32_t flags) {
     hipStream_t s = st->stream;
     if (!(flags & QPP_ONLY_CHACHA) && (suite_mask(ctx) & kAesSuites)) {
         RC_TRY(ensure_plan(ctx, st, n));
-        const bool burst = n <= ctx->burst_max;
-        const uint32_t per = burst ? burst_packets_per_item(n, ctx->n_cu) : aes_packets_per_item(n, ctx->n_cu);
-        HIP_TRY(ctx, launch_plan(ctx->d_keys, ctx->key_cap, descs, n, st->plan, per, s));
-        HIP_TRY(ctx, (burst ? launch_aes_gcm_burst : launch_aes_gcm)(true, ctx->d_keys, descs, st->plan, n,
-                                                                    ctx->key_cap, per, arena, masks, status, flags,
-                                                                    suite_mask(ctx), s));
+        const AesPath path = aes_path(ctx, n);
+        HIP_TRY(ctx, launch_plan(ctx->d_keys, ctx->key_cap, descs, n, st->plan, aes_per_item(ctx, path, n), s));
+        HIP_TRY(ctx, launch_aes(ctx, path, true, descs, st->plan, n, arena, masks, status, flags, s));
     }
     if (!(flags & QPP_ONLY_AES))
         HIP_TRY(ctx, launch_chacha(true, ctx->d_keys, ctx->key_cap, descs, n, arena, masks, status, flags,
@@ -453,12 +485,9 @@ int enqueue_open(qpp_ctx *ctx, StreamState *st, const qpp_pkt *descs, uint32_t n
     hipStream_t s = st->stream;
     if (!(flags & QPP_ONLY_CHACHA) && (suite_mask(ctx) & kAesSuites)) {
         RC_TRY(ensure_plan(ctx, st, n));
-        const bool burst = n <= ctx->burst_max;
-        const uint32_t per = burst ? burst_packets_per_item(n, ctx->n_cu) : aes_packets_per_item(n, ctx->n_cu);
-        HIP_TRY(ctx, launch_plan(ctx->d_keys, ctx->key_cap, descs, n, st->plan, per, s));
-        HIP_TRY(ctx, (burst ? launch_aes_gcm_burst : launch_aes_gcm)(false, ctx->d_keys, descs, st->plan, n,
-                                                                    ctx->key_cap, per, arena, nullptr, status, 0,
-                                                                    suite_mask(ctx), s));
+        const AesPath path = aes_path(ctx, n);
+        HIP_TRY(ctx, launch_plan(ctx->d_keys, ctx->key_cap, descs, n, st->plan, aes_per_item(ctx, path, n), s));
+        HIP_TRY(ctx, launch_aes(ctx, path, false, descs, st->plan, n, arena, nullptr, status, 0, s));
     }
     if (!(flags & QPP_ONLY_AES))
         HIP_TRY(ctx, launch_chacha(false, ctx->d_keys, ctx->key_cap, descs, n, arena, nullptr, status, 0,
@@ -652,6 +681,8 @@ int qpp_ctx_create(int device, qpp_ctx **out) {
     ctx->device = device;
     ctx->n_cu = (uint32_t)prop.multiProcessorCount;
     if (const char *e = getenv("QPP_BURST_MAX")) ctx->burst_max = (uint32_t)strtoul(e, nullptr, 10);
+    if (const char *e = getenv("QPP_AES_KERNEL"))
+        ctx->aes_kernel = !strcmp(e, "lane") ? QPP_AES_KERNEL_LANE : !strcmp(e, "wave") ? QPP_AES_KERNEL_WAVE : 0;
     int rc = QPP_OK;
     do {
         if (fail(ctx, hipSetDevice(device), "hipSetDevice")) { rc = QPP_DEVICE_ERROR; break; }
@@ -670,6 +701,12 @@ int qpp_ctx_create(int device, qpp_ctx **out) {
         return rc;
     }
     *out = ctx;
+    return QPP_OK;
+}
+
+int qpp_ctx_set_aes_kernel(qpp_ctx *ctx, int kernel) {
+    if (!ctx || kernel < QPP_AES_KERNEL_AUTO || kernel > QPP_AES_KERNEL_WAVE) return QPP_INTERNAL_ERROR;
+    ctx->aes_kernel = kernel;
     return QPP_OK;
 }
 

@@ -1,6 +1,8 @@
 // device_common.h — device-side building blocks shared by the packet-protection kernels (gfx950).
 #pragma once
 
+#include <utility>
+
 #include "qpp_internal.h"
 
 namespace qpp {
@@ -183,19 +185,31 @@ __device__ __forceinline__ void ctr_keystream(const AesLds &a, const CtrPage &pg
 // are issued before unit t is combined (D = NB - 1: unit t + NB is the first that needs the round unit t finishes).
 // So 4 (NB - 1) = 12 reads stay in flight (lgkmcnt(12) before each combine; the counter holds 15), and
 // sched_barrier(0) pins that order against the scheduler's clustering.
+template <typename F, int... Is>
+__device__ __forceinline__ void static_for_impl(F &&f, std::integer_sequence<int, Is...>) {
+    (f(std::integral_constant<int, Is>{}), ...);
+}
+// f(integral_constant<int, i>) for i = 0 .. N-1 with every index a compile-time constant: a #pragma unroll loop of
+// 192 steps (AES-256) is not unrolled by the compiler, and its state arrays then live in scratch memory
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F &&f) {
+    static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
 template <int NR, int NB>
 __device__ __forceinline__ void ctr_keystream_pipe(const AesLds &a, const CtrPage &pg, const uint32_t *__restrict__ rk,
                                                    uint32_t c0, uint4 (&ks)[NB]) {
     static_assert(NB >= 2 && NB <= 4, "pipeline depth NB - 1 lookups groups of 4 within the 15-read counter");
     constexpr int D = NB - 1;
     constexpr int U = (NR - 2) * 4 * NB;  // units of rounds 3..NR
-    uint32_t st[2][NB][4];                 // round states, ping-pong by round parity
-    uint32_t ld[D + 1][4];                 // lookups of the units in flight (ring)
-    uint32_t out[NB][4];
+    // round states by parity; the final round writes into the parity buffer of round NR - 2, dead by then
+    uint32_t st[2][NB][4];
+    uint32_t ld[D + 1][4];  // lookups of the units in flight (ring)
 #pragma unroll
     for (int j = 0; j < NB; j++) pg.two_rounds(a, c0 + j, st[0][j]);  // round-2 state (round 2 is even)
-    auto issue = [&](const int u) {
-        const int r = 3 + u / (4 * NB), c = (u / NB) & 3, j = u % NB;
+    auto issue = [&](auto uc) {
+        constexpr int u = decltype(uc)::value;
+        constexpr int r = 3 + u / (4 * NB), c = (u / NB) & 3, j = u % NB;
         const uint32_t *s = st[(r - 1) & 1][j];
         uint32_t *l = ld[u % (D + 1)];
         l[0] = a.t0<0>(s[c]);
@@ -203,29 +217,29 @@ __device__ __forceinline__ void ctr_keystream_pipe(const AesLds &a, const CtrPag
         l[2] = a.t0<2>(s[(c + 2) & 3]);
         l[3] = a.t1<3>(s[(c + 3) & 3]);
     };
-    auto combine = [&](const int u) {
-        const int r = 3 + u / (4 * NB), c = (u / NB) & 3, j = u % NB;
+    auto combine = [&](auto uc) {
+        constexpr int u = decltype(uc)::value;
+        constexpr int r = 3 + u / (4 * NB), c = (u / NB) & 3, j = u % NB;
         const uint32_t *l = ld[u % (D + 1)];
         const uint32_t k = rk[4 * r + c];
-        if (r < NR) {
+        if constexpr (r < NR) {
             st[r & 1][j][c] = xor3(l[0], l[1], k) ^ rotl16(l[2] ^ l[3]);
         } else {  // final round: S-box bytes only (AesLds::last)
             const uint32_t lo = __builtin_amdgcn_perm(l[1], l[0], 0x0c0c0601u);
             const uint32_t hi = __builtin_amdgcn_perm(l[3], l[2], 0x07020c0cu);
-            out[j][c] = xor3(lo, hi, k);
+            st[NR & 1][j][c] = xor3(lo, hi, k);
         }
     };
-#pragma unroll
-    for (int u = 0; u < D; u++) issue(u);
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-        if (u + D < U) issue(u + D);
+    static_for<D>([&](auto uc) { issue(uc); });
+    static_for<U>([&](auto uc) {
+        constexpr int u = decltype(uc)::value;
+        if constexpr (u + D < U) issue(std::integral_constant<int, u + D>{});
         __builtin_amdgcn_sched_barrier(0);
-        combine(u);
+        combine(uc);
         __builtin_amdgcn_sched_barrier(0);
-    }
+    });
 #pragma unroll
-    for (int j = 0; j < NB; j++) ks[j] = make_uint4(out[j][0], out[j][1], out[j][2], out[j][3]);
+    for (int j = 0; j < NB; j++) ks[j] = make_uint4(st[NR & 1][j][0], st[NR & 1][j][1], st[NR & 1][j][2], st[NR & 1][j][3]);
 }
 
 // AES T0/T1 bank-replicated tables for the AesLds view: row x = 256 B, dword slot 0..31 = T0[x], 32..63 =

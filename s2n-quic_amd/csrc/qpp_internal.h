@@ -86,7 +86,9 @@ struct WorkItem {
     uint32_t nr;     // AES rounds for this key
 };
 
-constexpr int kMinPacketsPerItem = 4;    // smallest AES work item: burst kernel, one packet per wave (plan scratch)
+constexpr int kMinPacketsPerItem = 4;
+constexpr uint32_t kWavePacketsPerItem = 64;  // aes_gcm_wave_kernel: one wave, one key, <= 64 packets per work item
+constexpr uint32_t kWaveKernelPacketsPerKey = 1024;  // batches with fewer packets per live AES key take the wave kernel    // smallest AES work item: burst kernel, one packet per wave (plan scratch)
 constexpr uint32_t kBurstMaxDefault = 16384;  // AES batches up to this many packets run one wave per packet
 constexpr uint32_t kChachaBurstShift = 2;     // ChaCha20-Poly1305 batches up to burst_max >> 2 do (its lane kernel
                                               // fills the chip with fewer packets: crossover ~6 Ki vs ~20 Ki)
@@ -128,6 +130,10 @@ hipError_t launch_aes_gcm_burst(bool seal, const DevKey *keys, const qpp_pkt *de
 hipError_t launch_aes_gcm(bool seal, const DevKey *keys, const qpp_pkt *descs, const PlanBuffers &pb, uint32_t n,
                           uint32_t key_cap, uint32_t per, uint8_t *arena, uint8_t *masks, int8_t *status,
                           uint32_t flags, uint32_t suites, hipStream_t s);
+// many keys: work items of <= kWavePacketsPerItem packets (plan with per = kWavePacketsPerItem), one wave each
+hipError_t launch_aes_gcm_wave(bool seal, const DevKey *keys, const qpp_pkt *descs, const PlanBuffers &pb, uint32_t n,
+                               uint32_t key_cap, uint32_t n_cu, uint8_t *arena, uint8_t *masks, int8_t *status,
+                               uint32_t flags, uint32_t suites, hipStream_t s);
 // burst: one wave per packet (small batches) instead of one lane per packet
 // key_cap: slots in the key table; a packet naming a slot >= key_cap is never dereferenced (status INTERNAL_ERROR)
 hipError_t launch_chacha(bool seal, const DevKey *keys, uint32_t key_cap, const qpp_pkt *descs, uint32_t n,

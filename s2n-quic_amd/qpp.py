@@ -28,6 +28,7 @@ HASH_LEN = {1: 32, 2: 48, 3: 32}
 OK, DECODE_ERROR, DECRYPT_ERROR, INTERNAL_ERROR, UNSUPPORTED, DEVICE_ERROR = 0, 1, 2, 3, 4, 5
 ROTATION_NOT_SUPPORTED = 6  # dc open::Error::RotationNotSupported
 HP_MASK_OUT, HP_APPLY, ONLY_AES, ONLY_CHACHA = 0x1, 0x2, 0x10, 0x20
+AES_KERNEL_AUTO, AES_KERNEL_LANE, AES_KERNEL_WAVE = 0, 1, 2
 ENDPOINT_CLIENT, ENDPOINT_SERVER = 0, 1
 
 # qpp_pkt (24 bytes) as a numpy structured dtype
@@ -44,7 +45,7 @@ assert RX_DTYPE.itemsize == 24
 # every symbol include/qpp.h declares (tests/test_abi.py checks the library exports them all)
 EXPORTS = [
     "qpp_abi_version", "qpp_ctx_create", "qpp_ctx_destroy", "qpp_ctx_stream", "qpp_ctx_synchronize",
-    "qpp_ctx_last_error", "qpp_key_new", "qpp_key_new_raw", "qpp_key_update", "qpp_key_free", "qpp_key_free_batch", "qpp_key_slot",
+    "qpp_ctx_last_error", "qpp_key_new", "qpp_key_new_raw", "qpp_key_update", "qpp_key_free", "qpp_key_free_batch", "qpp_ctx_set_aes_kernel", "qpp_key_slot",
     "qpp_key_suite", "qpp_tag_len", "qpp_sample_len", "qpp_confidentiality_limit", "qpp_integrity_limit",
     "qpp_key_material", "qpp_initial_keys", "qpp_seal", "qpp_seal_scatter", "qpp_open", "qpp_hp_mask",
     "qpp_seal_batch", "qpp_open_batch", "qpp_hp_mask_batch", "qpp_dev_alloc", "qpp_dev_free", "qpp_host_alloc",
@@ -95,6 +96,7 @@ def lib():
             "qpp_key_update": (ctypes.c_int, [vp, ctypes.POINTER(vp)]),
             "qpp_key_free": (None, [vp]),
             "qpp_key_free_batch": (None, [vp, sz]),
+            "qpp_ctx_set_aes_kernel": (ctypes.c_int, [vp, ctypes.c_int]),
             "qpp_key_slot": (u32, [vp]),
             "qpp_key_suite": (ctypes.c_int, [vp]),
             "qpp_tag_len": (sz, [vp]),
@@ -233,6 +235,10 @@ class Context:
     def set_burst_max(self, max_packets):
         """AES batches of <= max_packets run one wave per packet (burst kernel); 0 = always lane per packet."""
         self._check(lib().qpp_ctx_set_burst_max(self.handle, int(max_packets)), "set_burst_max")
+
+    def set_aes_kernel(self, kernel):
+        """AES_KERNEL_AUTO / _LANE / _WAVE for batches above burst_max (identical outputs; A/B and tests)."""
+        self._check(lib().qpp_ctx_set_aes_kernel(self.handle, int(kernel)), "set_aes_kernel")
 
     def sync(self, stream=None):
         self._check(lib().qpp_stream_synchronize(self.handle, stream), "sync")

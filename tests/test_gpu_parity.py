@@ -23,12 +23,16 @@ def ctx():
     c.close()
 
 
-@pytest.fixture(params=["burst", "lane"])
+@pytest.fixture(params=["burst", "lane", "wave"])
 def path(request, ctx):
-    """AES-GCM kernel path: wave per packet (small batches) or lane per packet (large); same outputs."""
+    """AES-GCM kernel path: wave per packet (small batches), lane per packet with one key per 1024-packet workgroup,
+    or lane per packet with one key per 64-packet wave (many keys); same outputs."""
     ctx.set_burst_max(1 << 30 if request.param == "burst" else 0)
+    ctx.set_aes_kernel({"burst": qpp.AES_KERNEL_AUTO, "lane": qpp.AES_KERNEL_LANE,
+                        "wave": qpp.AES_KERNEL_WAVE}[request.param])
     yield request.param
     ctx.set_burst_max(16384)
+    ctx.set_aes_kernel(qpp.AES_KERNEL_AUTO)
 
 
 # ------------------------------------------------------------------ RFC 9001 Appendix A through the trait mirror
@@ -335,6 +339,49 @@ def test_full_size_round_trip(ctx, suite):
         b.free()
     for k in keys:
         k.free()
+
+
+@pytest.mark.parametrize("kernel", ["lane", "wave"])
+def test_full_size_many_keys(ctx, kernel):
+    """1 Mi x 1200 B over 4096 AES keys (BASELINE configs[4]'s key count; 2048 AES-128 + 2048 AES-256, ~256 packets
+    per key) through both throughput kernels: a seeded 2000-packet sample is bit-exact against the oracle (ciphertext,
+    tag, mask) and every packet round-trips."""
+    n, pt_len = 1 << 20, 1200
+    rng = np.random.default_rng(77)
+    batch = []
+    for suite in (1, 2):
+        batch += ctx.keys_batch(suite, [rng.integers(0, 256, qpp.HASH_LEN[suite], dtype=np.uint8).tobytes()
+                                        for _ in range(2048)], 1)
+    slots = [k.slot for k in batch]
+    okeys = orc.make_keys([(k.suite, *k.material()) for k in batch])
+    ctx.set_aes_kernel(qpp.AES_KERNEL_LANE if kernel == "lane" else qpp.AES_KERNEL_WAVE)
+    try:
+        descs, arena = qpp.make_batch(n, pt_len, slots, seed=0x5eed0077)
+        d_desc, d_arena, d_mask, d_status = (ctx.alloc(descs.nbytes), ctx.alloc(arena.nbytes), ctx.alloc(5 * n),
+                                             ctx.alloc(n))
+        d_desc.upload(descs)
+        d_arena.upload(arena)
+        ctx.seal_batch(d_desc, n, d_arena, d_mask, d_status, qpp.HP_MASK_OUT)
+        sealed, masks = d_arena.download(), d_mask.download()
+        assert (d_status.download(dtype=np.int8) == 0).all()
+        stride = arena.size // n
+        pick = np.sort(np.random.default_rng(78).choice(n, 2000, replace=False))
+        sub_d = descs[pick].copy()
+        sub_a = np.concatenate([arena[i * stride:(i + 1) * stride] for i in pick])
+        sub_d["off"] = np.arange(len(pick)) * stride
+        want = sub_a.copy()
+        want_masks = orc.seal_batch(okeys, _oracle_keys_for(okeys, sub_d, slots), want, qpp.HP_MASK_OUT)
+        assert (np.concatenate([sealed[i * stride:(i + 1) * stride] for i in pick]) == want).all()
+        assert np.concatenate([masks[5 * i:5 * i + 5] for i in pick]).tobytes() == want_masks
+        ctx.open_batch(d_desc, n, d_arena, d_status)
+        assert (d_status.download(dtype=np.int8) == 0).all()
+        v, a = d_arena.download().reshape(n, stride), arena.reshape(n, stride)
+        assert (v[:, 21:21 + pt_len] == a[:, 21:21 + pt_len]).all()
+        for b in (d_desc, d_arena, d_mask, d_status):
+            b.free()
+    finally:
+        ctx.set_aes_kernel(qpp.AES_KERNEL_AUTO)
+        ctx.free_keys(batch)
 
 
 # ------------------------------------------------------------------ receive path: unprotect -> PN expand -> open

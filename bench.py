@@ -171,7 +171,7 @@ def main():
                          "txq: 64-packet GSO-burst flush latency through the transmit queue; packet: per-packet trait-API "
                          "latency")
     ap.add_argument("--cpu-seconds", type=float, default=1.5)
-    ap.add_argument("--pipe", default="65536,96,4",
+    ap.add_argument("--pipe", default="262144,384,4",
                     help="e2e: host pipeline geometry 'packets per chunk,MiB per chunk,chunk buffers'")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-hp", action="store_true", help="seal without the HP mask (diagnostic)")
@@ -330,7 +330,9 @@ def _host_batch(ctx, n, pt, aad, conn_of, pn_first, seed):
         m = min(block.size, host.size - o)
         host[o:o + m] = block[:m]
     host.reshape(n, stride)[:, 0] = 0x43
-    descs = np.zeros(n, dtype=qpp.PKT_DTYPE)
+    # descriptors pinned too: a pageable source or destination makes every chunk's copy synchronous (no overlap)
+    descs = ctx.host_alloc(n * qpp.PKT_DTYPE.itemsize).view(qpp.PKT_DTYPE)
+    descs[:] = 0
     idx = np.arange(n, dtype=np.uint64)
     descs["pn"] = np.uint64(pn_first) + idx
     descs["off"] = 0  # set per window by the caller
@@ -374,28 +376,36 @@ def e2e(args, rank, world, local_rank):
         d = descs[lo:hi]
         d["off"] = (np.arange(hi - lo, dtype=np.uint64) * np.uint64(stride)).astype(np.uint32)
         wins.append((lo, hi, host[lo * stride:hi * stride]))
-    masks = np.zeros(5 * n, np.uint8)
-    status = np.zeros(n, np.int8)
+    masks = ctx.host_alloc(5 * n)  # pinned (see _host_batch)
+    status = ctx.host_alloc(n).view(np.int8)
+    status[:] = 0
     flags = qpp.HP_MASK_OUT | (qpp.ONLY_CHACHA if suite == 3 else qpp.ONLY_AES)
     slots = np.array([k.slot for k in keys], dtype=np.uint32)
     descs["key_idx"] = slots[conn]
 
+    phase = {"rotate": 0.0, "pipeline": 0.0}
+
     def step():
         nonlocal keys, slots
+        t0 = time.perf_counter()
         if args.rotate:
             new = ctx.update_keys(keys)
             ctx.free_keys(keys)
             keys = new
             slots = np.array([k.slot for k in keys], dtype=np.uint32)
             descs["key_idx"] = slots[conn]
+        t1 = time.perf_counter()
         tickets = [ctx.host_submit(descs[lo:hi], arena, masks[5 * lo:5 * hi], status[lo:hi], flags,
                                    qpp.OP_SEAL | qpp.OP_OPEN) for lo, hi, arena in wins]
         for t in tickets:
             ctx.host_wait(t)
+        phase["rotate"] += t1 - t0
+        phase["pipeline"] += time.perf_counter() - t1
 
     for _ in range(args.warmup):
         step()
     ctl.barrier()
+    phase.update(rotate=0.0, pipeline=0.0)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -425,7 +435,9 @@ def e2e(args, rank, world, local_rank):
             "higher_is_better": True, "scaling": "strong" if args.total_packets else "weak", "dtype": "u8",
             "data": "synthetic (a 64 MiB PCG64 block tiled over the arena)",
             "config": {"workload": wl, "suite": args.suite, "packets_per_gpu": n, "keys": nk, "rotate": args.rotate,
-                       "h2d_d2h_bytes_per_step_per_gpu": 2 * n * stride, "windows": len(wins)},
+                       "h2d_d2h_bytes_per_step_per_gpu": 2 * n * stride, "windows": len(wins),
+                       "pipe": args.pipe, "rotate_ms_per_step": round(1e3 * phase["rotate"] / args.steps, 3),
+                       "pipeline_ms_per_step": round(1e3 * phase["pipeline"] / args.steps, 3)},
         }), flush=True)
     for k in keys:
         k.free()

@@ -244,8 +244,9 @@ int qpp_hp_mask_batch(qpp_ctx *ctx, const qpp_pkt *descs, size_t n, const uint8_
  * The path starts and ends in host memory (the UDP socket buffer, platform socket/io/tx.rs:204-268, rx.rs).  A host
  * batch is cut into chunks of consecutive packets; each chunk's span of the arena is copied H2D, sealed and/or
  * opened on the GPU and copied back D2H, chunks overlapping on three streams over a fixed ring of device buffers
- * (so a batch may be far larger than the ring).  descs / arena / masks / status are HOST pointers (arena: pinned,
- * qpp_host_alloc, for full PCIe rate); descriptors must be in ascending, non-overlapping arena order and stay
+ * (so a batch may be far larger than the ring).  descs / arena / masks / status are HOST pointers, all four pinned
+ * (qpp_host_alloc) for full PCIe rate and overlap: a pageable one makes every chunk's copies synchronous with the
+ * host thread, which serialises the pipeline.  Descriptors must be in ascending, non-overlapping arena order and stay
  * untouched until the ticket completes.  ops: QPP_OP_SEAL, QPP_OP_OPEN, or both (seal then open on the device:
  * the round trip; QPP_HP_APPLY is refused there since the opener needs the unprotected header).  Returns when every
  * chunk is enqueued; *ticket completes when the last chunk is back in host memory. */
@@ -257,7 +258,7 @@ int qpp_host_batch_submit(qpp_ctx *ctx, const qpp_pkt *descs, size_t n, uint8_t 
 int qpp_host_batch_query(qpp_ctx *ctx, uint64_t ticket, int *done);
 /* Blocks until the ticket's batch is back in host memory, then releases the ticket. */
 int qpp_host_batch_wait(qpp_ctx *ctx, uint64_t ticket);
-/* Ring geometry: packets and bytes per chunk, chunk buffers (defaults 65536, 96 MiB, 4).  Waits for the device. */
+/* Ring geometry: packets and bytes per chunk, chunk buffers (defaults 262144, 384 MiB, 4).  Waits for the device. */
 int qpp_ctx_set_host_pipe(qpp_ctx *ctx, size_t chunk_packets, size_t chunk_bytes, size_t slots);
 
 /* ------------------------------------------------------------------ deferred transmit queue */

@@ -56,7 +56,9 @@ struct PipeSlot {
 };
 
 struct HostPipe {
-    size_t chunk_packets = 65536, chunk_bytes = 96u << 20, nslots = 4;
+    // 256 Ki packets per chunk: with 4096 keys a chunk still holds ~64 packets per key (one full wave-item each);
+    // at 64 Ki the C5 pipeline ran 76 ms/step instead of 62 (profiles/r02_e2e.jsonl)
+    size_t chunk_packets = 262144, chunk_bytes = 384u << 20, nslots = 4;
     hipStream_t h2d = nullptr, comp = nullptr, d2h = nullptr;
     std::vector<PipeSlot> slots;
     size_t next = 0;

@@ -271,6 +271,11 @@ int qpp_ctx_set_host_pipe(qpp_ctx *ctx, size_t chunk_packets, size_t chunk_bytes
  * packet in one device batch: the ring then holds the protected packets, tags included. */
 typedef struct qpp_txq qpp_txq;
 int qpp_txq_create(qpp_ctx *ctx, size_t ring_bytes, size_t max_packets, qpp_txq **out);
+/* The same queue with up to in_flight (1..64) flushes outstanding (qpp_txq_flush_async): each flush has its own
+ * descriptors and plan; flushes go out round-robin on up to 4 streams of the queue.  The ring bytes of a flushed
+ * packet belong to the engine until its ticket completes (the transport encodes the next bursts elsewhere in the
+ * ring).  qpp_txq_create(..) = in_flight 1. */
+int qpp_txq_create_async(qpp_ctx *ctx, size_t ring_bytes, size_t max_packets, size_t in_flight, qpp_txq **out);
 void qpp_txq_destroy(qpp_txq *q);
 /* Host pointer to the ring (ring_bytes, pinned). */
 uint8_t *qpp_txq_ring(qpp_txq *q);
@@ -280,8 +285,23 @@ uint8_t *qpp_txq_ring(qpp_txq *q);
  * context. */
 int qpp_txq_push(qpp_txq *q, const qpp_key *key, uint64_t pn, size_t off, size_t header_len, size_t pn_len,
                  size_t payload_len);
+/* n pushes at once from ready descriptors (key_idx = qpp_key_slot of a live key of this context, off into the ring,
+ * aad_len = header_len + pn_len, flags 0): for bindings whose per-call cost dominates a GSO burst (Python), same
+ * checks as qpp_txq_push; nothing is queued unless every descriptor passes. */
+int qpp_txq_push_descs(qpp_txq *q, const qpp_pkt *descs, size_t n);
 /* Seal + header-protect every pushed packet (one qpp_seal_batch with QPP_HP_APPLY), wait, empty the queue. */
 int qpp_txq_flush(qpp_txq *q);
+/* The same without waiting: *ticket names the flush (0 when nothing was pushed).  Returns once the flush is enqueued;
+ * if all in_flight slots are busy, first waits for the oldest.  The queue is empty again for the next burst. */
+int qpp_txq_flush_async(qpp_txq *q, uint64_t *ticket);
+/* *done = 1 once the ticket's packets are protected in the ring (then the socket may send them). */
+int qpp_txq_poll(qpp_txq *q, uint64_t ticket, int *done);
+/* Blocks until the ticket's packets are protected in the ring. */
+int qpp_txq_wait(qpp_txq *q, uint64_t ticket);
+/* Coalescing: flush_async holds bursts back until `bursts` of them are in (or the next would not fit max_packets),
+ * then sends them as one launch; polling or waiting on a held ticket sends it at once.  Default 1 (every flush_async
+ * sends).  Fewer, larger launches: the host's per-launch cost is what bounds a stream of small GSO bursts. */
+int qpp_txq_set_coalesce(qpp_txq *q, size_t bursts);
 size_t qpp_txq_pending(const qpp_txq *q);
 
 /* ------------------------------------------------------------------ receive path */

@@ -497,10 +497,12 @@ __global__ void key_install_kernel(DevKey *keys, const uint32_t *__restrict__ sl
 }  // namespace
 
 hipError_t launch_key_install(DevKey *keys, const uint32_t *slots, const DevKey *records, uint32_t count,
-                              hipStream_t s) {
+                              const PowTables &pow, hipStream_t s) {
     if (!count) return hipSuccess;
     hipLaunchKernelGGL(key_install_kernel, dim3((count + 63) / 64), dim3(64), 0, s, keys, slots, records, count);
-    return hipGetLastError();
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return launch_pow_setup(keys, slots, count, pow, s);
 }
 
 namespace {

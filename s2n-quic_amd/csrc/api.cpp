@@ -81,6 +81,7 @@ struct qpp_ctx {
     // device key table + host mirror
     DevKey *d_keys = nullptr;
     uint32_t key_cap = 0;
+    PowTables pow{nullptr, 0};  // burst power tables of slots < pow.cap (grown with the key table, <= kPowSlots)
     std::vector<DevKey> h_keys;
     std::vector<uint8_t> dirty_flag;
     std::vector<uint32_t> dirty;          // slots whose host record must be installed before the next launch
@@ -218,8 +219,20 @@ int grow_keys(qpp_ctx *ctx, uint32_t need) {
                                     ctx->kstream));
         HIP_TRY(ctx, hipMemsetAsync(ctx->d_keys, 0, sizeof(DevKey) * ctx->key_cap, ctx->kstream));
     }
+    const uint32_t pcap = std::min<uint32_t>(cap, kPowSlots);
+    uint8_t *np = ctx->pow.base;
+    if (pcap > ctx->pow.cap) {  // the precomputed tables of the slots so far move along
+        HIP_TRY(ctx, hipMalloc(&np, (size_t)pcap * kPowBytes));
+        if (ctx->pow.cap)
+            HIP_TRY(ctx, hipMemcpyAsync(np, ctx->pow.base, (size_t)ctx->pow.cap * kPowBytes, hipMemcpyDeviceToDevice,
+                                        ctx->kstream));
+    }
     HIP_TRY(ctx, hipStreamSynchronize(ctx->kstream));
     if (ctx->d_keys) HIP_TRY(ctx, hipFree(ctx->d_keys));
+    if (np != ctx->pow.base) {
+        if (ctx->pow.base) HIP_TRY(ctx, hipFree(ctx->pow.base));
+        ctx->pow = PowTables{np, pcap};
+    }
     ctx->d_keys = nk;
     ctx->h_keys.resize(cap);
     ctx->dirty_flag.resize(cap, 0);
@@ -264,7 +277,7 @@ int flush_keys(qpp_ctx *ctx) {
     hipStream_t s = ctx->kstream;
     HIP_TRY(ctx, hipMemcpyAsync(ctx->d_kstage, ctx->h_kstage, rec + slots, hipMemcpyHostToDevice, s));
     HIP_TRY(ctx, launch_key_install(ctx->d_keys, (const uint32_t *)(ctx->d_kstage + rec),
-                                    (const DevKey *)ctx->d_kstage, n, s));
+                                    (const DevKey *)ctx->d_kstage, n, ctx->pow, s));
     HIP_TRY(ctx, hipMemsetAsync(ctx->d_kstage, 0, rec, s));
     HIP_TRY(ctx, hipEventRecord(ctx->keys_ready, s));
     ctx->key_gen++;
@@ -360,6 +373,10 @@ int flush_retire(qpp_ctx *ctx) {
         size_t j = i + 1;
         while (j < sorted.size() && sorted[j] == sorted[j - 1] + 1) j++;
         HIP_TRY(ctx, hipMemsetAsync(ctx->d_keys + sorted[i], 0, sizeof(DevKey) * (j - i), ctx->rstream));
+        if (sorted[i] < ctx->pow.cap) {  // the burst power tables are derived from H: zeroized with the record
+            const size_t k = std::min<size_t>(j - i, ctx->pow.cap - sorted[i]);
+            HIP_TRY(ctx, hipMemsetAsync(ctx->pow.base + (size_t)sorted[i] * kPowBytes, 0, kPowBytes * k, ctx->rstream));
+        }
         i = j;
     }
     hipEvent_t e = get_event(ctx);
@@ -456,7 +473,7 @@ hipError_t launch_aes(const qpp_ctx *ctx, AesPath p, bool seal, const qpp_pkt *d
     switch (p) {
         case AesPath::burst:
             return launch_aes_gcm_burst(seal, ctx->d_keys, descs, pb, n, ctx->key_cap, per, arena, masks, status, flags,
-                                        suite_mask(ctx), s);
+                                        suite_mask(ctx), ctx->pow, s);
         case AesPath::wave:
             return launch_aes_gcm_wave(seal, ctx->d_keys, descs, pb, n, ctx->key_cap, ctx->n_cu, arena, masks, status,
                                        flags, suite_mask(ctx), s);
@@ -533,9 +550,12 @@ int run_one(const qpp_key *k, bool seal, uint64_t pn, const uint8_t *header, siz
     int8_t *vst = (int8_t *)(v + 64);
     if (is_aes(k->suite)) {
         // key_cap = 0: grid = plan_max_work(1, 0, per) = 1; only work item 0 exists
-        HIP_TRY(ctx, (ctx->burst_max ? launch_aes_gcm_burst : launch_aes_gcm)(seal, ctx->d_keys, vd, pb, 1, 0, 1,
-                                                                             v + kOnePkt, v + 80, vst, 0,
-                                                                             1u << k->suite, s));
+        if (ctx->burst_max)
+            HIP_TRY(ctx, launch_aes_gcm_burst(seal, ctx->d_keys, vd, pb, 1, 0, 1, v + kOnePkt, v + 80, vst, 0,
+                                              1u << k->suite, ctx->pow, s));
+        else
+            HIP_TRY(ctx, launch_aes_gcm(seal, ctx->d_keys, vd, pb, 1, 0, 1, v + kOnePkt, v + 80, vst, 0,
+                                        1u << k->suite, s));
     } else {
         HIP_TRY(ctx, launch_chacha(seal, ctx->d_keys, ctx->key_cap, vd, 1, v + kOnePkt, v + 80, vst, 0,
                                    ctx->burst_max > 0, s));
@@ -591,7 +611,7 @@ int derive_batch(qpp_ctx *ctx, int suite, const uint8_t *secrets, const uint8_t 
     hipStream_t s = ctx->kstream;
     HIP_TRY(ctx, hipMemcpyAsync(d, h, o_slot + 4 * n, hipMemcpyHostToDevice, s));
     HIP_TRY(ctx, launch_key_derive(ctx->d_keys, (const uint32_t *)(d + o_slot), (uint32_t)n, suite, d,
-                                   hp_in ? d + o_hp : nullptr, updates, d + o_mat, s));
+                                   hp_in ? d + o_hp : nullptr, updates, d + o_mat, ctx->pow, s));
     HIP_TRY(ctx, hipMemcpyAsync(h + o_mat, d + o_mat, n * mb, hipMemcpyDeviceToHost, s));
     HIP_TRY(ctx, hipMemsetAsync(d, 0, total, s));
     HIP_TRY(ctx, hipEventRecord(ctx->keys_ready, s));
@@ -729,6 +749,11 @@ void qpp_ctx_destroy(qpp_ctx *ctx) {
         hipFree(ctx->d_keys);
     }
     secure_zero(ctx->h_keys.data(), sizeof(DevKey) * ctx->h_keys.size());
+    if (ctx->pow.base) {
+        hipMemsetAsync(ctx->pow.base, 0, (size_t)ctx->pow.cap * kPowBytes, ctx->stream);
+        hipStreamSynchronize(ctx->stream);
+        hipFree(ctx->pow.base);
+    }
     for (StreamState *st : ctx->streams) {
         free_plan(st->plan);
         if (st->last) hipEventDestroy(st->last);
@@ -1389,55 +1414,94 @@ int qpp_stream_wait_event(qpp_ctx *ctx, void *stream, void *event) {
 
 // ---------------------------------------------------------------- deferred transmit queue
 
-struct qpp_txq {
-    qpp_ctx *ctx = nullptr;
-    size_t ring_bytes = 0, max_packets = 0;
-    uint8_t *h_ring = nullptr, *d_ring = nullptr;
-    qpp_pkt *h_desc = nullptr, *d_desc = nullptr;
-    size_t count = 0, lo = SIZE_MAX, hi = 0;
-    uint32_t suites = 0;
-    // zero-copy flush of small bursts: the kernels read and write the pinned ring, descriptors and a host-built
-    // plan directly over PCIe (no DMA copies, no plan launches); device views of the pinned buffers
-    uint32_t zc_max = 0;
+// One in-flight flush of a txq: its descriptors and (zero-copy) plan in pinned memory, the device copies for the DMA
+// path, the stream it went out on and the event that ends it.
+struct TxqSlot {
+    qpp_pkt *h_desc = nullptr, *d_desc = nullptr, *v_desc = nullptr;
     uint32_t *h_perm = nullptr;  // pinned: perm[max_packets] | n_work | WorkItem work[max_packets + 1]
     WorkItem *h_work = nullptr;
     uint32_t *h_nwork = nullptr;
-    uint8_t *v_ring = nullptr;
-    qpp_pkt *v_desc = nullptr;
     PlanBuffers v_plan{};
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;
+    uint64_t first = 0, last = 0;  // tickets (bursts) of the flush that last used this slot (0: never)
+    bool busy = false;    // `done` recorded and not yet seen complete
+    size_t lo = 0, hi = 0;  // ring span of that flush (DMA path)
+};
+
+struct qpp_txq {
+    qpp_ctx *ctx = nullptr;
+    size_t ring_bytes = 0, max_packets = 0;
+    uint8_t *h_ring = nullptr, *d_ring = nullptr, *v_ring = nullptr;
+    // flushes in flight: the batch being pushed fills slots[cur]; flush_async sends it and moves to the next slot
+    std::vector<TxqSlot> slots;
+    std::vector<hipStream_t> streams;
+    size_t cur = 0;
+    uint64_t next_ticket = 1;
+    // bursts flushed into slots[cur] but not yet submitted (coalescing): tickets [pend_first, pend_last]
+    uint64_t pend_first = 0, pend_last = 0;
+    uint32_t pend_bursts = 0, coalesce = 1;
+    size_t count = 0, lo = SIZE_MAX, hi = 0;
+    size_t count_at_ticket = 0;  // q->count at the last flush_async (packets pushed since belong to the next ticket)
+    uint32_t suites = 0;
+    // zero-copy flush of small bursts: the kernels read and write the pinned ring, descriptors and a host-built
+    // plan directly over PCIe (no DMA copies, no plan launches)
+    uint32_t zc_max = 0;
     std::vector<uint32_t> order;
 };
 
 extern "C" {
 
 int qpp_txq_create(qpp_ctx *ctx, size_t ring_bytes, size_t max_packets, qpp_txq **out) {
-    if (!ctx || !out || !ring_bytes || !max_packets || ring_bytes > UINT32_MAX) return QPP_INTERNAL_ERROR;
+    return qpp_txq_create_async(ctx, ring_bytes, max_packets, 1, out);
+}
+
+int qpp_txq_create_async(qpp_ctx *ctx, size_t ring_bytes, size_t max_packets, size_t in_flight, qpp_txq **out) {
+    if (!ctx || !out || !ring_bytes || !max_packets || ring_bytes > UINT32_MAX || max_packets > UINT32_MAX ||
+        !in_flight || in_flight > 64)
+        return QPP_INTERNAL_ERROR;
     *out = nullptr;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     qpp_txq *q = new qpp_txq();
     q->ctx = ctx;
     q->ring_bytes = ring_bytes;
     q->max_packets = max_packets;
-    if (fail(ctx, hipHostMalloc(&q->h_ring, ring_bytes, hipHostMallocDefault), "txq ring") ||
-        fail(ctx, hipMalloc(&q->d_ring, ring_bytes), "txq ring") ||
-        fail(ctx, hipHostMalloc(&q->h_desc, sizeof(qpp_pkt) * max_packets, hipHostMallocDefault), "txq descs") ||
-        fail(ctx, hipMalloc(&q->d_desc, sizeof(qpp_pkt) * max_packets), "txq descs") ||
-        fail(ctx, hipHostMalloc(&q->h_perm, 4 * (max_packets + 4) + sizeof(WorkItem) * (max_packets + 1),
-                                hipHostMallocDefault), "txq plan")) {
-        qpp_txq_destroy(q);
-        return QPP_DEVICE_ERROR;
-    }
-    q->h_nwork = q->h_perm + max_packets;
-    q->h_work = (WorkItem *)(q->h_perm + max_packets + 4);  // 16-byte aligned
     void *v = nullptr;
-    if (fail(ctx, hipHostGetDevicePointer(&v, q->h_ring, 0), "txq ring view")) { qpp_txq_destroy(q); return QPP_DEVICE_ERROR; }
+    auto bad = [&](hipError_t e, const char *what) {
+        if (!fail(ctx, e, what)) return false;
+        qpp_txq_destroy(q);
+        return true;
+    };
+    if (bad(hipHostMalloc(&q->h_ring, ring_bytes, hipHostMallocDefault), "txq ring") ||
+        bad(hipMalloc(&q->d_ring, ring_bytes), "txq ring") || bad(hipHostGetDevicePointer(&v, q->h_ring, 0), "ring view"))
+        return QPP_DEVICE_ERROR;
     q->v_ring = (uint8_t *)v;
-    if (fail(ctx, hipHostGetDevicePointer(&v, q->h_desc, 0), "txq desc view")) { qpp_txq_destroy(q); return QPP_DEVICE_ERROR; }
-    q->v_desc = (qpp_pkt *)v;
-    if (fail(ctx, hipHostGetDevicePointer(&v, q->h_perm, 0), "txq plan view")) { qpp_txq_destroy(q); return QPP_DEVICE_ERROR; }
-    q->v_plan.perm = (uint32_t *)v;
-    q->v_plan.n_work = q->v_plan.perm + max_packets;
-    q->v_plan.work = (WorkItem *)(q->v_plan.perm + max_packets + 4);
+    // one stream per in-flight flush up to 4 (the hardware queues a process gets), shared round-robin beyond
+    const size_t nstreams = in_flight < 4 ? in_flight : 4;
+    for (size_t i = 0; i < nstreams; i++) {
+        hipStream_t st = nullptr;
+        if (bad(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "txq stream")) return QPP_DEVICE_ERROR;
+        q->streams.push_back(st);
+    }
+    q->slots.resize(in_flight);
+    for (size_t i = 0; i < in_flight; i++) {
+        TxqSlot &sl = q->slots[i];
+        sl.stream = q->streams[i % nstreams];
+        if (bad(hipHostMalloc(&sl.h_desc, sizeof(qpp_pkt) * max_packets, hipHostMallocDefault), "txq descs") ||
+            bad(hipMalloc(&sl.d_desc, sizeof(qpp_pkt) * max_packets), "txq descs") ||
+            bad(hipHostMalloc(&sl.h_perm, 4 * (max_packets + 4) + sizeof(WorkItem) * (max_packets + 1),
+                              hipHostMallocDefault), "txq plan") ||
+            bad(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming), "txq event"))
+            return QPP_DEVICE_ERROR;
+        sl.h_nwork = sl.h_perm + max_packets;
+        sl.h_work = (WorkItem *)(sl.h_perm + max_packets + 4);  // 16-byte aligned
+        if (bad(hipHostGetDevicePointer(&v, sl.h_desc, 0), "txq desc view")) return QPP_DEVICE_ERROR;
+        sl.v_desc = (qpp_pkt *)v;
+        if (bad(hipHostGetDevicePointer(&v, sl.h_perm, 0), "txq plan view")) return QPP_DEVICE_ERROR;
+        sl.v_plan.perm = (uint32_t *)v;
+        sl.v_plan.n_work = sl.v_plan.perm + max_packets;
+        sl.v_plan.work = (WorkItem *)(sl.v_plan.perm + max_packets + 4);
+    }
     q->zc_max = kTxqZeroCopyMax;
     if (const char *e = getenv("QPP_TXQ_ZC_MAX")) q->zc_max = (uint32_t)strtoul(e, nullptr, 10);
     q->order.reserve(max_packets);
@@ -1449,21 +1513,28 @@ int qpp_txq_create(qpp_ctx *ctx, size_t ring_bytes, size_t max_packets, qpp_txq 
 void qpp_txq_destroy(qpp_txq *q) {
     if (!q) return;
     hipSetDevice(q->ctx->device);
-    hipStreamSynchronize(q->ctx->stream);
+    for (hipStream_t st : q->streams) hipStreamSynchronize(st);
     if (q->h_ring) { secure_zero(q->h_ring, q->ring_bytes); hipHostFree(q->h_ring); }
     if (q->d_ring) {
         hipMemsetAsync(q->d_ring, 0, q->ring_bytes, q->ctx->stream);
         hipStreamSynchronize(q->ctx->stream);
         hipFree(q->d_ring);
     }
-    if (q->h_desc) hipHostFree(q->h_desc);
-    if (q->d_desc) hipFree(q->d_desc);
-    if (q->h_perm) hipHostFree(q->h_perm);
+    for (TxqSlot &sl : q->slots) {
+        if (sl.h_desc) hipHostFree(sl.h_desc);
+        if (sl.d_desc) hipFree(sl.d_desc);
+        if (sl.h_perm) hipHostFree(sl.h_perm);
+        if (sl.done) hipEventDestroy(sl.done);
+    }
+    for (hipStream_t st : q->streams) {
+        // the stream's StreamState (plan scratch of the DMA path) goes with it
+        qpp_stream_destroy(q->ctx, (void *)st);
+    }
     delete q;
 }
 
 uint8_t *qpp_txq_ring(qpp_txq *q) { return q ? q->h_ring : nullptr; }
-size_t qpp_txq_pending(const qpp_txq *q) { return q ? q->count : 0; }
+size_t qpp_txq_pending(const qpp_txq *q) { return q ? q->count - q->count_at_ticket : 0; }
 
 int qpp_txq_push(qpp_txq *q, const qpp_key *key, uint64_t pn, size_t off, size_t header_len, size_t pn_len,
                  size_t payload_len) {
@@ -1473,7 +1544,7 @@ int qpp_txq_push(qpp_txq *q, const qpp_key *key, uint64_t pn, size_t off, size_t
     const size_t end = off + header_len + pn_len + payload_len + 16;
     if (end > q->ring_bytes || end < off) return QPP_INTERNAL_ERROR;
     if (payload_len + pn_len < 4) return QPP_DECODE_ERROR;  // the sample at header_len + 4 must fit
-    qpp_pkt &d = q->h_desc[q->count++];
+    qpp_pkt &d = q->slots[q->cur].h_desc[q->count++];
     d = qpp_pkt{};
     d.pn = pn;
     d.key_idx = key->slot;
@@ -1487,71 +1558,171 @@ int qpp_txq_push(qpp_txq *q, const qpp_key *key, uint64_t pn, size_t off, size_t
     return QPP_OK;
 }
 
-// Zero-copy flush: host plan (AES packets grouped by key, work items of whole waves) in pinned memory, then the
-// burst kernel (AES) and the ChaCha kernel on the pinned ring itself; one launch per suite family, one sync.
-static int txq_flush_zero_copy(qpp_txq *q, hipStream_t s) {
+int qpp_txq_push_descs(qpp_txq *q, const qpp_pkt *descs, size_t n) {
+    if (!q || (n && !descs)) return QPP_INTERNAL_ERROR;
+    if (n > q->max_packets - q->count) return QPP_INTERNAL_ERROR;  // flush first
     qpp_ctx *ctx = q->ctx;
-    const uint32_t n = (uint32_t)q->count;
+    for (size_t i = 0; i < n; i++) {  // the checks of qpp_txq_push, all before anything is queued
+        const qpp_pkt &d = descs[i];
+        if (d.key_idx >= ctx->key_cap || ctx->h_keys[d.key_idx].live != 1) return QPP_INTERNAL_ERROR;
+        if (d.pn_len < 1 || d.pn_len > 4 || d.aad_len < d.pn_len || d.flags) return QPP_INTERNAL_ERROR;
+        const size_t end = (size_t)d.off + d.aad_len + d.pt_len + 16;
+        if (end > q->ring_bytes) return QPP_INTERNAL_ERROR;
+        if ((size_t)d.pt_len + d.pn_len < 4) return QPP_DECODE_ERROR;
+    }
+    memcpy(q->slots[q->cur].h_desc + q->count, descs, sizeof(qpp_pkt) * n);
+    for (size_t i = 0; i < n; i++) {
+        const qpp_pkt &d = descs[i];
+        q->lo = std::min<size_t>(q->lo, d.off);
+        q->hi = std::max<size_t>(q->hi, (size_t)d.off + d.aad_len + d.pt_len + 16);
+        q->suites |= 1u << ctx->h_keys[d.key_idx].suite;
+    }
+    q->count += n;
+    return QPP_OK;
+}
+
+// Zero-copy flush: host plan (AES packets grouped by key, work items of whole waves) in the slot's pinned memory,
+// then the burst kernel (AES) and the ChaCha kernel on the pinned ring itself; one launch per suite family.
+static int txq_enqueue_zero_copy(qpp_txq *q, TxqSlot &sl, uint32_t n) {
+    qpp_ctx *ctx = q->ctx;
+    hipStream_t s = sl.stream;
     if (q->suites & kAesSuites) {
         std::vector<uint32_t> &ord = q->order;
         ord.clear();
         for (uint32_t i = 0; i < n; i++)
-            if (is_aes(ctx->h_keys[q->h_desc[i].key_idx].suite)) ord.push_back(i);
+            if (is_aes(ctx->h_keys[sl.h_desc[i].key_idx].suite)) ord.push_back(i);
         std::stable_sort(ord.begin(), ord.end(),
-                         [q](uint32_t a, uint32_t b) { return q->h_desc[a].key_idx < q->h_desc[b].key_idx; });
+                         [&sl](uint32_t a, uint32_t b) { return sl.h_desc[a].key_idx < sl.h_desc[b].key_idx; });
         const uint32_t per = burst_packets_per_item((uint32_t)ord.size(), ctx->n_cu);
         uint32_t items = 0, keys = 0;
         for (uint32_t i = 0; i < ord.size();) {
-            const uint32_t slot = q->h_desc[ord[i]].key_idx;
+            const uint32_t slot = sl.h_desc[ord[i]].key_idx;
             uint32_t j = i;
-            while (j < ord.size() && q->h_desc[ord[j]].key_idx == slot) j++;
+            while (j < ord.size() && sl.h_desc[ord[j]].key_idx == slot) j++;
             for (uint32_t b = i; b < j; b += per)
-                q->h_work[items++] = WorkItem{slot, b, std::min(per, j - b), ctx->h_keys[slot].nr};
+                sl.h_work[items++] = WorkItem{slot, b, std::min(per, j - b), ctx->h_keys[slot].nr};
             keys++;
             i = j;
         }
-        std::copy(ord.begin(), ord.end(), q->h_perm);
-        *q->h_nwork = items;
-        HIP_TRY(ctx, launch_aes_gcm_burst(true, ctx->d_keys, q->v_desc, q->v_plan, (uint32_t)ord.size(), keys, per,
-                                          q->v_ring, nullptr, nullptr, QPP_HP_APPLY, q->suites & kAesSuites, s));
+        std::copy(ord.begin(), ord.end(), sl.h_perm);
+        *sl.h_nwork = items;
+        HIP_TRY(ctx, launch_aes_gcm_burst(true, ctx->d_keys, sl.v_desc, sl.v_plan, (uint32_t)ord.size(), keys, per,
+                                          q->v_ring, nullptr, nullptr, QPP_HP_APPLY, q->suites & kAesSuites, ctx->pow,
+                                          s));
     }
     if (q->suites & ~kAesSuites)
-        HIP_TRY(ctx, launch_chacha(true, ctx->d_keys, ctx->key_cap, q->v_desc, n, q->v_ring, nullptr, nullptr,
+        HIP_TRY(ctx, launch_chacha(true, ctx->d_keys, ctx->key_cap, sl.v_desc, n, q->v_ring, nullptr, nullptr,
                                    QPP_HP_APPLY, true, s));
-    HIP_TRY(ctx, hipStreamSynchronize(s));
     return QPP_OK;
 }
 
-int qpp_txq_flush(qpp_txq *q) {
-    if (!q) return QPP_INTERNAL_ERROR;
-    if (!q->count) return QPP_OK;
+// the slot's last flush is over (host wait); its buffers may be refilled
+static int txq_slot_drain(qpp_txq *q, TxqSlot &sl) {
+    if (!sl.busy) return QPP_OK;
+    HIP_TRY(q->ctx, hipEventSynchronize(sl.done));
+    sl.busy = false;
+    return QPP_OK;
+}
+
+// Sends slots[cur] (every burst flushed into it) and moves on to the next slot, once that one's last flush is over.
+static int txq_submit(qpp_txq *q) {
+    if (!q->pend_bursts) return QPP_OK;
     qpp_ctx *ctx = q->ctx;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    hipStream_t s = ctx->stream;
     RC_TRY(flush_keys(ctx));
-    int rc;
-    if (q->count <= q->zc_max) {
-        StreamState *st = nullptr;
-        RC_TRY(batch_stream(ctx, nullptr, &st));  // sees the latest key install; synchronous, so no note_work
-        rc = txq_flush_zero_copy(q, s);
+    TxqSlot &sl = q->slots[q->cur];
+    const uint32_t n = (uint32_t)q->count;
+    StreamState *st = nullptr;
+    RC_TRY(batch_stream(ctx, sl.stream, &st));  // sees the latest key install
+    if (n <= q->zc_max) {
+        RC_TRY(txq_enqueue_zero_copy(q, sl, n));
     } else {
+        hipStream_t s = sl.stream;
         const size_t span = q->hi - q->lo;
         HIP_TRY(ctx, hipMemcpyAsync(q->d_ring + q->lo, q->h_ring + q->lo, span, hipMemcpyHostToDevice, s));
-        HIP_TRY(ctx, hipMemcpyAsync(q->d_desc, q->h_desc, sizeof(qpp_pkt) * q->count, hipMemcpyHostToDevice, s));
+        HIP_TRY(ctx, hipMemcpyAsync(sl.d_desc, sl.h_desc, sizeof(qpp_pkt) * n, hipMemcpyHostToDevice, s));
         uint32_t flags = QPP_HP_APPLY;
         if (!(q->suites & ~kAesSuites)) flags |= QPP_ONLY_AES;
         else if (!(q->suites & kAesSuites)) flags |= QPP_ONLY_CHACHA;
-        rc = qpp_seal_batch(ctx, q->d_desc, q->count, q->d_ring, nullptr, nullptr, flags, s);
-        if (rc) return rc;
+        RC_TRY(enqueue_seal(ctx, st, sl.d_desc, n, q->d_ring, nullptr, nullptr, flags));
         HIP_TRY(ctx, hipMemcpyAsync(q->h_ring + q->lo, q->d_ring + q->lo, span, hipMemcpyDeviceToHost, s));
-        HIP_TRY(ctx, hipStreamSynchronize(s));
     }
-    if (rc) return rc;
-    q->count = 0;
+    RC_TRY(note_work(ctx, st));  // key retirement orders behind this flush
+    HIP_TRY(ctx, hipEventRecord(sl.done, sl.stream));
+    sl.busy = true;
+    sl.first = q->pend_first;
+    sl.last = q->pend_last;
+    sl.lo = q->lo;
+    sl.hi = q->hi;
+    q->pend_first = q->pend_last = 0;
+    q->pend_bursts = 0;
+    q->count = q->count_at_ticket = 0;
     q->lo = SIZE_MAX;
     q->hi = 0;
     q->suites = 0;
+    // the next batch fills the next slot, once that slot's previous flush is over (back-pressure)
+    q->cur = (q->cur + 1) % q->slots.size();
+    return txq_slot_drain(q, q->slots[q->cur]);
+}
+
+int qpp_txq_set_coalesce(qpp_txq *q, size_t bursts) {
+    if (!q || !bursts || bursts > 1024) return QPP_INTERNAL_ERROR;
+    q->coalesce = (uint32_t)bursts;
     return QPP_OK;
+}
+
+int qpp_txq_flush_async(qpp_txq *q, uint64_t *ticket) {
+    if (!q || !ticket) return QPP_INTERNAL_ERROR;
+    *ticket = 0;
+    const size_t burst = q->count - q->count_at_ticket;
+    if (!burst) return QPP_OK;  // nothing pushed since the last flush: ticket 0 is always complete
+    *ticket = q->next_ticket++;
+    if (!q->pend_first) q->pend_first = *ticket;
+    q->pend_last = *ticket;
+    q->pend_bursts++;
+    q->count_at_ticket = q->count;
+    // send now once `coalesce` bursts are in, or when another burst of this size would not fit the slot
+    if (q->pend_bursts >= q->coalesce || q->count + burst > q->max_packets) return txq_submit(q);
+    return QPP_OK;
+}
+
+// the slot holding `ticket` (submitting it first if it is still being coalesced); nullptr: long complete
+static int txq_slot_of(qpp_txq *q, uint64_t ticket, TxqSlot **out) {
+    *out = nullptr;
+    if (!ticket) return QPP_OK;
+    if (q->pend_first && ticket >= q->pend_first && ticket <= q->pend_last) RC_TRY(txq_submit(q));
+    for (TxqSlot &sl : q->slots)
+        if (sl.first && ticket >= sl.first && ticket <= sl.last) { *out = &sl; break; }
+    return QPP_OK;
+}
+
+int qpp_txq_poll(qpp_txq *q, uint64_t ticket, int *done) {
+    if (!q || !done) return QPP_INTERNAL_ERROR;
+    if (ticket >= q->next_ticket) return QPP_INTERNAL_ERROR;
+    TxqSlot *sl = nullptr;
+    RC_TRY(txq_slot_of(q, ticket, &sl));
+    if (!sl || !sl->busy) { *done = 1; return QPP_OK; }
+    const hipError_t e = hipEventQuery(sl->done);
+    if (e == hipErrorNotReady) { *done = 0; return QPP_OK; }
+    HIP_TRY(q->ctx, e);
+    sl->busy = false;
+    *done = 1;
+    return QPP_OK;
+}
+
+int qpp_txq_wait(qpp_txq *q, uint64_t ticket) {
+    if (!q) return QPP_INTERNAL_ERROR;
+    if (ticket >= q->next_ticket) return QPP_INTERNAL_ERROR;
+    TxqSlot *sl = nullptr;
+    RC_TRY(txq_slot_of(q, ticket, &sl));
+    if (!sl) return QPP_OK;
+    return txq_slot_drain(q, *sl);
+}
+
+int qpp_txq_flush(qpp_txq *q) {
+    uint64_t t = 0;
+    RC_TRY(qpp_txq_flush_async(q, &t));
+    return qpp_txq_wait(q, t);
 }
 
 }  // extern "C"

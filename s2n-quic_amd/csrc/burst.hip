@@ -51,24 +51,54 @@ __device__ __forceinline__ uint4 gmul(uint32_t base, uint4 z) {
     return xor3(acc[0], acc[1], acc[2] ^ acc[3]);
 }
 
-// AES tables + T_0 .. T_6 for one key.  All threads take part; ends with a barrier.
-__device__ void burst_tables(const DevKey *__restrict__ key) {
-    build_aes_tables(kBurstAes);
+// T_0 of one key from its V[m] (nibble bit j <-> GCM bit index 4 pos + 3 - j).  No barrier inside.
+__device__ __forceinline__ void burst_t0(const DevKey *__restrict__ key) {
     const uint4 *V = (const uint4 *)key->V;
     for (uint32_t e = threadIdx.x; e < 512; e += blockDim.x) {
         const uint32_t pos = e >> 4, nib = e & 15u;
         uint4 acc = make_uint4(0, 0, 0, 0);
 #pragma unroll
-        for (int j = 0; j < 4; j++)  // nibble bit j <-> GCM bit index 4 pos + 3 - j
+        for (int j = 0; j < 4; j++)
             if ((nib >> j) & 1u) acc = acc ^ V[4 * pos + 3 - j];
         lds_st128(tab(0) + 16u * e, acc);
     }
+}
+
+// T_1 .. T_6 from T_0 in LDS: T_{t+1}[e] = T_t[e] * P_t through T_t (6 dependent levels).  Ends with a barrier.
+__device__ __forceinline__ void burst_powers() {
     __syncthreads();
     for (int t = 0; t < 6; t++) {
         for (uint32_t e = threadIdx.x; e < 512; e += blockDim.x)
             lds_st128(tab(t + 1) + 16u * e, gmul(tab(t), lds_ld128(tab(t) + 16u * e)));
         __syncthreads();
     }
+}
+
+// AES tables + T_0 .. T_6 for one key.  T_1 .. T_6 come from the key's precomputed slot when it has one
+// (pow.cap > slot: filled by pow_setup_kernel at install), else they are built here.  Ends with a barrier.
+__device__ void burst_tables(const DevKey *__restrict__ key, uint32_t slot, const PowTables pow) {
+    build_aes_tables(kBurstAes);
+    burst_t0(key);
+    if (slot < pow.cap) {
+        const uint4 *src = (const uint4 *)(pow.base + (size_t)slot * kPowBytes);
+        for (uint32_t i = threadIdx.x; i < kPowBytes / 16; i += blockDim.x) lds_st128(tab(1) + 16u * i, src[i]);
+        __syncthreads();
+    } else {
+        burst_powers();
+    }
+}
+
+// One workgroup per listed slot: T_1 .. T_6 of an AES packet key into its pow slot.
+__global__ __launch_bounds__(512) void pow_setup_kernel(const DevKey *__restrict__ keys,
+                                                        const uint32_t *__restrict__ slots, const PowTables pow) {
+    const uint32_t slot = slots[blockIdx.x];
+    if (slot >= pow.cap) return;  // uniform
+    const DevKey *__restrict__ key = keys + slot;
+    if (key->live != 1 || key->suite == QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256) return;
+    burst_t0(key);
+    burst_powers();
+    uint4 *dst = (uint4 *)(pow.base + (size_t)slot * kPowBytes);
+    for (uint32_t i = threadIdx.x; i < kPowBytes / 16; i += blockDim.x) dst[i] = lds_ld128(tab(1) + 16u * i);
 }
 
 __device__ __forceinline__ uint4 shfl4(uint4 v, int src) {
@@ -195,12 +225,12 @@ __global__ __launch_bounds__(kBurstWG) void aes_gcm_burst_kernel(const DevKey *_
                                                                   const WorkItem *__restrict__ work,
                                                                   const uint32_t *__restrict__ n_work,
                                                                   uint8_t *__restrict__ arena, uint8_t *masks,
-                                                                  int8_t *status, uint32_t flags) {
+                                                                  int8_t *status, uint32_t flags, const PowTables pow) {
     if (blockIdx.x >= *n_work) return;  // uniform: grid is sized for the worst case
     const WorkItem w = work[blockIdx.x];
     if (w.nr != NR) return;
     const DevKey *__restrict__ key = keys + w.key;
-    burst_tables(key);
+    burst_tables(key, w.key, pow);
     const AesLds aes = make_aes(kBurstAes);
     uint32_t rk[4 * (NR + 1)];
 #pragma unroll
@@ -216,9 +246,9 @@ __global__ __launch_bounds__(kBurstWG) void aes_gcm_burst_kernel(const DevKey *_
 
 template <bool SEAL, int NR>
 void launch_burst(dim3 grid, hipStream_t s, const DevKey *keys, const qpp_pkt *descs, const PlanBuffers &pb,
-                  uint8_t *arena, uint8_t *masks, int8_t *status, uint32_t flags) {
+                  uint8_t *arena, uint8_t *masks, int8_t *status, uint32_t flags, const PowTables &pow) {
     hipLaunchKernelGGL((aes_gcm_burst_kernel<SEAL, NR>), grid, dim3(kBurstWG), kBurstLds, s, keys, descs, pb.perm,
-                       pb.work, pb.n_work, arena, masks, status, flags);
+                       pb.work, pb.n_work, arena, masks, status, flags, pow);
 }
 }  // namespace
 
@@ -233,17 +263,25 @@ uint32_t burst_packets_per_item(uint32_t n, uint32_t n_cu) {
 
 hipError_t launch_aes_gcm_burst(bool seal, const DevKey *keys, const qpp_pkt *descs, const PlanBuffers &pb,
                                 uint32_t n, uint32_t key_cap, uint32_t per, uint8_t *arena, uint8_t *masks,
-                                int8_t *status, uint32_t flags, uint32_t suites, hipStream_t s) {
+                                int8_t *status, uint32_t flags, uint32_t suites, const PowTables &pow,
+                                hipStream_t s) {
     if (!n) return hipSuccess;
     const dim3 grid(plan_max_work(n, key_cap, per));
     if (suites & (1u << QPP_SUITE_TLS_AES_128_GCM_SHA256)) {
-        if (seal) launch_burst<true, 10>(grid, s, keys, descs, pb, arena, masks, status, flags);
-        else launch_burst<false, 10>(grid, s, keys, descs, pb, arena, masks, status, flags);
+        if (seal) launch_burst<true, 10>(grid, s, keys, descs, pb, arena, masks, status, flags, pow);
+        else launch_burst<false, 10>(grid, s, keys, descs, pb, arena, masks, status, flags, pow);
     }
     if (suites & (1u << QPP_SUITE_TLS_AES_256_GCM_SHA384)) {
-        if (seal) launch_burst<true, 14>(grid, s, keys, descs, pb, arena, masks, status, flags);
-        else launch_burst<false, 14>(grid, s, keys, descs, pb, arena, masks, status, flags);
+        if (seal) launch_burst<true, 14>(grid, s, keys, descs, pb, arena, masks, status, flags, pow);
+        else launch_burst<false, 14>(grid, s, keys, descs, pb, arena, masks, status, flags, pow);
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_pow_setup(const DevKey *keys, const uint32_t *slots, uint32_t count, const PowTables &pow,
+                            hipStream_t s) {
+    if (!count || !pow.cap) return hipSuccess;
+    hipLaunchKernelGGL(pow_setup_kernel, dim3(count), dim3(512), kBurstLds, s, keys, slots, pow);
     return hipGetLastError();
 }
 

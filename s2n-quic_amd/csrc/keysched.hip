@@ -225,13 +225,14 @@ __global__ __launch_bounds__(64) void key_derive_kernel(DevKey *keys, const uint
 uint32_t key_material_bytes() { return kMatBytes; }
 
 hipError_t launch_key_derive(DevKey *keys, const uint32_t *slots, uint32_t n, int suite, const uint8_t *secrets,
-                             const uint8_t *hp_in, uint32_t updates, uint8_t *material, hipStream_t s) {
+                             const uint8_t *hp_in, uint32_t updates, uint8_t *material, const PowTables &pow,
+                             hipStream_t s) {
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(key_derive_kernel, dim3((n + 63) / 64), dim3(64), 0, s, keys, slots, n, suite, secrets, hp_in,
                        updates, material);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    return launch_key_install(keys, slots, nullptr, n, s);
+    return launch_key_install(keys, slots, nullptr, n, pow, s);
 }
 
 }  // namespace qpp

@@ -92,9 +92,20 @@ constexpr uint32_t kWaveKernelPacketsPerKey = 1024;  // batches with fewer packe
 constexpr uint32_t kBurstMaxDefault = 16384;  // AES batches up to this many packets run one wave per packet
 constexpr uint32_t kChachaBurstShift = 2;     // ChaCha20-Poly1305 batches up to burst_max >> 2 do (its lane kernel
                                               // fills the chip with fewer packets: crossover ~6 Ki vs ~20 Ki)
-constexpr uint32_t kTxqZeroCopyMax = 256;     // txq flushes up to this many packets run on the pinned ring in place
+constexpr uint32_t kTxqZeroCopyMax = 1024;    // txq flushes up to this many packets run on the pinned ring in place
+                                              // (coalesced bursts: 512-packet launches were 36 % faster in place)
 constexpr int kDefaultAesVariant = 0;  // see aes_gcm.hip launch_variant
 constexpr int kMaxPlanKeys = 8192;      // keys binned in LDS by the plan kernels (larger tables: global bins)
+
+// Per-key GHASH power tables of the burst kernel (burst.hip): T_t = 4-bit tables of H^(2^t), t = 1..6, 48 KiB per
+// key slot below `cap`, computed when the key is installed (they used to be rebuilt by every workgroup of every
+// burst launch: about half of a 64-packet flush).  Slots >= cap (huge key tables) still build them per launch.
+constexpr uint32_t kPowBytes = 6u * 8192u;
+constexpr uint32_t kPowSlots = 4096;  // at most 192 MiB per context
+struct PowTables {
+    uint8_t *base;  // [cap][kPowBytes]
+    uint32_t cap;
+};
 
 // ---------------------------------------------------------------- launchers (aes_gcm.hip, chacha.hip, plan.hip)
 struct PlanBuffers {
@@ -108,12 +119,13 @@ struct PlanBuffers {
 
 // aes_gcm.hip: records[i] (device, may be nullptr = already in place) -> keys[slots[i]], then H / V[m] for AES keys
 hipError_t launch_key_install(DevKey *keys, const uint32_t *slots, const DevKey *records, uint32_t count,
-                              hipStream_t s);
+                              const PowTables &pow, hipStream_t s);
 // keysched.hip: n secrets -> updates x "quic ku" -> key/iv -> DevKey records keys[slots[i]] and per-key material
 // (secret' | key | iv | hp, key_material_bytes() each); then key install.  The header key is derived from the given
 // secret ("quic hp") when hp_in is nullptr, else taken from hp_in (suite key length per key: update batches).
 hipError_t launch_key_derive(DevKey *keys, const uint32_t *slots, uint32_t n, int suite, const uint8_t *secrets,
-                             const uint8_t *hp_in, uint32_t updates, uint8_t *material, hipStream_t s);
+                             const uint8_t *hp_in, uint32_t updates, uint8_t *material, const PowTables &pow,
+                             hipStream_t s);
 uint32_t key_material_bytes();
 hipError_t launch_plan(const DevKey *keys, uint32_t key_cap, const qpp_pkt *descs, uint32_t n, PlanBuffers pb,
                        uint32_t per, hipStream_t s);
@@ -125,7 +137,10 @@ uint32_t aes_packets_per_item(uint32_t n, uint32_t n_cu);
 uint32_t burst_packets_per_item(uint32_t n, uint32_t n_cu);
 hipError_t launch_aes_gcm_burst(bool seal, const DevKey *keys, const qpp_pkt *descs, const PlanBuffers &pb,
                                 uint32_t n, uint32_t key_cap, uint32_t per, uint8_t *arena, uint8_t *masks,
-                                int8_t *status, uint32_t flags, uint32_t suites, hipStream_t s);
+                                int8_t *status, uint32_t flags, uint32_t suites, const PowTables &pow, hipStream_t s);
+// the burst power tables of keys[slots[i]] (AES packet keys with slot < pow.cap), after their V[m] are in place
+hipError_t launch_pow_setup(const DevKey *keys, const uint32_t *slots, uint32_t count, const PowTables &pow,
+                            hipStream_t s);
 // suites: bit (1 << suite) for every suite with a live key in the context (launches only what can occur)
 hipError_t launch_aes_gcm(bool seal, const DevKey *keys, const qpp_pkt *descs, const PlanBuffers &pb, uint32_t n,
                           uint32_t key_cap, uint32_t per, uint8_t *arena, uint8_t *masks, int8_t *status,

@@ -53,6 +53,7 @@ EXPORTS = [
     "qpp_stream_destroy", "qpp_stream_synchronize", "qpp_event_create", "qpp_event_destroy", "qpp_event_record",
     "qpp_event_elapsed_ms", "qpp_stream_wait_event", "qpp_unprotect_open_batch", "qpp_pn_truncate", "qpp_pn_expand",
     "qpp_key_new_batch", "qpp_txq_create", "qpp_txq_destroy", "qpp_txq_ring", "qpp_txq_push", "qpp_txq_flush",
+    "qpp_txq_create_async", "qpp_txq_flush_async", "qpp_txq_poll", "qpp_txq_wait", "qpp_txq_push_descs", "qpp_txq_set_coalesce",
     "qpp_txq_pending", "qpp_memcpy_d2d", "qpp_ctx_set_burst_max", "qpp_dc_key_new", "qpp_dc_seal", "qpp_dc_open",
     "qpp_dc_open_in_place", "qpp_ctx_key_slots", "qpp_key_new_pair", "qpp_key_update_batch", "qpp_initial_keys_pair",
     "qpp_header_key_new", "qpp_header_key_new_raw", "qpp_header_key_free", "qpp_header_key_slot",
@@ -136,6 +137,12 @@ def lib():
             "qpp_txq_ring": (vp, [vp]),
             "qpp_txq_push": (ctypes.c_int, [vp, vp, u64, sz, sz, sz, sz]),
             "qpp_txq_flush": (ctypes.c_int, [vp]),
+            "qpp_txq_create_async": (ctypes.c_int, [vp, sz, sz, sz, ctypes.POINTER(vp)]),
+            "qpp_txq_flush_async": (ctypes.c_int, [vp, ctypes.POINTER(u64)]),
+            "qpp_txq_poll": (ctypes.c_int, [vp, u64, ctypes.POINTER(ctypes.c_int)]),
+            "qpp_txq_wait": (ctypes.c_int, [vp, u64]),
+            "qpp_txq_push_descs": (ctypes.c_int, [vp, vp, sz]),
+            "qpp_txq_set_coalesce": (ctypes.c_int, [vp, sz]),
             "qpp_txq_pending": (sz, [vp]),
             "qpp_memcpy_d2d": (ctypes.c_int, [vp, vp, vp, sz, vp]),
             "qpp_ctx_set_burst_max": (ctypes.c_int, [vp, sz]),
@@ -625,9 +632,9 @@ def pn_expand(largest_acked, truncated, pn_len):
 class TxQueue:
     """qpp_txq: deferred Key::encrypt + header protection over a pinned ring (the GSO segment buffer)."""
 
-    def __init__(self, ctx, ring_bytes, max_packets):
+    def __init__(self, ctx, ring_bytes, max_packets, in_flight=1):
         h = vp()
-        rc = lib().qpp_txq_create(ctx.handle, ring_bytes, max_packets, ctypes.byref(h))
+        rc = lib().qpp_txq_create_async(ctx.handle, ring_bytes, max_packets, in_flight, ctypes.byref(h))
         if rc != OK:
             raise QppError(rc, "qpp_txq_create")
         self.handle, self.ctx = h.value, ctx
@@ -642,6 +649,38 @@ class TxQueue:
         rc = lib().qpp_txq_flush(self.handle)
         if rc != OK:
             raise QppError(rc, "qpp_txq_flush")
+
+    def push_descs(self, descs):
+        """qpp_txq_push_descs: a PKT_DTYPE array of ready descriptors in one call"""
+        descs = np.ascontiguousarray(descs, dtype=PKT_DTYPE)
+        rc = lib().qpp_txq_push_descs(self.handle, descs.ctypes.data, len(descs))
+        if rc != OK:
+            raise QppError(rc, "qpp_txq_push_descs")
+
+    def set_coalesce(self, bursts):
+        rc = lib().qpp_txq_set_coalesce(self.handle, bursts)
+        if rc != OK:
+            raise QppError(rc, "qpp_txq_set_coalesce")
+
+    def flush_async(self):
+        """qpp_txq_flush_async -> ticket (the pushed packets' ring bytes belong to the engine until it completes)"""
+        t = u64()
+        rc = lib().qpp_txq_flush_async(self.handle, ctypes.byref(t))
+        if rc != OK:
+            raise QppError(rc, "qpp_txq_flush_async")
+        return t.value
+
+    def poll(self, ticket):
+        d = ctypes.c_int()
+        rc = lib().qpp_txq_poll(self.handle, ticket, ctypes.byref(d))
+        if rc != OK:
+            raise QppError(rc, "qpp_txq_poll")
+        return bool(d.value)
+
+    def wait(self, ticket):
+        rc = lib().qpp_txq_wait(self.handle, ticket)
+        if rc != OK:
+            raise QppError(rc, "qpp_txq_wait")
 
     def pending(self):
         return lib().qpp_txq_pending(self.handle)

@@ -573,6 +573,54 @@ def test_txq_deferred_seal_matches_encode_packet(ctx, path, flush, monkeypatch):
         k.free()
 
 
+@pytest.mark.parametrize("coalesce", [1, 3])
+@pytest.mark.parametrize("flush", ["zero_copy", "dma"])
+def test_txq_async_bursts_in_flight(ctx, flush, coalesce, monkeypatch):
+    """GSO bursts flushed without waiting (qpp_txq_flush_async): 24 bursts of 64 packets, up to 8 in flight on the
+    queue's streams, each in its own region of the ring; back-pressure reuses a slot only after its flush is over.
+    Every packet equals crypto::encrypt + crypto::protect of the oracle once its ticket completes."""
+    monkeypatch.setenv("QPP_TXQ_ZC_MAX", "1024" if flush == "zero_copy" else "0")
+    rng = np.random.default_rng(18)
+    keys = [ctx.key(s, rng.integers(0, 256, qpp.HASH_LEN[s], dtype=np.uint8).tobytes()) for s in (1, 2, 3, 1)]
+    region, bursts, per = 96 << 10, 24, 64
+    q = qpp.TxQueue(ctx, region * bursts, per * coalesce, in_flight=8)
+    q.set_coalesce(coalesce)  # bursts held back and sent `coalesce` at a time (poll / wait send a held one at once)
+    largest = int(rng.integers(0, 2**40))
+    want, tickets, pn = [], [], largest + 1
+    for b in range(bursts):
+        off = b * region
+        staged = np.zeros(per, dtype=qpp.PKT_DTYPE)  # odd bursts go in with one qpp_txq_push_descs call
+        for i in range(per):
+            k = keys[(b + i) % len(keys)]
+            trunc, pn_len = qpp.pn_truncate(pn, largest)
+            header = bytes([0x40 | (pn_len - 1)]) + rng.integers(0, 256, 16, dtype=np.uint8).tobytes()
+            payload = rng.integers(0, 256, int(rng.integers(4, 1400)), dtype=np.uint8).tobytes()
+            pkt = header + trunc.to_bytes(pn_len, "big") + payload
+            q.ring[off:off + len(pkt)] = np.frombuffer(pkt, dtype=np.uint8)
+            if b % 2:
+                staged[i] = (pn, k.slot, off, len(header) + pn_len, len(payload), pn_len, 0, 0)
+            else:
+                q.push(k, pn, off, len(header), pn_len, len(payload))
+            suite, (kk, iv, hp) = k.suite, k.material()
+            want.append((off, orc.protect_packet(suite, kk, iv, hp, pn, header, pn_len, payload)[1]))
+            off += len(pkt) + 16
+            pn += 1
+        if b % 2:
+            q.push_descs(staged)
+        assert q.pending() == per
+        tickets.append(q.flush_async())
+        assert q.pending() == 0
+    for t in tickets[::-1]:  # any order
+        q.wait(t)
+        assert q.poll(t)
+    for o, p in want:
+        assert q.ring[o:o + len(p)].tobytes() == p
+    assert q.flush_async() == 0  # nothing pushed: ticket 0, complete
+    q.close()
+    for k in keys:
+        k.free()
+
+
 # ------------------------------------------------------------------ dc consumers (SURVEY §8(f) row 4)
 
 @pytest.mark.parametrize("name,suite", [("aead_aes128gcm.json", 1), ("aead_aes256gcm.json", 2),

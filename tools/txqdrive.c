@@ -1,0 +1,45 @@
+/* txqdrive.c — native driver loop for `bench.py --mode txq --inflight K` (the transport's side of qpp_txq, in C so
+ * that the bench measures the engine and not Python's per-call cost).  Per burst: wait for the ring region's previous
+ * ticket, push `burst` ready descriptors (one qpp_txq_push_descs), qpp_txq_flush_async.  Build: see Makefile.
+ *
+ *   double txq_drive(qpp_txq *q, const qpp_pkt *proto, size_t burst, size_t region_bytes, size_t regions,
+ *                    size_t bursts, uint64_t pn0)  -> seconds for `bursts` bursts (all waited for), < 0 on error
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "../include/qpp.h"
+
+static double now_s(void) {
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
+}
+
+double txq_drive(qpp_txq *q, const qpp_pkt *proto, size_t burst, size_t region_bytes, size_t regions, size_t bursts,
+                 uint64_t pn0) {
+    qpp_pkt *d = (qpp_pkt *)malloc(sizeof(qpp_pkt) * burst);
+    uint64_t *tickets = (uint64_t *)calloc(regions, sizeof(uint64_t));
+    if (!d || !tickets) return -1.0;
+    uint64_t pn = pn0;
+    const double t0 = now_s();
+    for (size_t k = 0; k < bursts; k++) {
+        const size_t r = k % regions;
+        if (qpp_txq_wait(q, tickets[r]) != QPP_OK) return -2.0;  /* the region's previous burst is sent */
+        memcpy(d, proto, sizeof(qpp_pkt) * burst);
+        for (size_t i = 0; i < burst; i++) {
+            d[i].pn = pn++;
+            d[i].off += (uint32_t)(r * region_bytes);
+        }
+        if (qpp_txq_push_descs(q, d, burst) != QPP_OK) return -3.0;
+        if (qpp_txq_flush_async(q, &tickets[r]) != QPP_OK) return -4.0;
+    }
+    for (size_t r = 0; r < regions; r++)
+        if (qpp_txq_wait(q, tickets[r]) != QPP_OK) return -5.0;
+    const double t = now_s() - t0;
+    free(d);
+    free(tickets);
+    return t;
+}

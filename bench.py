@@ -162,6 +162,7 @@ def main():
                          "region")
     ap.add_argument("--pt", type=int, default=1200, help="payload bytes per packet")
     ap.add_argument("--aad", type=int, default=21, help="short header: 0x43 || DCID16 || PN4")
+    ap.add_argument("--stride", type=int, default=0, help="device mode: arena bytes per packet (0: 16-B rounded)")
     ap.add_argument("--keys", type=int, default=1)
     ap.add_argument("--key-run", type=int, default=1,
                     help="consecutive packets per key run (1: every packet's key drawn independently; 64: GSO bursts)")
@@ -171,8 +172,9 @@ def main():
                          "txq: 64-packet GSO-burst flush latency through the transmit queue; packet: per-packet trait-API "
                          "latency")
     ap.add_argument("--cpu-seconds", type=float, default=1.5)
-    ap.add_argument("--pipe", default="262144,384,4",
-                    help="e2e: host pipeline geometry 'packets per chunk,MiB per chunk,chunk buffers'")
+    ap.add_argument("--pipe", default="auto",
+                    help="e2e: host pipeline geometry 'packets per chunk,MiB per chunk,chunk buffers' (auto: the "
+                         "engine's default, chunks sized by batch and key count)")
     ap.add_argument("--inflight", type=int, default=1, help="txq: GSO bursts in flight (qpp_txq_flush_async)")
     ap.add_argument("--coalesce", type=int, default=1, help="txq: bursts sent per launch (qpp_txq_set_coalesce)")
     ap.add_argument("--no-cpu", action="store_true")
@@ -201,7 +203,7 @@ def main():
     sh = multigpu.shard(rank, world, n, seed_base=0x5eed0000 + 1)
     sh["pn_base"] = args.pn_first
     descs, arena = qpp.make_batch(n, pt, [k.slot for k in keys], seed=sh["seed"], aad_len=aad, pn_base=sh["pn_base"],
-                                  run=args.key_run)
+                                  run=args.key_run, stride=args.stride or None)
     flags = (0 if args.no_hp else qpp.HP_MASK_OUT) | (qpp.ONLY_CHACHA if suite == 3 else qpp.ONLY_AES)
     d_desc, d_mask, d_status = ctx.alloc(descs.nbytes), ctx.alloc(5 * n), ctx.alloc(n)
     d_desc.upload(descs)
@@ -269,7 +271,7 @@ def main():
         t = tdb.get(f"{args.suite}/{pt}/{args.keys}")
         if t and n == 1 << 20:
             traffic = {"bytes": t["traffic_bytes"], "per_alg": round(t["traffic_bytes"] / (n * seal_bytes_per_packet(pt, aad)), 3),
-                       "source": "profiles/traffic.json: " + t["source"]}
+                       "fetch": t["fetch_bytes"], "write": t["write_bytes"], "source": "profiles/traffic.json: " + t["source"]}
     except (OSError, ValueError, KeyError):
         traffic = None
     value = payload / (t_max / 1e3) / GiB
@@ -293,7 +295,8 @@ def main():
             },
             "roofline": {
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic["bytes"] if traffic else None,
+                "traffic_detail": traffic,
                 "kernel": (("chacha" if suite == 3 else "aes_gcm") + ("_burst" if n <= burst_max else "")
                            + "_kernel<seal>" + ("" if suite == 3 else " + plan (per seal call)")),
                 "bytes_per_packet": seal_bytes_per_packet(pt, aad),
@@ -366,8 +369,9 @@ def e2e(args, rank, world, local_rank):
         z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
         return ((z ^ (z >> np.uint64(31))) % np.uint64(nk)).astype(np.uint32)
 
-    cp, cmib, cs = (int(x) for x in args.pipe.split(","))
-    ctx.set_host_pipe(cp, cmib << 20, cs)
+    if args.pipe != "auto":
+        cp, cmib, cs = (int(x) for x in args.pipe.split(","))
+        ctx.set_host_pipe(cp, cmib << 20, cs)
     host, descs, stride = _host_batch(ctx, n, pt, aad, conn_of, args.pn_first, 0x5eed0000 + 7919 * rank)
     conn = descs["key_idx"].copy()
     # one submit addresses a 4 GiB window of the arena (qpp_pkt.off is 32-bit): split larger shards into windows

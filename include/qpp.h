@@ -258,7 +258,9 @@ int qpp_host_batch_submit(qpp_ctx *ctx, const qpp_pkt *descs, size_t n, uint8_t 
 int qpp_host_batch_query(qpp_ctx *ctx, uint64_t ticket, int *done);
 /* Blocks until the ticket's batch is back in host memory, then releases the ticket. */
 int qpp_host_batch_wait(qpp_ctx *ctx, uint64_t ticket);
-/* Ring geometry: packets and bytes per chunk, chunk buffers (defaults 262144, 384 MiB, 4).  Waits for the device. */
+/* Ring geometry: packets and bytes per chunk, chunk buffers.  Default: buffers for 262144 packets / 384 MiB, 4 of
+ * them, and each batch cut into ~16 chunks of 64 Ki-256 Ki packets (at least 64 per live AES key); setting a geometry
+ * fixes the chunk size.  Waits for the device. */
 int qpp_ctx_set_host_pipe(qpp_ctx *ctx, size_t chunk_packets, size_t chunk_bytes, size_t slots);
 
 /* ------------------------------------------------------------------ deferred transmit queue */

@@ -56,9 +56,12 @@ struct PipeSlot {
 };
 
 struct HostPipe {
-    // 256 Ki packets per chunk: with 4096 keys a chunk still holds ~64 packets per key (one full wave-item each);
-    // at 64 Ki the C5 pipeline ran 76 ms/step instead of 62 (profiles/r02_e2e.jsonl)
+    // Buffers for chunks of up to 256 Ki packets.  Unless the geometry is set (qpp_ctx_set_host_pipe), a batch is cut
+    // into ~16 chunks of 64-256 Ki packets, and at least 64 packets per live AES key (one full wave-item each): with
+    // 4096 keys, 64 Ki-packet chunks ran the C5 pipeline at 76 ms/step instead of 62; with one key, 256 Ki-packet
+    // chunks made a 1 Mi-packet batch 33 ms instead of 29 (pipeline fill and drain).  profiles/r02_e2e.jsonl
     size_t chunk_packets = 262144, chunk_bytes = 384u << 20, nslots = 4;
+    bool auto_chunk = true;
     hipStream_t h2d = nullptr, comp = nullptr, d2h = nullptr;
     std::vector<PipeSlot> slots;
     size_t next = 0;
@@ -1225,6 +1228,7 @@ int qpp_ctx_set_host_pipe(qpp_ctx *ctx, size_t chunk_packets, size_t chunk_bytes
     ctx->pipe->chunk_packets = chunk_packets;
     ctx->pipe->chunk_bytes = chunk_bytes;
     ctx->pipe->nslots = slots;
+    ctx->pipe->auto_chunk = false;
     return QPP_OK;
 }
 
@@ -1245,13 +1249,19 @@ int qpp_host_batch_submit(qpp_ctx *ctx, const qpp_pkt *descs, size_t n, uint8_t 
     RC_TRY(batch_stream(ctx, p->comp, &st));
     // chunks of consecutive packets: at most chunk_packets, span [lo, hi) of at most chunk_bytes; packets must be in
     // ascending, non-overlapping arena order so that spans of different chunks never overlap
+    size_t cap = p->chunk_packets;
+    if (p->auto_chunk) {
+        const size_t keys = ctx->live_by_suite[QPP_SUITE_TLS_AES_128_GCM_SHA256] +
+                            ctx->live_by_suite[QPP_SUITE_TLS_AES_256_GCM_SHA384];
+        cap = std::min(p->chunk_packets, std::max<size_t>({(n + 15) / 16, 65536, 64 * keys}));
+    }
     size_t i = 0;
     uint64_t prev_end = 0;
     while (i < n) {
         const size_t first = i;
         const uint64_t lo = descs[i].off;
         uint64_t hi = lo;
-        while (i < n && i - first < p->chunk_packets) {
+        while (i < n && i - first < cap) {
             const qpp_pkt &d = descs[i];
             const uint64_t end = (uint64_t)d.off + d.aad_len + d.pt_len + 16;
             if (d.off < prev_end) return QPP_INTERNAL_ERROR;  // out of order or overlapping

@@ -19,5 +19,9 @@ run txq_aes128 --mode txq && \
 run txq_chacha --mode txq --suite chacha20poly1305 && \
 run packet_aes128 --mode packet && \
 run packet_chacha --mode packet --suite chacha20poly1305 && \
+run txq_aes128_32inflight --mode txq --inflight 32 --coalesce 8 && \
+run txq_chacha_64inflight --mode txq --suite chacha20poly1305 --inflight 64 --coalesce 16 && \
 run e2e_aes128 --mode e2e --steps 3 && \
-run e2e_c5_4ki_keys --mode e2e --keys 4096 --packets 2097152 --steps 3
+run e2e_c5_4ki_keys_rotating --mode e2e --keys 4096 --packets 2097152 --rotate --steps 3 && \
+run c2_aes128_keyruns64_64keys --keys 64 --key-run 64 && \
+run c3_aes128_64keys --keys 64

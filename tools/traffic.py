@@ -3,9 +3,13 @@ written to profiles/traffic.json for bench.py's roofline.traffic.
 
     python tools/traffic.py gpurun_out/<prof dir> <workload key, e.g. aes128gcm/1200/1> [profiles/traffic.json]
 
-FETCH_SIZE / WRITE_SIZE are the L2's memory-side request counters (MI355X_MICROARCH.md, HBM/rocprofv3): the bytes
-are reported as counted (KiB x 1024), without the x2 streaming-read correction the guide calibrates for 16-B-per-lane
-coalesced streams -- this kernel's 64-B per-packet chunks are not that pattern, so the raw count is the one stated.
+FETCH_SIZE / WRITE_SIZE are the L2's memory-side request counters (MI355X_MICROARCH.md, HBM/rocprofv3), KiB x 1024.
+The guide's x2 read correction is calibrated for 16-B-per-lane coalesced streams, and tells to calibrate other
+patterns on a known byte count: tools/ubench/copy_pattern.hip moves exactly 1200 B in + 1200 B out per packet with
+this kernel's cooperative 64-B chunks at +21 offsets, and its FETCH_SIZE reads 1.191x the true bytes
+(profiles/r02_copy_pattern_calibration.json, "coop_unaligned"), so fetch = FETCH_SIZE / 1.191.  WRITE_SIZE is taken as
+counted: the same copy reports 1.477x for writes whose 64-B chunks straddle 64-B segments, and those partial-segment
+writes are real memory transactions (the aligned variant of the copy reports 1.115x).
 """
 import csv
 import glob
@@ -22,11 +26,15 @@ def main(d, key, out="profiles/traffic.json"):
             if not (("aes_gcm_kernel<true" in name) or ("chacha_kernel<true" in name)):
                 continue
             acc.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
-    fetch = sum(acc["FETCH_SIZE"]) / len(acc["FETCH_SIZE"]) * 1024
+    fetch_raw = sum(acc["FETCH_SIZE"]) / len(acc["FETCH_SIZE"]) * 1024
     write = sum(acc["WRITE_SIZE"]) / len(acc["WRITE_SIZE"]) * 1024
+    cal = json.load(open("profiles/r02_copy_pattern_calibration.json"))["coop_unaligned"]["fetch_per_alg"]
+    fetch = fetch_raw / cal
     db = json.load(open(out)) if os.path.exists(out) else {}
-    db[key] = {"fetch_bytes": round(fetch), "write_bytes": round(write), "traffic_bytes": round(fetch + write),
-               "source": os.path.basename(os.path.normpath(d)) + " (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, seal kernel)"}
+    db[key] = {"fetch_bytes": round(fetch), "fetch_size_raw_bytes": round(fetch_raw), "fetch_calibration": cal,
+               "write_bytes": round(write), "traffic_bytes": round(fetch + write),
+               "source": os.path.basename(os.path.normpath(d)) + " (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, seal kernel;"
+                         " fetch / " + str(cal) + " per the copy_pattern calibration)"}
     json.dump(db, open(out, "w"), indent=1, sort_keys=True)
     print(key, db[key])
 

@@ -200,6 +200,12 @@ def main():
     rng = np.random.default_rng(0x5eed0000 + 1)
     keys = [ctx.key(suite, rng.integers(0, 256, qpp.HASH_LEN[suite], dtype=np.uint8).tobytes()) for _ in range(args.keys)]
     n, pt, aad = args.packets, args.pt, args.aad
+    if args.mode == "keys":
+        return keys_churn(args, ctx, suite, rank, world, barrier, max_over_ranks)
+    if args.mode == "txq":
+        return txq_bursts(args, ctx, keys, rank, world, max_over_ranks)
+    if args.mode == "packet":
+        return per_packet(args, ctx, keys, rank, world, max_over_ranks)
     sh = multigpu.shard(rank, world, n, seed_base=0x5eed0000 + 1)
     sh["pn_base"] = args.pn_first
     descs, arena = qpp.make_batch(n, pt, [k.slot for k in keys], seed=sh["seed"], aad_len=aad, pn_base=sh["pn_base"],
@@ -211,12 +217,6 @@ def main():
 
     if args.mode == "rx":
         return rx(args, ctx, keys, descs, arena, d_desc, d_mask, d_status, flags, rank, world, barrier, max_over_ranks)
-    if args.mode == "keys":
-        return keys_churn(args, ctx, suite, rank, world, barrier, max_over_ranks)
-    if args.mode == "txq":
-        return txq_bursts(args, ctx, keys, rank, world, max_over_ranks)
-    if args.mode == "packet":
-        return per_packet(args, ctx, keys, rank, world, max_over_ranks)
 
     d_arena = ctx.alloc(arena.nbytes)
     d_arena.upload(arena)

@@ -11,6 +11,9 @@ run c3_chacha_64keys --suite chacha20poly1305 --keys 64 && \
 run c4_aes128_pt300 --pt 300 --packets 4194304 && \
 run c4_aes128_pt1452 --pt 1452 && \
 run c4_aes128_pt8000 --pt 8000 --packets 131072 && \
+run c4_txq_pt300 --mode txq --pt 300 --inflight 32 --coalesce 8 && \
+run c4_txq_pt1452 --mode txq --pt 1452 --inflight 32 --coalesce 8 && \
+run c4_txq_pt8000 --mode txq --pt 8000 --inflight 32 --coalesce 8 && \
 run c5_aes128_4ki_keys --keys 4096 --packets 2097152 && \
 run rx_aes128 --mode rx && \
 run rx_chacha_64keys --mode rx --suite chacha20poly1305 --keys 64 && \

@@ -69,27 +69,6 @@ struct Ghash {
         return lds_ld128(kLdsGhash + __builtin_amdgcn_perm(wk, lc[K], sel[I]));
     }
     // (Z * H) ^ c in natural word order, from W = rot(Z)
-#ifdef QPP_GHASH_SPLIT
-    // Two halves of 8 lookups: the second half's addresses are made to depend on the first half's sum (an empty
-    // asm), so at most 8 ds_read_b128 results (32 VGPRs) are live per step instead of 16 (64 VGPRs).
-    __device__ __forceinline__ static uint32_t after(uint32_t v, uint32_t dep) {
-        asm volatile("; ghash split" : "+v"(v) : "v"(dep));
-        return v;
-    }
-    __device__ __forceinline__ uint4 prod(const uint4 &w, uint4 c) const {
-        const uint4 a = xor3(look<0, 0>(w), look<0, 1>(w), look<0, 2>(w));
-        const uint4 b = xor3(look<0, 3>(w), look<1, 0>(w), look<1, 1>(w));
-        const uint4 d = xor3(look<1, 2>(w), look<1, 3>(w), c);
-        const uint4 h1 = xor3(a, b, d);
-        uint4 w2 = w;
-        w2.z = after(w.z, h1.x);
-        w2.w = after(w.w, h1.x);
-        const uint4 e = xor3(look<2, 0>(w2), look<2, 1>(w2), look<2, 2>(w2));
-        const uint4 f = xor3(look<2, 3>(w2), look<3, 0>(w2), look<3, 1>(w2));
-        const uint4 g = xor3(look<3, 2>(w2), look<3, 3>(w2), h1);
-        return xor3(e, f, g);
-    }
-#else
     __device__ __forceinline__ uint4 prod(const uint4 &w, uint4 c) const {
         const uint4 a = xor3(look<0, 0>(w), look<0, 1>(w), look<0, 2>(w));
         const uint4 b = xor3(look<0, 3>(w), look<1, 0>(w), look<1, 1>(w));
@@ -100,7 +79,6 @@ struct Ghash {
         const uint4 h = xor3(e, f, look<3, 3>(w));
         return xor3(g, h, c);
     }
-#endif
     // one chain step: W' = rot(Z * H ^ c)
     __device__ __forceinline__ uint4 mulx(const uint4 &w, uint4 c) const { return rot(prod(w, c)); }
 };
@@ -201,18 +179,18 @@ __device__ __forceinline__ uint4 ghash_aad_w(const GH &gh, const uint8_t *aad, u
 }
 
 // One packet per lane (has = false: the lane only helps with the wave's cooperative I/O).  Counter blocks are
-// grouped [NB*g, NB*g + NB) with NB | 256, so a group never crosses a 256-block page (CtrPage constants hold for
-// the whole group) and the packet runs through ONE loop body:
-//   counter 0: unused (its keystream is discarded), counter 1: J0 -> E_K(J0) masks the tag,
-//   counter b + 2: data block b.
-// The GHASH steps of group g-1 are issued in the same basic block as the keystream of group g, so the two
-// independent dependency chains overlap.
+// grouped [NB*g + 1, NB*g + NB + 1): counter 1 is J0 (E_K(J0) masks the tag), counter b + 2 is data block b, so a
+// packet of n blocks takes ceil((n + 1) / NB) groups (75 blocks: 19 groups of 4, not 20 with a discarded counter 0).
+// A group normally lies inside one 256-block page (CtrPage constants hold for all of it); the group that straddles a
+// page boundary (packets of >= 253 blocks, once per 256) is wave-uniform and takes full AES rounds.
+// The GHASH steps of group g-1 are issued in the same loop body as the keystream of group g, so the two independent
+// dependency chains overlap.
 template <int NR, int NB, bool SEAL, typename GH>
 __device__ __forceinline__ void process_packet(const AesLds &aes, const GH &gh, const Stage<NB> &st,
                                                const DevKey *__restrict__ key, const uint32_t *__restrict__ rk,
                                                bool has, const qpp_pkt &d, uint32_t pkt_index, uint8_t *arena,
                                                uint8_t *masks, int8_t *status, uint32_t flags) {
-    static_assert(NB >= 2 && (256 % NB) == 0, "NB must divide 256 (and hold counter 1)");
+    static_assert(NB >= 2 && (256 % NB) == 0, "NB must divide 256");
     PacketView p = load_packet(d, key, arena);
     if (!has) p.len = 0;
     uint8_t *pay = p.base + p.aad_len;
@@ -222,7 +200,7 @@ __device__ __forceinline__ void process_packet(const AesLds &aes, const GH &gh, 
 
     const int nfull = (int)(p.len >> 4), rem = (int)(p.len & 15);
     const int nblk = nfull + (rem ? 1 : 0);
-    const int ngroups = has ? (nblk + 2 + NB - 1) / NB : 0;
+    const int ngroups = has ? (nblk + 1 + NB - 1) / NB : 0;
     const int G = (int)wave_max((uint32_t)ngroups);  // the wave runs the longest packet's groups
 
     // cooperative roles: payload offset and length of the packet whose chunk this lane moves in instruction i
@@ -234,11 +212,11 @@ __device__ __forceinline__ void process_packet(const AesLds &aes, const GH &gh, 
         co_len[i] = (uint32_t)__shfl((int)p.len, (int)st.coop_src(i), 64);
         co_k[i] = st.coop_chunk(i);
     }
-    // chunk of block b = NB g - 2 + k, clamped inside payload||tag (its value is unused when out of range)
+    // chunk of block b = NB g - 1 + k, clamped inside payload||tag (its value is unused when out of range)
     auto co_load = [&](int g, uint4 (&v)[NB]) {
 #pragma unroll
         for (int i = 0; i < NB; i++) {
-            const int b = NB * g - 2 + (int)co_k[i];
+            const int b = NB * g - 1 + (int)co_k[i];
             const bool ok = b >= 0 && 16 * b <= (int)co_len[i];
             v[i] = ld16(arena + co_off[i] + (ok ? 16u * (uint32_t)b : 0u));
         }
@@ -252,7 +230,7 @@ __device__ __forceinline__ void process_packet(const AesLds &aes, const GH &gh, 
     auto co_store = [&](int g, const uint4 (&v)[NB]) {
 #pragma unroll
         for (int i = 0; i < NB; i++) {
-            const int b = NB * g - 2 + (int)co_k[i];
+            const int b = NB * g - 1 + (int)co_k[i];
             if (b >= 0 && b < (int)(co_len[i] >> 4)) st16(arena + co_off[i] + 16u * (uint32_t)b, v[i]);
         }
     };
@@ -274,44 +252,38 @@ __device__ __forceinline__ void process_packet(const AesLds &aes, const GH &gh, 
         for (int j = 0; j < NB; j++) in[j] = lds_ld128(st.own(j));
         co_load(g + 1, cin);  // prefetch the next group (latency hidden by this group's AES)
 
-        const uint32_t c = (uint32_t)(NB * g);
-        if ((c >> 8) != pg.page) pg.build(aes, rk, p.n0, p.n1, p.n2, c >> 8);
+        const uint32_t c = (uint32_t)(NB * g + 1);  // counter of slot 0 (wave-uniform)
+        if (((c + NB - 1) >> 8) == (c >> 8)) {
+            if ((c >> 8) != pg.page) pg.build(aes, rk, p.n0, p.n1, p.n2, c >> 8);
 #ifdef QPP_AES_NOPIPE
-        ctr_keystream<NR, NB>(aes, pg, rk, c, ks);
+            ctr_keystream<NR, NB>(aes, pg, rk, c, ks);
 #else
-        ctr_keystream_pipe<NR, NB>(aes, pg, rk, c, ks);  // +3-4 % over the scheduler's own order
+            ctr_keystream_pipe<NR, NB>(aes, pg, rk, c, ks);  // +3-4 % over the scheduler's own order
 #endif
-#ifndef QPP_LEAN
+        } else {  // straddles a page boundary: plain rounds (unrolled: a runtime index into ks[] would make the
+                  // compiler move the array to LDS, on top of the 160 KiB the launch reserves)
+            static_for<NB>([&](auto jc) {
+                constexpr int j = decltype(jc)::value;
+                ks[j] = aes.encrypt<NR>(make_uint4(p.n0, p.n1, p.n2, bswap32(c + j)), rk);
+            });
+        }
         // GHASH of the previous group (independent of the keystream just issued)
 #pragma unroll
         for (int j = 0; j < NB; j++)
             if (bprev + j >= 0 && bprev + j < nblk) z = gh.mulx(z, cprev[j]);
-        if (g == 0) ek0 = ks[1];
-#endif
-        const int b0 = NB * g - 2;  // data block of slot 0
+        if (g == 0) ek0 = ks[0];
+        const int b0 = NB * g - 1;  // data block of slot 0
 #pragma unroll
         for (int j = 0; j < NB; j++) {
             const int b = b0 + j;
             const uint4 out = in[j] ^ ks[j];
             lds_st128(st.own(j), out);  // full blocks leave through the cooperative store below
-#ifdef QPP_LEAN
-            // lean form: this group's GHASH right away (no deferred ciphertext registers)
-            if (b >= 0 && b < nfull) {
-                z = gh.mulx(z, SEAL ? out : in[j]);
-            } else if (b == nfull && rem) {
-                const uint4 o = keep_bytes(out, rem);
-                st_bytes(pay + 16 * b, o, rem);
-                z = gh.mulx(z, SEAL ? o : keep_bytes(in[j], rem));
-            }
-#else
-            if (b >= 0 && b < nfull) {
-                cprev[j] = SEAL ? out : in[j];
-            } else if (b == nfull && rem) {
+            cprev[j] = SEAL ? out : in[j];  // (unused unless 0 <= b < nblk)
+            if (b == nfull && rem) {
                 const uint4 o = keep_bytes(out, rem);
                 st_bytes(pay + 16 * b, o, rem);
                 cprev[j] = SEAL ? o : keep_bytes(in[j], rem);
             }
-#endif
         }
         bprev = b0;
         wave_lds_sync();
@@ -323,15 +295,9 @@ __device__ __forceinline__ void process_packet(const AesLds &aes, const GH &gh, 
         co_store(G - 1, co_out);
         wave_lds_sync();  // the next packet pass reuses the staging area
     }
-#ifdef QPP_LEAN
-    (void)cprev;
-    (void)bprev;
-    ek0 = aes.encrypt<NR>(make_uint4(p.n0, p.n1, p.n2, bswap32(1u)), rk);  // E_K(J0), recomputed: 4 fewer VGPRs
-#else
 #pragma unroll
     for (int j = 0; j < NB; j++)
         if (bprev + j >= 0 && bprev + j < nblk) z = gh.mulx(z, cprev[j]);
-#endif
     if (!has) return;
     // length block: be64(aad bits) || be64(payload bits); tag = Y * H ^ E_K(J0)
     z = gh.mulx(z, make_uint4(0, bswap32(p.aad_len * 8), 0, bswap32(p.len * 8)));

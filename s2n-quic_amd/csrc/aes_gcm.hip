@@ -222,7 +222,7 @@ __device__ __forceinline__ void process_packet(const AesLds &aes, const GH &gh, 
         }
     };
 
-    uint4 ks[NB], cin[NB], cprev[NB], ek0 = make_uint4(0, 0, 0, 0);
+    uint4 ks[NB], cin[NB], cprev[NB], ek0 = make_uint4(0, 0, 0, 0), smp = make_uint4(0, 0, 0, 0);
     int bprev = -NB;  // first block index of the previous group (for its GHASH validity)
     // Cooperative stores of group g-1 are issued at the top of iteration g, AFTER this group's prefetched loads
     // have been consumed: vmcnt counts loads and stores together, so a store issued behind a prefetch would make
@@ -267,11 +267,29 @@ __device__ __forceinline__ void process_packet(const AesLds &aes, const GH &gh, 
                 ks[j] = aes.encrypt<NR>(make_uint4(p.n0, p.n1, p.n2, bswap32(c + j)), rk);
             });
         }
-        // GHASH of the previous group (independent of the keystream just issued)
+        // GHASH of the previous group (independent of the keystream just issued).  Inside the packets (every lane's
+        // NB blocks valid: all but the first and last groups of a uniform batch) the steps run branch-free, so the
+        // word rotation is a select and no exec-mask bookkeeping surrounds each step.
+        if (__all(bprev >= 0 && bprev + NB <= nblk)) {
 #pragma unroll
-        for (int j = 0; j < NB; j++)
-            if (bprev + j >= 0 && bprev + j < nblk) z = gh.mulx(z, cprev[j]);
-        if (g == 0) ek0 = ks[0];
+            for (int j = 0; j < NB; j++) z = gh.mulx(z, cprev[j]);
+        } else {
+#pragma unroll
+            for (int j = 0; j < NB; j++)
+                if (bprev + j >= 0 && bprev + j < nblk) z = gh.mulx(z, cprev[j]);
+        }
+        if (g == 0) {
+            ek0 = ks[0];
+            // header-protection sample = ciphertext bytes [4 - pn_len, 20 - pn_len) (payload.rs:151-169), from
+            // blocks 0 and 1 (slots 1 and 2 of group 0) while they are in registers; packets whose sample reaches
+            // into the tag (payload < 20 - pn_len bytes) read it back from memory at the end instead
+            if constexpr (SEAL && NB >= 3) {
+                const uint4 o1 = in[1] ^ ks[1], o2 = in[2] ^ ks[2];
+                const uint32_t sh = (4u - p.pn_len) & 3u;
+                smp = make_uint4(__builtin_amdgcn_alignbyte(o1.y, o1.x, sh), __builtin_amdgcn_alignbyte(o1.z, o1.y, sh),
+                                 __builtin_amdgcn_alignbyte(o1.w, o1.z, sh), __builtin_amdgcn_alignbyte(o2.x, o1.w, sh));
+            }
+        }
         const int b0 = NB * g - 1;  // data block of slot 0
 #pragma unroll
         for (int j = 0; j < NB; j++) {
@@ -295,6 +313,13 @@ __device__ __forceinline__ void process_packet(const AesLds &aes, const GH &gh, 
         co_store(G - 1, co_out);
         wave_lds_sync();  // the next packet pass reuses the staging area
     }
+    // HP round keys and header bytes: loads issued here, used after the last GHASH steps
+    constexpr int HNR = NR == 10 ? 10 : 14;
+    const bool hp = SEAL && (flags & (QPP_HP_MASK_OUT | QPP_HP_APPLY)) && has && p.pn_len >= 1 && p.pn_len <= 4 &&
+                    p.len >= 4 - p.pn_len;
+    const uint32_t hdr_len = p.aad_len - p.pn_len;
+    HpPrefetch<HNR> hpk;
+    if (hp) hpk.load(key->hp_rk, p.base, hdr_len, flags);
 #pragma unroll
     for (int j = 0; j < NB; j++)
         if (bprev + j >= 0 && bprev + j < nblk) z = gh.mulx(z, cprev[j]);
@@ -307,18 +332,16 @@ __device__ __forceinline__ void process_packet(const AesLds &aes, const GH &gh, 
         st16(pay + p.len, tag);
         int8_t st = QPP_OK;
         if (flags & (QPP_HP_MASK_OUT | QPP_HP_APPLY)) {
-            // sample = ciphertext||tag bytes [4 - pn_len, 20 - pn_len)  (payload.rs:151-169), read back from memory:
-            // full ciphertext blocks 0 and 1 were stored by OTHER lanes of this wave (cooperative co_store), the tail
-            // and the tag by this lane, so the wave's stores are ordered before this load by a wavefront fence
-            const uint32_t s = 4 - p.pn_len;
-            if (p.pn_len < 1 || p.pn_len > 4 || p.len < s) {
+            if (!hp) {
                 st = QPP_DECODE_ERROR;
             } else {
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-                const uint4 smp = ld16(pay + s);
-                const uint32_t hdr_len = p.aad_len - p.pn_len;
-                hp_finish<NR == 10 ? 10 : 14>(aes, key->hp_rk, smp, p.base, hdr_len, p.pn_len,
-                                              masks + 5 * (size_t)pkt_index, flags);
+                if (NB < 3 || p.len < 20 - p.pn_len) {
+                    // the sample reaches into the tag: read ciphertext||tag back (blocks 0/1 were stored by OTHER
+                    // lanes of this wave, the tail and the tag by this lane: a wavefront fence orders them first)
+                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                    smp = ld16(pay + 4 - p.pn_len);
+                }
+                hpk.finish(aes, smp, p.base, hdr_len, p.pn_len, masks + 5 * (size_t)pkt_index, flags);
             }
         }
         if (status) status[pkt_index] = st;
@@ -474,11 +497,14 @@ hipError_t launch_key_install(DevKey *keys, const uint32_t *slots, const DevKey 
 namespace {
 // (blocks per lane-iteration NB, workgroup size WG, packets per work item PER) variants; QPP_AES_VARIANT=<index>
 // selects one (tuning knob).  One workgroup per CU (tables + staging fill the 160 KiB LDS), so
-// WG = waves per CU x 64.
+// WG = waves per CU x 64.  Items of up to 1024 packets: 4096-packet items (variant 5) make a 1-key 1 Mi batch one round of
+// 256 workgroups (1.5-2 % faster), but with 64 keys every key's remainder item spills into a second round
+// (1.71 -> 2.70 ms per seal), so the smaller item stays the default.
 struct Variant {
     int nb, wg, per;
 };
-constexpr Variant kVariants[] = {{4, 512, 1024}, {2, 1024, 1024}, {2, 512, 1024}, {4, 256, 1024}, {2, 768, 1536}};
+constexpr Variant kVariants[] = {{4, 512, 1024}, {2, 1024, 1024}, {2, 512, 1024}, {4, 256, 1024}, {2, 768, 1536},
+                                  {4, 512, 4096}};
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 constexpr uint32_t lds_bytes(int nb, int wg) {
     return kLdsStage + (uint32_t)(wg / 64) * 1024u * (uint32_t)nb;
@@ -496,6 +522,7 @@ void launch_variant(int v, dim3 grid, hipStream_t s, const DevKey *keys, const q
         case 2: { QPP_AES_LAUNCH(2, 512); break; }
         case 3: { QPP_AES_LAUNCH(4, 256); break; }
         case 4: { QPP_AES_LAUNCH(2, 768); break; }
+        case 5:
         default: { QPP_AES_LAUNCH(4, 512); break; }
     }
 #undef QPP_AES_LAUNCH

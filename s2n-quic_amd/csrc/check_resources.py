@@ -1,0 +1,28 @@
+"""Build-time check of the kernel resource remarks (-Rpass-analysis=kernel-resource-usage, one .res file per .hip).
+
+The AES-GCM kernels reserve the whole 160 KiB of LDS dynamically, so any static LDS the compiler adds (e.g. a private
+array it promotes to LDS because of a runtime index) makes every launch fail with an invalid-allocation error; and
+the default variants must not touch scratch memory.  usage: python3 check_resources.py *.res"""
+import re
+import sys
+
+bad = []
+for path in sys.argv[1:]:
+    name = None
+    for line in open(path, errors="replace"):
+        m = re.search(r"remark: Function Name: (\S+)", line)
+        if m:
+            name = m.group(1)
+            continue
+        if not name:
+            continue
+        lds = re.search(r"LDS Size \[bytes/block\]: (\d+)", line)
+        scr = re.search(r"ScratchSize \[bytes/lane\]: (\d+)", line)
+        dyn_lds = "aes_gcm_kernel" in name or "aes_gcm_wave_kernel" in name
+        default = "aes_gcm_wave_kernel" in name or re.search(r"aes_gcm_kernelILb[01]ELi4ELi512E", name)
+        if lds and dyn_lds and int(lds.group(1)) != 0:
+            bad.append(f"{name}: {lds.group(1)} B of static LDS on top of the dynamic 160 KiB")
+        if scr and default and int(scr.group(1)) != 0:
+            bad.append(f"{name}: {scr.group(1)} B/lane of scratch")
+if bad:
+    sys.exit("kernel resource check failed:\n  " + "\n  ".join(bad))

@@ -309,31 +309,44 @@ __device__ __forceinline__ void hdr_apply(uint8_t *base, uint32_t hdr_len, uint3
 }
 
 // Header protection mask from the 16-byte sample (first 5 bytes of AES_hp(sample)).  The HP round keys are read
-// here, once per packet, into VGPRs: hoisted into SGPRs for the whole kernel they pushed the packet round keys out
-// of SGPRs (measured: 36 SGPR spills and per-iteration round-key reloads, a slower seal).
+// once per packet into VGPRs: hoisted into SGPRs for the whole kernel they pushed the packet round keys out of
+// SGPRs (measured: 36 SGPR spills and per-iteration round-key reloads, a slower seal).  Split in two so that a
+// caller can issue the key and header loads early and let their latency pass under other work.
+template <int HNR>
+struct HpPrefetch {
+    uint32_t rk[4 * (HNR + 1)];
+    HdrBytes h;
+    __device__ __forceinline__ void load(const uint32_t *hp_rk_g, const uint8_t *base, uint32_t hdr_len,
+                                         uint32_t flags) {
+        // launder the pointer through a VGPR: the loads below cannot be hoisted or kept in SGPRs
+        uint64_t a = (uint64_t)hp_rk_g;
+        asm volatile("" : "+v"(a));
+        const uint4 *src = (const uint4 *)a;
+#pragma unroll
+        for (int i = 0; i < HNR + 1; i++) {
+            const uint4 v = src[i];
+            rk[4 * i] = v.x; rk[4 * i + 1] = v.y; rk[4 * i + 2] = v.z; rk[4 * i + 3] = v.w;
+        }
+        h = (flags & QPP_HP_APPLY) ? hdr_load(base, hdr_len) : HdrBytes{0, 0};
+    }
+    __device__ __forceinline__ void finish(const AesLds &aes, uint4 sample, uint8_t *base, uint32_t hdr_len,
+                                           uint32_t pn_len, uint8_t *mask_out, uint32_t flags) const {
+        const uint4 m = aes.encrypt<HNR>(sample, rk);
+        if (flags & QPP_HP_MASK_OUT) {
+            mask_out[0] = (uint8_t)m.x; mask_out[1] = (uint8_t)(m.x >> 8); mask_out[2] = (uint8_t)(m.x >> 16);
+            mask_out[3] = (uint8_t)(m.x >> 24); mask_out[4] = (uint8_t)m.y;
+        }
+        if (flags & QPP_HP_APPLY) hdr_apply(base, hdr_len, pn_len, h, m.x, m.y);  // header_crypto.rs:80-95
+    }
+};
+
 template <int HNR>
 __device__ __forceinline__ void hp_finish(const AesLds &aes, const uint32_t *hp_rk_g, uint4 sample,
                                           uint8_t *base, uint32_t hdr_len, uint32_t pn_len, uint8_t *mask_out,
                                           uint32_t flags) {
-    // launder the pointer through a VGPR: the loads below cannot be hoisted or kept in SGPRs
-    uint64_t a = (uint64_t)hp_rk_g;
-    asm volatile("" : "+v"(a));
-    const uint4 *src = (const uint4 *)a;
-    uint32_t hp_rk[4 * (HNR + 1)];
-#pragma unroll
-    for (int i = 0; i < HNR + 1; i++) {
-        const uint4 v = src[i];
-        hp_rk[4 * i] = v.x; hp_rk[4 * i + 1] = v.y; hp_rk[4 * i + 2] = v.z; hp_rk[4 * i + 3] = v.w;
-    }
-    const HdrBytes h = (flags & QPP_HP_APPLY) ? hdr_load(base, hdr_len) : HdrBytes{0, 0};
-    uint4 m = aes.encrypt<HNR>(sample, hp_rk);
-    if (flags & QPP_HP_MASK_OUT) {
-        mask_out[0] = (uint8_t)m.x; mask_out[1] = (uint8_t)(m.x >> 8); mask_out[2] = (uint8_t)(m.x >> 16);
-        mask_out[3] = (uint8_t)(m.x >> 24); mask_out[4] = (uint8_t)m.y;
-    }
-    if (flags & QPP_HP_APPLY) {
-        hdr_apply(base, hdr_len, pn_len, h, m.x, m.y);  // header_crypto.rs:80-95
-    }
+    HpPrefetch<HNR> hp;
+    hp.load(hp_rk_g, base, hdr_len, flags);
+    hp.finish(aes, sample, base, hdr_len, pn_len, mask_out, flags);
 }
 
 // ---------------------------------------------------------------- per-wave payload staging

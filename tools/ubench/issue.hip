@@ -34,7 +34,8 @@ int main(int argc, char **argv) {
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
-    const int blocks = 256 * 8, iters = 8192;
+    const int bpc = argc > 2 ? atoi(argv[2]) : 8;  // 256-thread blocks per CU (2: 2 waves per SIMD)
+    const int blocks = 256 * bpc, iters = 8192;
     const char *names[] = {"v_xor_b32", "v_add_u32", "v_alignbit_b32", "v_bitop3_b32", "v_perm_b32", "v_mul_lo_u32"};
     for (int op = 0; op < 6; op++) {
         for (int rep = 0; rep < 3; rep++) {
@@ -54,7 +55,7 @@ int main(int argc, char **argv) {
             const double wi = (double)blocks * 4 * iters * 8;  // 4 waves per block, 8 instructions per iteration
             const double per_ns = wi / (ms * 1e6);
             if (rep == 2)
-                printf("%-16s %.3f ms  %.0f wave-instr/ns chip-wide  %.2f cycles/wave-instr/SIMD at %.2f GHz\n", names[op],
+                printf("bpc %d %-16s %.3f ms  %.0f wave-instr/ns chip-wide  %.2f cycles/wave-instr/SIMD at %.2f GHz\n", bpc, names[op],
                        ms, per_ns, 1024.0 * ghz / per_ns, ghz);
         }
     }

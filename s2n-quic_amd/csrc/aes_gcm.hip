@@ -359,33 +359,53 @@ __device__ __forceinline__ void process_packet(const AesLds &aes, const GH &gh, 
     }
 }
 
+// One workgroup per CU (grid = CUs), each with an equal slice of the key-sorted packet list (perm): the slice may
+// cross key boundaries, and the workgroup rebuilds its tables per key segment.  Fixed per-key work items instead made
+// every key's remainder a workgroup of its own: 64 keys x ~16 Ki packets were 1088 items of <= 1024 on 256 CUs, and
+// the last quarter round ran alone.  meta (plan_scan): {items, AES-128 items, AES-128 packets, AES-256 packets};
+// work[] holds one item per key (begin = its first perm index), AES-128 keys first.
 template <bool SEAL, int NB, int WG, int NR>
 __global__ __launch_bounds__(WG) void aes_gcm_kernel(const DevKey *__restrict__ keys, const qpp_pkt *__restrict__ descs,
                                                     const uint32_t *__restrict__ perm, const WorkItem *__restrict__ work,
-                                                    const uint32_t *__restrict__ n_work, uint8_t *__restrict__ arena,
+                                                    const uint32_t *__restrict__ meta, uint8_t *__restrict__ arena,
                                                     uint8_t *masks, int8_t *status, uint32_t flags) {
     // dynamic LDS (tables + this variant's staging, reserved by the launch), addressed by offset (lds_ld32 / lds_ld128)
-    if (blockIdx.x >= *n_work) return;  // uniform: grid is sized for the worst case
-    const WorkItem w = work[blockIdx.x];
-    if (w.nr != NR) return;  // AES-128 and AES-256 work items are served by separate launches (SGPR budget)
-    const DevKey *__restrict__ key = keys + w.key;
-    build_tables(key);
+    const uint32_t items = meta[0], i10 = meta[1], n10 = meta[2], n14 = meta[3];
+    const uint32_t i_lo = NR == 10 ? 0 : i10, i_hi = NR == 10 ? i10 : items;
+    const uint32_t p0 = NR == 10 ? 0 : n10, n = NR == 10 ? n10 : n14;
+    const uint32_t P = ((n + gridDim.x - 1) / gridDim.x + 63u) & ~63u;  // whole waves per slice
+    uint32_t lo = p0 + min(n, blockIdx.x * P);
+    const uint32_t hi = p0 + min(n, (blockIdx.x + 1) * P);
+    if (lo >= hi) return;  // uniform
+    uint32_t i = i_lo, j = i_hi;  // the item holding lo: largest i with work[i].begin <= lo
+    while (j - i > 1) {
+        const uint32_t m = (i + j) >> 1;
+        if (work[m].begin <= lo) i = m; else j = m;
+    }
     const AesLds aes = make_aes(kLdsAes);
     const Ghash gh = Ghash::make();
-    // packet round keys in SGPRs for the whole work item (uniform: one key per workgroup)
-    uint32_t rk[4 * (NR + 1)];
-#pragma unroll
-    for (int i = 0; i < 4 * (NR + 1); i++) rk[i] = __builtin_amdgcn_readfirstlane(key->rk[i]);
     Stage<NB> st;
     st.lane = threadIdx.x & 63u;
     st.base = kLdsStage + (threadIdx.x >> 6) * (64u * 16u * NB);
-    for (uint32_t t0 = 0; t0 < w.count; t0 += WG) {  // WG < 1024: several passes over the work item
-        const uint32_t t = t0 + threadIdx.x;
-        const bool real = t < w.count;
-        const uint32_t pi = real ? perm[w.begin + t] : 0;
-        const qpp_pkt d = descs[pi];  // (any valid descriptor for helper lanes)
-        const bool has = real && !(d.flags & QPP_PKT_SKIP);
-        process_packet<NR, NB, SEAL>(aes, gh, st, key, rk, has, d, pi, arena, masks, status, flags);
+    for (; lo < hi; i++) {  // key segments of the slice
+        const WorkItem w = work[i];
+        const uint32_t end = min(hi, w.begin + w.count);
+        const DevKey *__restrict__ key = keys + w.key;
+        __syncthreads();  // every wave is done with the previous segment's tables
+        build_tables(key);
+        // packet round keys in SGPRs for the whole segment (uniform: one key per workgroup)
+        uint32_t rk[4 * (NR + 1)];
+#pragma unroll
+        for (int r = 0; r < 4 * (NR + 1); r++) rk[r] = __builtin_amdgcn_readfirstlane(key->rk[r]);
+        for (uint32_t t0 = lo; t0 < end; t0 += WG) {
+            const uint32_t t = t0 + threadIdx.x;
+            const bool real = t < end;
+            const uint32_t pi = perm[real ? t : lo];
+            const qpp_pkt d = descs[pi];  // (any valid descriptor for helper lanes)
+            const bool has = real && !(d.flags & QPP_PKT_SKIP);
+            process_packet<NR, NB, SEAL>(aes, gh, st, key, rk, has, d, pi, arena, masks, status, flags);
+        }
+        lo = end;
     }
 }
 
@@ -495,16 +515,12 @@ hipError_t launch_key_install(DevKey *keys, const uint32_t *slots, const DevKey 
 }
 
 namespace {
-// (blocks per lane-iteration NB, workgroup size WG, packets per work item PER) variants; QPP_AES_VARIANT=<index>
-// selects one (tuning knob).  One workgroup per CU (tables + staging fill the 160 KiB LDS), so
-// WG = waves per CU x 64.  Items of up to 1024 packets: 4096-packet items (variant 5) make a 1-key 1 Mi batch one round of
-// 256 workgroups (1.5-2 % faster), but with 64 keys every key's remainder item spills into a second round
-// (1.71 -> 2.70 ms per seal), so the smaller item stays the default.
+// (blocks per lane-iteration NB, workgroup size WG) variants; QPP_AES_VARIANT=<index> selects one (tuning knob,
+// DESIGN.md §4).  One workgroup per CU (tables + staging fill the 160 KiB LDS), so WG = waves per CU x 64.
 struct Variant {
-    int nb, wg, per;
+    int nb, wg;
 };
-constexpr Variant kVariants[] = {{4, 512, 1024}, {2, 1024, 1024}, {2, 512, 1024}, {4, 256, 1024}, {2, 768, 1536},
-                                  {4, 512, 4096}};
+constexpr Variant kVariants[] = {{4, 512}, {2, 1024}, {2, 512}, {4, 256}, {2, 768}};
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 constexpr uint32_t lds_bytes(int nb, int wg) {
     return kLdsStage + (uint32_t)(wg / 64) * 1024u * (uint32_t)nb;
@@ -522,7 +538,6 @@ void launch_variant(int v, dim3 grid, hipStream_t s, const DevKey *keys, const q
         case 2: { QPP_AES_LAUNCH(2, 512); break; }
         case 3: { QPP_AES_LAUNCH(4, 256); break; }
         case 4: { QPP_AES_LAUNCH(2, 768); break; }
-        case 5:
         default: { QPP_AES_LAUNCH(4, 512); break; }
     }
 #undef QPP_AES_LAUNCH
@@ -537,20 +552,6 @@ int aes_variant() {
     return v;
 }
 }  // namespace
-
-uint32_t aes_packets_per_item(uint32_t n, uint32_t n_cu) {
-    // rounds of one-workgroup-per-CU residency the batch needs at the variant's item size; then the smallest whole-wave
-    // item size that still fits the batch in that many rounds.  (128 Ki packets at 1024 per item were 128 items on
-    // 256 CUs: half the chip idle, 0.63x the rate of the balanced split.)
-    const uint32_t full = (uint32_t)kVariants[aes_variant()].per;
-    if (!n_cu) return full;
-    const uint64_t slots = (uint64_t)n_cu * full;
-    const uint64_t rounds = (n + slots - 1) / slots;
-    uint64_t per = (n + (uint64_t)n_cu * rounds - 1) / ((uint64_t)n_cu * rounds);
-    per = (per + 63) & ~uint64_t(63);
-    if (per < (uint64_t)kMinPacketsPerItem) per = kMinPacketsPerItem;
-    return per > full ? full : (uint32_t)per;
-}
 
 hipError_t launch_aes_gcm_wave(bool seal, const DevKey *keys, const qpp_pkt *descs, const PlanBuffers &pb, uint32_t n,
                                uint32_t key_cap, uint32_t n_cu, uint8_t *arena, uint8_t *masks, int8_t *status,
@@ -578,10 +579,12 @@ hipError_t launch_aes_gcm_wave(bool seal, const DevKey *keys, const qpp_pkt *des
 }
 
 hipError_t launch_aes_gcm(bool seal, const DevKey *keys, const qpp_pkt *descs, const PlanBuffers &pb, uint32_t n,
-                          uint32_t key_cap, uint32_t per, uint8_t *arena, uint8_t *masks, int8_t *status,
-                          uint32_t flags, uint32_t suites, hipStream_t s) {
+                          uint32_t n_cu, uint8_t *arena, uint8_t *masks, int8_t *status, uint32_t flags,
+                          uint32_t suites, hipStream_t s) {
     if (!n) return hipSuccess;
-    const dim3 grid(plan_max_work(n, key_cap, per));
+    // one slice per CU; a batch smaller than a wave per CU takes fewer workgroups
+    const uint32_t waves = (n + 63) / 64;
+    const dim3 grid(waves < n_cu ? waves : n_cu);
     const int v = aes_variant();
     if (suites & (1u << QPP_SUITE_TLS_AES_128_GCM_SHA256)) {
         if (seal) launch_variant<true, 10>(v, grid, s, keys, descs, pb, arena, masks, status, flags);

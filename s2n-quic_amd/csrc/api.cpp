@@ -309,10 +309,10 @@ int ensure_plan(qpp_ctx *ctx, StreamState *st, uint32_t n) {
     // on top of stale words and the scatter wrote past perm[] -- an illegal address under two concurrent streams.)
     HIP_TRY(ctx, hipMemsetAsync(p.counts, 0, sizeof(uint32_t) * kcap, st->stream));  // plan_scan re-zeroes it after each plan
     HIP_TRY(ctx, hipMalloc(&p.cursor, sizeof(uint32_t) * kcap));
-    HIP_TRY(ctx, hipMalloc(&p.istart, sizeof(uint32_t) * (kcap + 1)));
+    HIP_TRY(ctx, hipMalloc(&p.istart, sizeof(uint32_t) * 2 * (kcap + 1)));
     HIP_TRY(ctx, hipMalloc(&p.perm, sizeof(uint32_t) * std::max<uint32_t>(ncap, 1)));
     HIP_TRY(ctx, hipMalloc(&p.work, sizeof(WorkItem) * (plan_max_work(ncap, kcap, kMinPacketsPerItem) + 1)));
-    HIP_TRY(ctx, hipMalloc(&p.n_work, sizeof(uint32_t)));
+    HIP_TRY(ctx, hipMalloc(&p.n_work, 4 * sizeof(uint32_t)));
     st->plan_n_cap = ncap;
     st->plan_key_cap = kcap;
     return QPP_OK;
@@ -468,7 +468,7 @@ AesPath aes_path(const qpp_ctx *ctx, uint32_t n) {
 uint32_t aes_per_item(const qpp_ctx *ctx, AesPath p, uint32_t n) {
     return p == AesPath::burst ? burst_packets_per_item(n, ctx->n_cu)
            : p == AesPath::wave ? kWavePacketsPerItem
-                                : aes_packets_per_item(n, ctx->n_cu);
+                                : kLanePerItem;
 }
 hipError_t launch_aes(const qpp_ctx *ctx, AesPath p, bool seal, const qpp_pkt *descs, const PlanBuffers &pb, uint32_t n,
                       uint8_t *arena, uint8_t *masks, int8_t *status, uint32_t flags, hipStream_t s) {
@@ -481,7 +481,7 @@ hipError_t launch_aes(const qpp_ctx *ctx, AesPath p, bool seal, const qpp_pkt *d
             return launch_aes_gcm_wave(seal, ctx->d_keys, descs, pb, n, ctx->key_cap, ctx->n_cu, arena, masks, status,
                                        flags, suite_mask(ctx), s);
         default:
-            return launch_aes_gcm(seal, ctx->d_keys, descs, pb, n, ctx->key_cap, per, arena, masks, status, flags,
+            return launch_aes_gcm(seal, ctx->d_keys, descs, pb, n, ctx->n_cu, arena, masks, status, flags,
                                   suite_mask(ctx), s);
     }
 }
@@ -518,8 +518,8 @@ int enqueue_open(qpp_ctx *ctx, StreamState *st, const qpp_pkt *descs, uint32_t n
 }
 
 // One packet through the batch kernels, zero-copy: the kernel reads and writes the pinned stage directly (no DMA
-// copies; one launch, one wait).  Stage layout: descriptor @0 | perm @32 | n_work @36 | work item @48 | status @64
-// | mask @80 | packet @kOnePkt = [pad 16 | header | payload | tag].
+// copies; one launch, one wait).  Stage layout: descriptor @0 | perm @32 | plan meta @36 (4 words) | work item @52
+// | status @72 | mask @80 | packet @kOnePkt = [pad 16 | header | payload | tag].
 constexpr size_t kOnePkt = 128;
 int run_one(const qpp_key *k, bool seal, uint64_t pn, const uint8_t *header, size_t header_len, const uint8_t *payload,
             size_t payload_len, uint8_t *out, uint8_t *tag_out, int8_t *status_out) {
@@ -543,22 +543,27 @@ int run_one(const qpp_key *k, bool seal, uint64_t pn, const uint8_t *header, siz
     d.off = 16;
     d.aad_len = (uint16_t)header_len;
     d.pt_len = (uint16_t)payload_len;
+    const uint32_t nr = ctx->h_keys[k->slot].nr;
     *(uint32_t *)(h + 32) = 0;  // perm = {0}
-    *(uint32_t *)(h + 36) = 1;  // one work item, on this key
-    *(WorkItem *)(h + 48) = WorkItem{k->slot, 0, 1, ctx->h_keys[k->slot].nr};
-    h[64] = (uint8_t)QPP_INTERNAL_ERROR;  // overwritten by the kernel
-    const PlanBuffers pb{nullptr, nullptr, nullptr, (uint32_t *)(v + 32), (WorkItem *)(v + 48), (uint32_t *)(v + 36)};
+    uint32_t *meta = (uint32_t *)(h + 36);  // one work item, on this key, in its AES size's class
+    meta[0] = 1;
+    meta[1] = nr == 10 ? 1 : 0;
+    meta[2] = nr == 10 ? 1 : 0;
+    meta[3] = nr == 10 ? 0 : 1;
+    *(WorkItem *)(h + 52) = WorkItem{k->slot, 0, 1, nr};
+    h[72] = (uint8_t)QPP_INTERNAL_ERROR;  // overwritten by the kernel
+    const PlanBuffers pb{nullptr, nullptr, nullptr, (uint32_t *)(v + 32), (WorkItem *)(v + 52), (uint32_t *)(v + 36)};
     hipStream_t s = ctx->stream;
     const qpp_pkt *vd = (const qpp_pkt *)v;
-    int8_t *vst = (int8_t *)(v + 64);
+    int8_t *vst = (int8_t *)(v + 72);
     if (is_aes(k->suite)) {
         // key_cap = 0: grid = plan_max_work(1, 0, per) = 1; only work item 0 exists
         if (ctx->burst_max)
             HIP_TRY(ctx, launch_aes_gcm_burst(seal, ctx->d_keys, vd, pb, 1, 0, 1, v + kOnePkt, v + 80, vst, 0,
                                               1u << k->suite, ctx->pow, s));
         else
-            HIP_TRY(ctx, launch_aes_gcm(seal, ctx->d_keys, vd, pb, 1, 0, 1, v + kOnePkt, v + 80, vst, 0,
-                                        1u << k->suite, s));
+            HIP_TRY(ctx, launch_aes_gcm(seal, ctx->d_keys, vd, pb, 1, 1, v + kOnePkt, v + 80, vst, 0, 1u << k->suite,
+                                        s));
     } else {
         HIP_TRY(ctx, launch_chacha(seal, ctx->d_keys, ctx->key_cap, vd, 1, v + kOnePkt, v + 80, vst, 0,
                                    ctx->burst_max > 0, s));
@@ -567,7 +572,7 @@ int run_one(const qpp_key *k, bool seal, uint64_t pn, const uint8_t *header, siz
     HIP_TRY(ctx, hipStreamSynchronize(s));
     memcpy(out, pkt + 16 + header_len, payload_len);
     if (seal) memcpy(tag_out, pkt + 16 + header_len + payload_len, 16);
-    *status_out = (int8_t)h[64];
+    *status_out = (int8_t)h[72];
     secure_zero(h, total);
     return QPP_OK;
 }

@@ -15,8 +15,11 @@ namespace {
 constexpr int kPlanBlock = 1024;
 constexpr uint32_t kPlanPerThread = 4;  // packets per thread in plan_hist / plan_scatter (amortises the per-block bins)
 
+// a live AES packet key (freed slots, header-key-only slots and ChaCha keys are not planned; the ChaCha kernel, which
+// visits every packet, reports the refused ones)
 __device__ __forceinline__ bool is_aes(const DevKey *keys, uint32_t k) {
-    return keys[k].suite != QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256;
+    const DevKey &d = keys[k];
+    return d.live == 1 && d.suite != QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256 && (d.nr == 10 || d.nr == 14);
 }
 
 // key_cap <= kMaxPlanKeys: bins in LDS.  Larger key tables use global atomics directly.
@@ -58,50 +61,59 @@ __global__ __launch_bounds__(kPlanBlock) void plan_hist(const DevKey *__restrict
 // Single workgroup.  Exclusive scans over keys of (a) packet counts -> cursor (scatter base per key) and
 // (b) work items per key -> istart; then every thread emits work items w = tid, tid+1024, ... by a binary
 // search of istart (in LDS), so a single key with 16 Ki work items is not written by one lane.
+// Class-major: the AES-128 keys' packets and items come first, then the AES-256 keys' (two scans), so each AES size's
+// launch sees one contiguous range of perm and of the work list.  meta = {items, AES-128 items, AES-128 packets,
+// AES-256 packets}.
 __global__ __launch_bounds__(kPlanBlock) void plan_scan(const DevKey *__restrict__ keys, uint32_t key_cap,
                                                        uint32_t *__restrict__ counts, uint32_t *__restrict__ cursor,
                                                        uint32_t *__restrict__ istart_g, WorkItem *__restrict__ work,
-                                                       uint32_t *__restrict__ n_work, uint32_t per) {
+                                                       uint32_t *__restrict__ meta, uint32_t per) {
     __shared__ uint32_t sc[kPlanBlock], si[kPlanBlock];
-    __shared__ uint32_t istart_l[kMaxPlanKeys + 1];
-    __shared__ uint32_t carry_c, carry_i;
+    __shared__ uint32_t istart_l[2 * (kMaxPlanKeys + 1)];
+    __shared__ uint32_t carry_c, carry_i, cls_i[2], cls_c[2];
     const bool local = key_cap <= (uint32_t)kMaxPlanKeys;
-    uint32_t *istart = local ? istart_l : istart_g;
+    uint32_t *istart = local ? istart_l : istart_g;  // [2][key_cap + 1]: per class, non-decreasing in k
     if (threadIdx.x == 0) { carry_c = 0; carry_i = 0; }
     __syncthreads();
-    for (uint32_t base = 0; base < key_cap; base += kPlanBlock) {
-        const uint32_t k = base + threadIdx.x;
-        const uint32_t c = k < key_cap ? counts[k] : 0;
-        const uint32_t items = (c + per - 1) / per;
-        sc[threadIdx.x] = c;
-        si[threadIdx.x] = items;
-        __syncthreads();
-        for (uint32_t off = 1; off < kPlanBlock; off <<= 1) {  // Hillis-Steele inclusive scan
-            uint32_t a = threadIdx.x >= off ? sc[threadIdx.x - off] : 0;
-            uint32_t b = threadIdx.x >= off ? si[threadIdx.x - off] : 0;
+    for (uint32_t cls = 0; cls < 2; cls++) {
+        uint32_t *ist = istart + cls * (key_cap + 1);
+        for (uint32_t base = 0; base < key_cap; base += kPlanBlock) {
+            const uint32_t k = base + threadIdx.x;
+            uint32_t c = k < key_cap ? counts[k] : 0;
+            if (c && (keys[k].nr == 14) != (cls == 1)) c = 0;  // the other class's key
+            const uint32_t items = c ? (c - 1) / per + 1 : 0;
+            sc[threadIdx.x] = c;
+            si[threadIdx.x] = items;
             __syncthreads();
-            sc[threadIdx.x] += a;
-            si[threadIdx.x] += b;
+            for (uint32_t off = 1; off < kPlanBlock; off <<= 1) {  // Hillis-Steele inclusive scan
+                uint32_t a = threadIdx.x >= off ? sc[threadIdx.x - off] : 0;
+                uint32_t b = threadIdx.x >= off ? si[threadIdx.x - off] : 0;
+                __syncthreads();
+                sc[threadIdx.x] += a;
+                si[threadIdx.x] += b;
+                __syncthreads();
+            }
+            if (k < key_cap) {
+                if (c) cursor[k] = carry_c + sc[threadIdx.x] - c;
+                ist[k] = carry_i + si[threadIdx.x] - items;
+            }
+            __syncthreads();
+            if (threadIdx.x == kPlanBlock - 1) { carry_c += sc[threadIdx.x]; carry_i += si[threadIdx.x]; }
             __syncthreads();
         }
-        if (k < key_cap) {
-            cursor[k] = carry_c + sc[threadIdx.x] - c;
-            istart[k] = carry_i + si[threadIdx.x] - items;
-        }
-        __syncthreads();
-        if (threadIdx.x == kPlanBlock - 1) { carry_c += sc[threadIdx.x]; carry_i += si[threadIdx.x]; }
+        if (threadIdx.x == 0) { ist[key_cap] = carry_i; cls_i[cls] = carry_i; cls_c[cls] = carry_c; }
         __syncthreads();
     }
-    const uint32_t total = carry_i;
-    if (threadIdx.x == 0) { istart[key_cap] = total; *n_work = total; }
-    __syncthreads();
+    const uint32_t total = cls_i[1], i10 = cls_i[0];
+    if (threadIdx.x == 0) { meta[0] = total; meta[1] = i10; meta[2] = cls_c[0]; meta[3] = cls_c[1] - cls_c[0]; }
     for (uint32_t w = threadIdx.x; w < total; w += kPlanBlock) {
-        uint32_t lo = 0, hi = key_cap;  // largest k with istart[k] <= w (keys with no items share a start)
+        const uint32_t *ist = istart + (w >= i10 ? key_cap + 1 : 0);
+        uint32_t lo = 0, hi = key_cap;  // largest k with ist[k] <= w (keys with no items share a start)
         while (hi - lo > 1) {
             const uint32_t mid = (lo + hi) >> 1;
-            if (istart[mid] <= w) lo = mid; else hi = mid;
+            if (ist[mid] <= w) lo = mid; else hi = mid;
         }
-        const uint32_t i = w - istart[lo];
+        const uint32_t i = w - ist[lo];
         const uint32_t left = counts[lo] - i * per;
         // cursor[] still holds the key's first perm index: plan_scatter runs after this kernel
         work[w] = WorkItem{lo, cursor[lo] + i * per, left < per ? left : per, keys[lo].nr};
@@ -161,17 +173,17 @@ __global__ __launch_bounds__(kPlanBlock) void plan_scatter(const DevKey *__restr
 // Small batches (n <= kPlanSmallMax = 8 Ki, key_cap <= kMaxPlanKeys): the three stages above in ONE workgroup and one
 // launch (a GSO burst pays ~4 us here instead of a memset + three launches, ~17 us).  Each thread keeps the keys
 // of its <= 8 packets in registers; keys are scanned 8 per thread with a wave scan + a 16-entry workgroup scan.
-// Dynamic LDS: cur[kMaxPlanKeys + 1] (counts, then scatter cursors), ist[kMaxPlanKeys + 1] (first work item),
-// wave totals.
+// Dynamic LDS: counts / scatter cursors, start cursors, first work item per key and class, wave totals.
 constexpr uint32_t kPlanSmallMax = 8 * kPlanBlock;  // (at 16 Ki the one workgroup took ~18 us more than the 3 launches)
-constexpr uint32_t kPlanSmallLds = 4 * (2 * (kMaxPlanKeys + 1) + 64);
+constexpr uint32_t kPlanSmallLds = 4 * (4 * (kMaxPlanKeys + 1) + 64);
 
 __global__ __launch_bounds__(kPlanBlock) void plan_small(const DevKey *__restrict__ keys, uint32_t key_cap,
                                                         const qpp_pkt *__restrict__ descs, uint32_t n,
                                                         uint32_t *__restrict__ perm, WorkItem *__restrict__ work,
                                                         uint32_t *__restrict__ n_work, uint32_t per) {
     extern __shared__ uint32_t smem[];
-    uint32_t *cur = smem, *ist = smem + kMaxPlanKeys + 1, *wt = ist + kMaxPlanKeys + 1;  // wt: [2][16]
+    // cur[kMaxPlanKeys + 1] (counts, then scatter cursors) | start cursors | ist2[2][kMaxPlanKeys + 1] | wt[2][16]
+    uint32_t *cur = smem, *ist2 = smem + 2 * (kMaxPlanKeys + 1), *wt = ist2 + 2 * (kMaxPlanKeys + 1);
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     for (uint32_t k = tid; k <= key_cap; k += kPlanBlock) cur[k] = 0;
     __syncthreads();
@@ -188,50 +200,70 @@ __global__ __launch_bounds__(kPlanBlock) void plan_small(const DevKey *__restric
         mine[j] = k;
     }
     __syncthreads();
-    // exclusive scans over keys of counts (-> cursors) and work items (-> ist), kpt consecutive keys per thread
+    // exclusive scans over keys of counts (-> cursors) and work items (-> ist), kpt consecutive keys per thread,
+    // class-major (AES-128 keys first, then AES-256: see plan_scan); ist[cls][k] non-decreasing in k per class
     const uint32_t kpt = (key_cap + kPlanBlock - 1) / kPlanBlock, k0 = tid * kpt;
-    uint32_t lc = 0, li = 0;
-    for (uint32_t j = 0; j < kpt; j++) {
-        const uint32_t c = k0 + j < key_cap ? cur[k0 + j] : 0;
-        lc += c;
-        li += (c + per - 1) / per;
-    }
-    uint32_t sc = lc, si = li;  // inclusive wave scan
+    uint32_t cnt[2], itm[2];  // class totals
+    uint32_t *st0 = smem + kMaxPlanKeys + 1;  // start cursors (cur[] is reused for the counts until the scans end)
+    for (uint32_t cls = 0; cls < 2; cls++) {
+        uint32_t *ist = ist2 + cls * (kMaxPlanKeys + 1);
+        const uint32_t cb = cls ? cnt[0] : 0, ib = cls ? itm[0] : 0;
+        auto cnt_of = [&](uint32_t k) -> uint32_t {
+            const uint32_t c = cur[k];
+            return c && (keys[k].nr == 14) == (cls == 1) ? c : 0;
+        };
+        uint32_t lc = 0, li = 0;
+        for (uint32_t j = 0; j < kpt; j++) {
+            const uint32_t c = k0 + j < key_cap ? cnt_of(k0 + j) : 0;
+            lc += c;
+            li += c ? (c - 1) / per + 1 : 0;
+        }
+        uint32_t sc = lc, si = li;  // inclusive wave scan
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t a = (uint32_t)__shfl_up((int)sc, o, 64), b = (uint32_t)__shfl_up((int)si, o, 64);
-        if (lane >= (uint32_t)o) { sc += a; si += b; }
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t a = (uint32_t)__shfl_up((int)sc, o, 64), b = (uint32_t)__shfl_up((int)si, o, 64);
+            if (lane >= (uint32_t)o) { sc += a; si += b; }
+        }
+        if (lane == 63) { wt[wave] = sc; wt[16 + wave] = si; }
+        __syncthreads();
+        uint32_t bc = 0, bi = 0, tc = 0, ti = 0;
+        for (uint32_t w = 0; w < kPlanBlock / 64; w++) {
+            if (w < wave) { bc += wt[w]; bi += wt[16 + w]; }
+            tc += wt[w];
+            ti += wt[16 + w];
+        }
+        __syncthreads();  // wt[] is rewritten by the next class
+        uint32_t pc = cb + bc + sc - lc, pw = ib + bi + si - li;  // exclusive prefixes at this thread's first key
+        for (uint32_t j = 0; j < kpt; j++) {  // each thread writes only its own keys
+            const uint32_t k = k0 + j;
+            if (k >= key_cap) break;
+            const uint32_t c = cnt_of(k);
+            if (c) st0[k] = pc;
+            ist[k] = pw;
+            pc += c;
+            pw += c ? (c - 1) / per + 1 : 0;
+        }
+        cnt[cls] = cb + tc;
+        itm[cls] = ib + ti;
+        if (tid == 0) ist[key_cap] = itm[cls];
     }
-    if (lane == 63) { wt[wave] = sc; wt[16 + wave] = si; }
     __syncthreads();
-    uint32_t bc = 0, bi = 0, tc = 0, ti = 0;
-    for (uint32_t w = 0; w < kPlanBlock / 64; w++) {
-        if (w < wave) { bc += wt[w]; bi += wt[16 + w]; }
-        tc += wt[w];
-        ti += wt[16 + w];
-    }
-    uint32_t pc = bc + sc - lc, pw = bi + si - li;  // exclusive prefixes at this thread's first key
-    for (uint32_t j = 0; j < kpt; j++) {  // each thread rewrites only its own keys
-        const uint32_t k = k0 + j;
-        if (k >= key_cap) break;
-        const uint32_t c = cur[k];
-        cur[k] = pc;
-        ist[k] = pw;
-        pc += c;
-        pw += (c + per - 1) / per;
-    }
-    if (tid == 0) { cur[key_cap] = tc; ist[key_cap] = ti; *n_work = ti; }
-    __syncthreads();
+    const uint32_t ti = itm[1], i10 = itm[0];
+    if (tid == 0) { n_work[0] = ti; n_work[1] = i10; n_work[2] = cnt[0]; n_work[3] = cnt[1] - cnt[0]; }
     for (uint32_t w = tid; w < ti; w += kPlanBlock) {
+        const uint32_t *ist = ist2 + (w >= i10 ? kMaxPlanKeys + 1 : 0);
         uint32_t lo = 0, hi = key_cap;  // largest k with ist[k] <= w (keys without items share a start)
         while (hi - lo > 1) {
             const uint32_t mid = (lo + hi) >> 1;
             if (ist[mid] <= w) lo = mid; else hi = mid;
         }
         const uint32_t i = w - ist[lo];
-        const uint32_t left = cur[lo + 1] - cur[lo] - i * per;
-        work[w] = WorkItem{lo, cur[lo] + i * per, left < per ? left : per, keys[lo].nr};
+        const uint32_t left = cur[lo] - i * per;
+        work[w] = WorkItem{lo, st0[lo] + i * per, left < per ? left : per, keys[lo].nr};
     }
+    __syncthreads();  // the counts are read by the work items; from here cur[] holds the scatter cursors
+    for (uint32_t k = tid; k < key_cap; k += kPlanBlock)
+        if (cur[k]) cur[k] = st0[k];
     __syncthreads();  // the work items read the cursors' start values; the scatter advances them
 #pragma unroll
     for (uint32_t j = 0; j < kPlanSmallMax / kPlanBlock; j++)

@@ -88,7 +88,8 @@ struct WorkItem {
 
 constexpr int kMinPacketsPerItem = 4;
 constexpr uint32_t kWavePacketsPerItem = 64;  // aes_gcm_wave_kernel: one wave, one key, <= 64 packets per work item
-constexpr uint32_t kWaveKernelPacketsPerKey = 1024;  // batches with fewer packets per live AES key take the wave kernel    // smallest AES work item: burst kernel, one packet per wave (plan scratch)
+constexpr uint32_t kWaveKernelPacketsPerKey = 1024;  // batches with fewer packets per live AES key take the wave kernel
+constexpr uint32_t kLanePerItem = 0x7fffffffu;  // aes_gcm_kernel: one work item per key (workgroups take equal slices)
 constexpr uint32_t kBurstMaxDefault = 16384;  // AES batches up to this many packets run one wave per packet
 constexpr uint32_t kChachaBurstShift = 2;     // ChaCha20-Poly1305 batches up to burst_max >> 2 do (its lane kernel
                                               // fills the chip with fewer packets: crossover ~6 Ki vs ~20 Ki)
@@ -111,10 +112,10 @@ struct PowTables {
 struct PlanBuffers {
     uint32_t *counts;   // [key_cap] packets per key
     uint32_t *cursor;   // [key_cap] scatter cursors
-    uint32_t *istart;   // [key_cap + 1] first work item per key (used when key_cap > kMaxPlanKeys)
+    uint32_t *istart;   // [2][key_cap + 1] first work item per key and AES size (used when key_cap > kMaxPlanKeys)
     uint32_t *perm;     // [n_cap] packet indices grouped by key
     WorkItem *work;     // [n_cap / kMinPacketsPerItem + key_cap + 1]
-    uint32_t *n_work;   // [1]
+    uint32_t *n_work;   // [4] plan meta: work items, AES-128 items, AES-128 packets, AES-256 packets
 };
 
 // aes_gcm.hip: records[i] (device, may be nullptr = already in place) -> keys[slots[i]], then H / V[m] for AES keys
@@ -130,9 +131,6 @@ uint32_t key_material_bytes();
 hipError_t launch_plan(const DevKey *keys, uint32_t key_cap, const qpp_pkt *descs, uint32_t n, PlanBuffers pb,
                        uint32_t per, hipStream_t s);
 uint32_t plan_max_work(uint32_t n, uint32_t key_cap, uint32_t per);
-// AES work-item size for an n-packet batch on n_cu compute units: the selected variant's size, shrunk (in whole
-// waves) so that the work items fill every CU in balanced rounds when n is small (one workgroup per CU).
-uint32_t aes_packets_per_item(uint32_t n, uint32_t n_cu);
 // burst.hip: one wave per packet for small batches (GSO bursts); work items of whole waves, <= 64 packets
 uint32_t burst_packets_per_item(uint32_t n, uint32_t n_cu);
 hipError_t launch_aes_gcm_burst(bool seal, const DevKey *keys, const qpp_pkt *descs, const PlanBuffers &pb,
@@ -142,9 +140,10 @@ hipError_t launch_aes_gcm_burst(bool seal, const DevKey *keys, const qpp_pkt *de
 hipError_t launch_pow_setup(const DevKey *keys, const uint32_t *slots, uint32_t count, const PowTables &pow,
                             hipStream_t s);
 // suites: bit (1 << suite) for every suite with a live key in the context (launches only what can occur)
+// plan with per = kLanePerItem; one workgroup per CU, each an equal slice of the key-sorted packets
 hipError_t launch_aes_gcm(bool seal, const DevKey *keys, const qpp_pkt *descs, const PlanBuffers &pb, uint32_t n,
-                          uint32_t key_cap, uint32_t per, uint8_t *arena, uint8_t *masks, int8_t *status,
-                          uint32_t flags, uint32_t suites, hipStream_t s);
+                          uint32_t n_cu, uint8_t *arena, uint8_t *masks, int8_t *status, uint32_t flags,
+                          uint32_t suites, hipStream_t s);
 // many keys: work items of <= kWavePacketsPerItem packets (plan with per = kWavePacketsPerItem), one wave each
 hipError_t launch_aes_gcm_wave(bool seal, const DevKey *keys, const qpp_pkt *descs, const PlanBuffers &pb, uint32_t n,
                                uint32_t key_cap, uint32_t n_cu, uint8_t *arena, uint8_t *masks, int8_t *status,

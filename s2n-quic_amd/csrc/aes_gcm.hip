@@ -231,7 +231,7 @@ __device__ __forceinline__ void process_packet(const AesLds &aes, const GH &gh, 
 #pragma unroll
         for (int i = 0; i < NB; i++) {
             const int b = NB * g - 1 + (int)co_k[i];
-            if (b >= 0 && b < (int)(co_len[i] >> 4)) st16(arena + co_off[i] + 16u * (uint32_t)b, v[i]);
+            if (b >= 0 && b < (int)(co_len[i] >> 4)) st16_nt(arena + co_off[i] + 16u * (uint32_t)b, v[i]);
         }
     };
     co_load(0, cin);

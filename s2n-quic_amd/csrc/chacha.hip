@@ -188,7 +188,7 @@ __global__ __launch_bounds__(256) void chacha_kernel(const DevKey *__restrict__ 
 #pragma unroll
         for (int i = 0; i < 4; i++) {
             const uint32_t o = 16u * (4u * c + co_k[i]);
-            if (o + 16 <= co_len[i]) st16(arena + co_off[i] + o, v[i]);
+            if (o + 16 <= co_len[i]) st16_nt(arena + co_off[i] + o, v[i]);
         }
     };
     uint4 cin[4], cb[4];

@@ -272,6 +272,8 @@ def main():
         if t and n == 1 << 20:
             traffic = {"bytes": t["traffic_bytes"], "per_alg": round(t["traffic_bytes"] / (n * seal_bytes_per_packet(pt, aad)), 3),
                        "fetch": t["fetch_bytes"], "write": t["write_bytes"], "source": "profiles/traffic.json: " + t["source"]}
+            if t.get("note"):
+                traffic["note"] = t["note"]
     except (OSError, ValueError, KeyError):
         traffic = None
     value = payload / (t_max / 1e3) / GiB

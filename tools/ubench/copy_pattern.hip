@@ -5,6 +5,8 @@
 //   1 aligned  : the same pattern with every chunk 64-B aligned (1280-B stride, payload at +64, chunk = blocks 4g..4g+3)
 //   2 stream   : in-place 16 B per lane over the same payload bytes, consecutive lanes consecutive (the guide's
 //                calibrated case)
+//   3 coop_nt  : mode 0 with streaming (nt) stores, as the kernels store their payload chunks since round 2
+//   4 coop_read: mode 0's loads only (one dword per packet written), for the read-side calibration alone
 // Algorithmic traffic is the same in all modes: 1200 B read + 1200 B written per packet.
 // usage: copy_pattern <mode> [packets] [reps]   (prints mode, ms per launch, algorithmic GB)
 #include <hip/hip_runtime.h>
@@ -20,6 +22,12 @@ __device__ __forceinline__ uint4 ld16(const uint8_t *p) {
     return v;
 }
 __device__ __forceinline__ void st16(uint8_t *p, uint4 v) { __builtin_memcpy(p, &v, 16); }
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st16_nt(uint8_t *p, uint4 v) {
+    u32x4 t;
+    t.x = v.x; t.y = v.y; t.z = v.z; t.w = v.w;
+    __builtin_nontemporal_store(t, (u32x4 *)p);
+}
 
 template <int MODE>
 __global__ __launch_bounds__(256) void copy_kernel(uint8_t *arena, uint32_t n, uint32_t stride, uint32_t pay_off) {
@@ -38,16 +46,22 @@ __global__ __launch_bounds__(256) void copy_kernel(uint8_t *arena, uint32_t n, u
     const uint32_t first = wave * 64;
     if (first >= n) return;
     const int groups = (kPay / 16 + 2 + 3) / 4;
+    uint32_t acc = 0;
     for (int g = 0; g < groups; g++) {
 #pragma unroll
         for (int i = 0; i < 4; i++) {           // wave instruction i: lane-group q = lane / 4 moves packet 16 i + q
             const uint32_t p = first + 16 * i + lane / 4;
-            const int b = MODE == 0 ? 4 * g - 2 + (int)(lane & 3) : 4 * g + (int)(lane & 3);
+            const int b = MODE != 1 ? 4 * g - 2 + (int)(lane & 3) : 4 * g + (int)(lane & 3);
             if (p >= n || b < 0 || 16 * (b + 1) > kPay) continue;
             uint8_t *q = arena + (size_t)p * stride + pay_off + 16 * b;
-            st16(q, ld16(q) ^ make_uint4(0x01010101u, 0, 0, p));
+            const uint4 v = ld16(q);
+            if (MODE == 4) acc += v.x ^ v.y ^ v.z ^ v.w;
+            else if (MODE == 3) st16_nt(q, v ^ make_uint4(0x01010101u, 0, 0, p));
+            else st16(q, v ^ make_uint4(0x01010101u, 0, 0, p));
         }
     }
+    if (MODE == 4 && lane < 16 && first + lane < n)  // keeps the loads; 4 B per 4 packets, noise in WRITE_SIZE
+        *(uint32_t *)(arena + (size_t)(first + lane) * stride) = acc;
 }
 
 int main(int argc, char **argv) {
@@ -67,6 +81,8 @@ int main(int argc, char **argv) {
         hipEventRecord(e0, 0);
         if (mode == 0) hipLaunchKernelGGL(copy_kernel<0>, grid, block, 0, 0, arena, n, stride, pay_off);
         else if (mode == 1) hipLaunchKernelGGL(copy_kernel<1>, grid, block, 0, 0, arena, n, stride, pay_off);
+        else if (mode == 3) hipLaunchKernelGGL(copy_kernel<3>, grid, block, 0, 0, arena, n, stride, pay_off);
+        else if (mode == 4) hipLaunchKernelGGL(copy_kernel<4>, grid, block, 0, 0, arena, n, stride, pay_off);
         else hipLaunchKernelGGL(copy_kernel<2>, grid, block, 0, 0, arena, n, stride, pay_off);
         hipEventRecord(e1, 0);
         hipEventSynchronize(e1);

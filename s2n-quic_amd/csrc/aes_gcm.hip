@@ -37,13 +37,14 @@ using namespace dev;
 // {4-11,16-19,28-31}, and the same + 32) the lanes have distinct r, hence distinct j: one LDS cycle per group.
 // The word part of that order is a rotation of Z's words by q (W[k] = Z.w[(k + q) & 3], two v_cndmask levels),
 // the byte part a per-lane v_perm selector; the address (x << 8 | j << 4) is that one v_perm.
-struct Ghash {
+template <bool PIPE>
+struct GhashT {
     uint32_t lc[4];   // byte i of lc[k] = 16 * j(k, i)
     uint32_t sel[4];  // v_perm selector of step i: byte0 <- lc[k].b_i, byte1 <- W[k].b_((i+b)&3), bytes 2,3 <- 0
     bool q1, q2;      // word rotation by q = q1 + 2 q2
 
-    __device__ __forceinline__ static Ghash make() {
-        Ghash g;
+    __device__ __forceinline__ static GhashT make() {
+        GhashT g;
         const uint32_t r = threadIdx.x & 15u, q = r >> 2, b = r & 3u;
 #pragma unroll
         for (int k = 0; k < 4; k++) {
@@ -68,20 +69,52 @@ struct Ghash {
         const uint32_t wk = K == 0 ? w.x : K == 1 ? w.y : K == 2 ? w.z : w.w;
         return lds_ld128(kLdsGhash + __builtin_amdgcn_perm(wk, lc[K], sel[I]));
     }
-    // (Z * H) ^ c in natural word order, from W = rot(Z)
+    // (Z * H) ^ c in natural word order, from W = rot(Z).
+    // PIPE: 9 reads in flight, the xor tree consuming them 3 at a time and each consumed triple's registers taking the
+    // next reads (left alone, the scheduler issued 3, waited for them, and so on: six LDS round trips per product).
+    // AES-128 seal 1.389 -> 1.362 ms; all 16 reads in flight spilled VGPRs (1.459 ms); the AES-256 kernels (60 round
+    // key SGPRs) spill with it too and keep the plain form.
     __device__ __forceinline__ uint4 prod(const uint4 &w, uint4 c) const {
-        const uint4 a = xor3(look<0, 0>(w), look<0, 1>(w), look<0, 2>(w));
-        const uint4 b = xor3(look<0, 3>(w), look<1, 0>(w), look<1, 1>(w));
-        const uint4 d = xor3(look<1, 2>(w), look<1, 3>(w), look<2, 0>(w));
-        const uint4 e = xor3(look<2, 1>(w), look<2, 2>(w), look<2, 3>(w));
-        const uint4 f = xor3(look<3, 0>(w), look<3, 1>(w), look<3, 2>(w));
+        if constexpr (!PIPE) {
+            const uint4 a = xor3(look<0, 0>(w), look<0, 1>(w), look<0, 2>(w));
+            const uint4 b = xor3(look<0, 3>(w), look<1, 0>(w), look<1, 1>(w));
+            const uint4 d = xor3(look<1, 2>(w), look<1, 3>(w), look<2, 0>(w));
+            const uint4 e = xor3(look<2, 1>(w), look<2, 2>(w), look<2, 3>(w));
+            const uint4 f = xor3(look<3, 0>(w), look<3, 1>(w), look<3, 2>(w));
+            const uint4 g = xor3(a, b, d);
+            const uint4 h = xor3(e, f, look<3, 3>(w));
+            return xor3(g, h, c);
+        }
+        uint4 l[16];
+        auto issue = [&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            l[i] = look<i / 4, i % 4>(w);
+        };
+        static_for<9>(issue);
+        __builtin_amdgcn_sched_barrier(0);
+        const uint4 a = xor3(l[0], l[1], l[2]);
+        issue(std::integral_constant<int, 9>{});
+        issue(std::integral_constant<int, 10>{});
+        issue(std::integral_constant<int, 11>{});
+        __builtin_amdgcn_sched_barrier(0);
+        const uint4 b = xor3(l[3], l[4], l[5]);
+        issue(std::integral_constant<int, 12>{});
+        issue(std::integral_constant<int, 13>{});
+        issue(std::integral_constant<int, 14>{});
+        __builtin_amdgcn_sched_barrier(0);
+        const uint4 d = xor3(l[6], l[7], l[8]);
+        issue(std::integral_constant<int, 15>{});
+        __builtin_amdgcn_sched_barrier(0);
         const uint4 g = xor3(a, b, d);
-        const uint4 h = xor3(e, f, look<3, 3>(w));
+        const uint4 e = xor3(l[9], l[10], l[11]);
+        const uint4 f = xor3(l[12], l[13], l[14]);
+        const uint4 h = xor3(e, f, l[15]);
         return xor3(g, h, c);
     }
     // one chain step: W' = rot(Z * H ^ c)
     __device__ __forceinline__ uint4 mulx(const uint4 &w, uint4 c) const { return rot(prod(w, c)); }
 };
+using Ghash = GhashT<false>;
 
 // Build both table sets for one key.  All threads take part; ends with a barrier.
 __device__ void build_tables(const DevKey *__restrict__ key) {
@@ -383,7 +416,7 @@ __global__ __launch_bounds__(WG) void aes_gcm_kernel(const DevKey *__restrict__ 
         if (work[m].begin <= lo) i = m; else j = m;
     }
     const AesLds aes = make_aes(kLdsAes);
-    const Ghash gh = Ghash::make();
+    const GhashT<NR == 10> gh = GhashT<NR == 10>::make();
     Stage<NB> st;
     st.lane = threadIdx.x & 63u;
     st.base = kLdsStage + (threadIdx.x >> 6) * (64u * 16u * NB);

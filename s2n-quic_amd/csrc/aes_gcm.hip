@@ -161,15 +161,32 @@ struct Ghash4 {
     __device__ __forceinline__ uint4 look(uint32_t wk) const {
         return lds_ld128(kLdsGhash + __builtin_amdgcn_perm(wk, g.lc[K], g.sel[I]));
     }
-    template <int K>
-    __device__ __forceinline__ uint4 word(uint32_t wk) const {  // the 8 reads of word K of W
-        const uint32_t h = __builtin_amdgcn_bitop3_b32(wk >> 4, 0x0f0f0f0fu, hi_or, 0xea);  // (a & b) | c
-        const uint32_t l = __builtin_amdgcn_bitop3_b32(wk, 0x0f0f0f0fu, lo_or, 0xea);
-        return xor3(xor3(look<K, 0>(h), look<K, 1>(h), look<K, 2>(h)), xor3(look<K, 3>(h), look<K, 0>(l), look<K, 1>(l)),
-                    look<K, 2>(l) ^ look<K, 3>(l));
-    }
+    // 32 reads, ~9 in flight: the running xor takes two per step and the next two are issued behind it (4096 keys x
+    // 2 Mi packets: seal 3.64 -> 3.50 ms over the word-by-word form the scheduler serialised)
     __device__ __forceinline__ uint4 prod(const uint4 &w, uint4 c) const {
-        return xor3(xor3(word<0>(w.x), word<1>(w.y), c), word<2>(w.z), word<3>(w.w));
+        const uint32_t wk[4] = {w.x, w.y, w.z, w.w};
+        uint32_t hs[4], ls[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            hs[k] = __builtin_amdgcn_bitop3_b32(wk[k] >> 4, 0x0f0f0f0fu, hi_or, 0xea);  // (a & b) | c
+            ls[k] = __builtin_amdgcn_bitop3_b32(wk[k], 0x0f0f0f0fu, lo_or, 0xea);
+        }
+        uint4 r[32];
+        auto issue = [&](auto ic) {
+            constexpr int i = decltype(ic)::value, k = i / 8, j = i % 8;
+            r[i] = look<k, j % 4>(j < 4 ? hs[k] : ls[k]);
+        };
+        static_for<9>(issue);
+        __builtin_amdgcn_sched_barrier(0);
+        uint4 acc = c;
+        static_for<16>([&](auto tc) {
+            constexpr int t = decltype(tc)::value;
+            acc = xor3(acc, r[2 * t], r[2 * t + 1]);
+            if constexpr (2 * t + 9 < 32) issue(std::integral_constant<int, 2 * t + 9>{});
+            if constexpr (2 * t + 10 < 32) issue(std::integral_constant<int, 2 * t + 10>{});
+            __builtin_amdgcn_sched_barrier(0);
+        });
+        return acc;
     }
     __device__ __forceinline__ uint4 mulx(const uint4 &w, uint4 c) const { return rot(prod(w, c)); }
 };

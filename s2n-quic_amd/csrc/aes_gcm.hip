@@ -272,8 +272,7 @@ __device__ __forceinline__ void process_packet(const AesLds &aes, const GH &gh, 
         }
     };
 
-    uint4 ks[NB], cin[NB], cprev[NB], ek0 = make_uint4(0, 0, 0, 0), smp = make_uint4(0, 0, 0, 0);
-    int bprev = -NB;  // first block index of the previous group (for its GHASH validity)
+    uint4 ks[NB], cin[NB], ek0 = make_uint4(0, 0, 0, 0), smp = make_uint4(0, 0, 0, 0);
     // Cooperative stores of group g-1 are issued at the top of iteration g, AFTER this group's prefetched loads
     // have been consumed: vmcnt counts loads and stores together, so a store issued behind a prefetch would make
     // the next wait for that prefetch also wait for the store's write acknowledgement.
@@ -317,17 +316,6 @@ __device__ __forceinline__ void process_packet(const AesLds &aes, const GH &gh, 
                 ks[j] = aes.encrypt<NR>(make_uint4(p.n0, p.n1, p.n2, bswap32(c + j)), rk);
             });
         }
-        // GHASH of the previous group (independent of the keystream just issued).  Inside the packets (every lane's
-        // NB blocks valid: all but the first and last groups of a uniform batch) the steps run branch-free, so the
-        // word rotation is a select and no exec-mask bookkeeping surrounds each step.
-        if (__all(bprev >= 0 && bprev + NB <= nblk)) {
-#pragma unroll
-            for (int j = 0; j < NB; j++) z = gh.mulx(z, cprev[j]);
-        } else {
-#pragma unroll
-            for (int j = 0; j < NB; j++)
-                if (bprev + j >= 0 && bprev + j < nblk) z = gh.mulx(z, cprev[j]);
-        }
         if (g == 0) {
             ek0 = ks[0];
             // header-protection sample = ciphertext bytes [4 - pn_len, 20 - pn_len) (payload.rs:151-169), from
@@ -341,19 +329,31 @@ __device__ __forceinline__ void process_packet(const AesLds &aes, const GH &gh, 
             }
         }
         const int b0 = NB * g - 1;  // data block of slot 0
+        uint4 cg[NB];               // the group's ciphertext blocks, for GHASH
 #pragma unroll
         for (int j = 0; j < NB; j++) {
             const int b = b0 + j;
             const uint4 out = in[j] ^ ks[j];
             lds_st128(st.own(j), out);  // full blocks leave through the cooperative store below
-            cprev[j] = SEAL ? out : in[j];  // (unused unless 0 <= b < nblk)
+            cg[j] = SEAL ? out : in[j];  // (unused unless 0 <= b < nblk)
             if (b == nfull && rem) {
                 const uint4 o = keep_bytes(out, rem);
                 st_bytes(pay + 16 * b, o, rem);
-                cprev[j] = SEAL ? o : keep_bytes(in[j], rem);
+                cg[j] = SEAL ? o : keep_bytes(in[j], rem);
             }
         }
-        bprev = b0;
+        // GHASH of the group.  Inside the packets (every lane's NB blocks valid: all but the first and last groups of a
+        // uniform batch) the steps run branch-free, so the word rotation is a select and no exec-mask bookkeeping
+        // surrounds each step.  (Deferring them behind the next group's keystream kept 16 more VGPRs live for no
+        // overlap: the keystream pipeline is fenced by scheduling barriers.)
+        if (__all(b0 >= 0 && b0 + NB <= nblk)) {
+#pragma unroll
+            for (int j = 0; j < NB; j++) z = gh.mulx(z, cg[j]);
+        } else {
+#pragma unroll
+            for (int j = 0; j < NB; j++)
+                if (b0 + j >= 0 && b0 + j < nblk) z = gh.mulx(z, cg[j]);
+        }
         wave_lds_sync();
     }
     if (G) {
@@ -370,9 +370,6 @@ __device__ __forceinline__ void process_packet(const AesLds &aes, const GH &gh, 
     const uint32_t hdr_len = p.aad_len - p.pn_len;
     HpPrefetch<HNR> hpk;
     if (hp) hpk.load(key->hp_rk, p.base, hdr_len, flags);
-#pragma unroll
-    for (int j = 0; j < NB; j++)
-        if (bprev + j >= 0 && bprev + j < nblk) z = gh.mulx(z, cprev[j]);
     if (!has) return;
     // length block: be64(aad bits) || be64(payload bits); tag = Y * H ^ E_K(J0)
     z = gh.mulx(z, make_uint4(0, bswap32(p.aad_len * 8), 0, bswap32(p.len * 8)));

@@ -7,6 +7,9 @@
 //                calibrated case)
 //   3 coop_nt  : mode 0 with streaming (nt) stores, as the kernels store their payload chunks since round 2
 //   4 coop_read: mode 0's loads only (one dword per packet written), for the read-side calibration alone
+//   5 coop128_read: loads only, 8 lanes per packet (128-B chunks, 8 packets per wave instruction)
+//   6 coop256_read: loads only, 16 lanes per packet (256-B chunks, 4 packets per wave instruction)
+//   7 / 8 / 9: nt stores only with 64- / 128- / 256-B chunks; 10 / 11: in-place copy (nt stores) with 128- / 256-B chunks
 // Algorithmic traffic is the same in all modes: 1200 B read + 1200 B written per packet.
 // usage: copy_pattern <mode> [packets] [reps]   (prints mode, ms per launch, algorithmic GB)
 #include <hip/hip_runtime.h>
@@ -45,6 +48,26 @@ __global__ __launch_bounds__(256) void copy_kernel(uint8_t *arena, uint32_t n, u
     }
     const uint32_t first = wave * 64;
     if (first >= n) return;
+    if (MODE >= 5) {
+        constexpr int L = (MODE == 5 || MODE == 8 || MODE == 10) ? 8 : MODE == 7 ? 4 : 16, PPI = 64 / L;
+        constexpr bool LD = MODE == 5 || MODE == 6 || MODE >= 10, ST = MODE >= 7;
+        uint32_t acc = 0;
+        for (int g = 0; g < (kPay / 16 + 2 + L - 1) / L; g++) {
+#pragma unroll
+            for (int i = 0; i < L; i++) {
+                const uint32_t p = first + PPI * i + lane / L;
+                const int b = L * g - 2 + (int)(lane % L);
+                if (p >= n || b < 0 || 16 * (b + 1) > kPay) continue;
+                uint8_t *q = arena + (size_t)p * stride + pay_off + 16 * b;
+                const uint4 v = LD ? ld16(q) : make_uint4(p, b, 0, 0);
+                if (ST) st16_nt(q, v ^ make_uint4(0x01010101u, 0, 0, p));
+                else acc += v.x ^ v.y ^ v.z ^ v.w;
+            }
+        }
+        if (ST) return;
+        if (lane < 16 && first + lane < n) *(uint32_t *)(arena + (size_t)(first + lane) * stride) = acc;
+        return;
+    }
     const int groups = (kPay / 16 + 2 + 3) / 4;
     uint32_t acc = 0;
     for (int g = 0; g < groups; g++) {
@@ -83,6 +106,13 @@ int main(int argc, char **argv) {
         else if (mode == 1) hipLaunchKernelGGL(copy_kernel<1>, grid, block, 0, 0, arena, n, stride, pay_off);
         else if (mode == 3) hipLaunchKernelGGL(copy_kernel<3>, grid, block, 0, 0, arena, n, stride, pay_off);
         else if (mode == 4) hipLaunchKernelGGL(copy_kernel<4>, grid, block, 0, 0, arena, n, stride, pay_off);
+        else if (mode == 5) hipLaunchKernelGGL(copy_kernel<5>, grid, block, 0, 0, arena, n, stride, pay_off);
+        else if (mode == 6) hipLaunchKernelGGL(copy_kernel<6>, grid, block, 0, 0, arena, n, stride, pay_off);
+        else if (mode == 7) hipLaunchKernelGGL(copy_kernel<7>, grid, block, 0, 0, arena, n, stride, pay_off);
+        else if (mode == 8) hipLaunchKernelGGL(copy_kernel<8>, grid, block, 0, 0, arena, n, stride, pay_off);
+        else if (mode == 9) hipLaunchKernelGGL(copy_kernel<9>, grid, block, 0, 0, arena, n, stride, pay_off);
+        else if (mode == 10) hipLaunchKernelGGL(copy_kernel<10>, grid, block, 0, 0, arena, n, stride, pay_off);
+        else if (mode == 11) hipLaunchKernelGGL(copy_kernel<11>, grid, block, 0, 0, arena, n, stride, pay_off);
         else hipLaunchKernelGGL(copy_kernel<2>, grid, block, 0, 0, arena, n, stride, pay_off);
         hipEventRecord(e1, 0);
         hipEventSynchronize(e1);

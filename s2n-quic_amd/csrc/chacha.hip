@@ -5,9 +5,9 @@
 // (src/aead/default.rs:44-93) and quic::CHACHA20 HeaderProtectionKey::new_mask (src/header_key.rs:52-56):
 //   mask = ChaCha20(hp, counter = LE32(sample[0..4]), nonce = sample[4..16]) over 5 zero bytes.
 //
-// Mapping: one lane per packet, pure VALU (ARX + 26-bit-limb Poly1305), no LDS, so keys are per
-// lane and a mixed-key batch needs no grouping.  Each iteration produces one 64-byte keystream block,
-// seals 4 x 16 bytes and absorbs them into Poly1305.
+// Mapping: one lane per packet, pure VALU (ARX + 26-bit-limb Poly1305); LDS only stages the payload for coalesced
+// I/O, so keys are per lane and a mixed-key batch needs no grouping.  Each iteration produces one 64-byte keystream
+// block, seals 4 x 16 bytes and absorbs them into Poly1305.
 #include "device_common.h"
 
 namespace qpp {
@@ -121,9 +121,17 @@ __device__ __forceinline__ void apply_mask(uint8_t *base, uint32_t hdr_len, uint
 }
 
 // One lane per packet, software-pipelined over 64-byte chunks: the keystream of chunk c+1 is computed in the same
-// basic block as the Poly1305 steps of chunk c (independent chains).  The payload moves through the per-wave LDS
-// staging (Stage<4>, device_common.h): each wave instruction loads/stores 16 packets x 64 contiguous bytes instead
-// of 64 scattered 16-byte pieces, and chunk c+1's input is loaded one chunk ahead.
+// basic block as the Poly1305 steps of chunk c (independent chains).  The payload moves through per-wave LDS
+// staging: loads through Stage<4> (device_common.h; each wave instruction loads 16 packets x 64 contiguous bytes
+// instead of 64 scattered 16-byte pieces, chunk c+1's input one chunk ahead), stores through a 2-chunk output stage
+// that goes out every other chunk as 8 packets x 128 contiguous bytes per wave instruction.  The kernel is bound by
+// this payload I/O (1 Mi x 1200 B seal: 1.10 ms with it, 0.71 ms with the loads and stores cut out, 1.09 ms with the
+// ChaCha20 or the Poly1305 work cut out instead), and 128-B store chunks are what the copy ubench showed cheapest
+// (tools/ubench/copy_pattern.hip: in-place copy 1.09 ms with 64-B chunks, 0.86-0.92 with 128-B stores).
+// Per-wave LDS: input stage 4 KiB | output stage 8 KiB | (payload offset, length) of the wave's 64 packets.
+constexpr uint32_t kChachaInStage = 64u * 16u * 4u;
+constexpr uint32_t kChachaOutStage = 64u * 16u * 8u;
+constexpr uint32_t kChachaWaveLds = kChachaInStage + kChachaOutStage + 64u * 8u;
 template <bool SEAL>
 __global__ __launch_bounds__(256) void chacha_kernel(const DevKey *__restrict__ keys, uint32_t key_cap,
                                                     const qpp_pkt *__restrict__ descs, uint32_t n,
@@ -142,7 +150,8 @@ __global__ __launch_bounds__(256) void chacha_kernel(const DevKey *__restrict__ 
     if (!__any(has)) return;  // wave-uniform: AES packets go to aes_gcm_kernel
     Stage<4> st;
     st.lane = threadIdx.x & 63u;
-    st.base = (threadIdx.x >> 6) * (64u * 16u * 4u);
+    st.base = (threadIdx.x >> 6) * kChachaWaveLds;
+    const uint32_t out_base = st.base + kChachaInStage, tab = out_base + kChachaOutStage;
     uint32_t k[8];
 #pragma unroll
     for (int i = 0; i < 8; i++) k[i] = key->rk[i];
@@ -182,28 +191,29 @@ __global__ __launch_bounds__(256) void chacha_kernel(const DevKey *__restrict__ 
             v[i] = ld16(arena + co_off[i] + (o < co_len[i] ? o : 0u));
         }
     };
-    // cooperative stores of chunk c-1 go out at the top of iteration c, after chunk c's prefetched loads were
-    // consumed (vmcnt counts loads and stores together: see aes_gcm.hip)
-    auto co_store = [&](uint32_t c, const uint4 (&v)[4]) {
+    // output stage: packet p's block 8 m + j (of chunk pair m) at slot 64 (p / 8) + 8 (p % 8) + ((j + p) % 8): the
+    // owner's ds_write_b128s hit 8 distinct bank quads per 8-lane group, and a lane-linear read of slot 64 i + l
+    // gives lane l packet 8 i + l / 8, block j = (l - l / 8) % 8: 8 lanes = 128 contiguous bytes of one packet
+    lds_st64(tab + 8u * st.lane, make_uint2(my_off, len));
+    auto out_slot = [&](uint32_t j) {
+        return out_base + 16u * (64u * (st.lane / 8u) + 8u * (st.lane % 8u) + ((j + st.lane) & 7u));
+    };
+    auto pair_store = [&](uint32_t m) {  // the full blocks of chunks 2 m, 2 m + 1 of the wave's 64 packets
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const uint32_t o = 16u * (4u * c + co_k[i]);
-            if (o + 16 <= co_len[i]) st16_nt(arena + co_off[i] + o, v[i]);
+        for (int i = 0; i < 8; i++) {
+            const uint32_t pp = 8u * i + st.lane / 8u, j = (st.lane - st.lane / 8u) & 7u;
+            const uint4 v = lds_ld128(out_base + 16u * (64u * i + st.lane));
+            const uint2 ol = lds_ld64(tab + 8u * pp);
+            const uint32_t o = 16u * (8u * m + j);
+            if (o + 16 <= ol.y) st16_nt(arena + ol.x + o, v);
         }
     };
     uint4 cin[4], cb[4];
     co_load(0, cin);
     chacha_block(k, 1, n0, n1, n2, ks);
     for (uint32_t c = 0; c < C; c++) {
-        uint4 co_out[4];
-        if (c) {
-#pragma unroll
-            for (int i = 0; i < 4; i++) co_out[i] = lds_ld128(st.coop(i));
-            wave_lds_sync();
-        }
 #pragma unroll
         for (int i = 0; i < 4; i++) lds_st128(st.coop(i), cin[i]);
-        if (c) co_store(c - 1, co_out);
         wave_lds_sync();
         uint4 in[4];
 #pragma unroll
@@ -213,7 +223,7 @@ __global__ __launch_bounds__(256) void chacha_kernel(const DevKey *__restrict__ 
         for (int q = 0; q < 4; q++) {
             const uint32_t o = 64 * c + 16 * q;
             uint4 out = in[q] ^ make_uint4(ks[4 * q], ks[4 * q + 1], ks[4 * q + 2], ks[4 * q + 3]);
-            lds_st128(st.own(q), out);  // full blocks leave through the cooperative store
+            lds_st128(out_slot(4u * (c & 1u) + q), out);  // full blocks leave through the pair store
             cb[q] = SEAL ? out : in[q];
             if (o < len && len - o < 16) {  // the partial last block: this lane stores its bytes
                 const uint32_t r = len - o;
@@ -223,16 +233,15 @@ __global__ __launch_bounds__(256) void chacha_kernel(const DevKey *__restrict__ 
             }
         }
         wave_lds_sync();
+        // stores are issued after this chunk's prefetch loads (vmcnt counts loads and stores together, in order)
+        if ((c & 1u) || c + 1 == C) {
+            pair_store(c >> 1);
+            wave_lds_sync();  // the next pair's outputs overwrite the stage
+        }
         chacha_block(k, c + 2, n0, n1, n2, ks);  // next chunk ...
 #pragma unroll
         for (int q = 0; q < 4; q++)
             if (64 * c + 16 * q < len) mac.block(cb[q]);  // ... beside this chunk's MAC
-    }
-    if (C) {
-        uint4 co_out[4];
-#pragma unroll
-        for (int i = 0; i < 4; i++) co_out[i] = lds_ld128(st.coop(i));
-        co_store(C - 1, co_out);
     }
     if (!has) return;
     mac.block(make_uint4(aad_len, 0, len, 0));  // le64(aad_len) || le64(ct_len)
@@ -607,7 +616,7 @@ hipError_t launch_chacha(bool seal, const DevKey *keys, uint32_t key_cap, const 
         return hipGetLastError();
     }
     const dim3 grid((n + 255) / 256), block(256);
-    const uint32_t lds = 4u * 64u * 16u * 4u;  // Stage<4> per wave, 4 waves
+    const uint32_t lds = 4u * kChachaWaveLds;  // 4 waves (3 workgroups per CU: 150 KiB)
     if (seal)
         hipLaunchKernelGGL(chacha_kernel<true>, grid, block, lds, s, keys, key_cap, descs, n, arena, masks, status, flags);
     else

@@ -27,6 +27,17 @@ __device__ __forceinline__ uint4 lds_ld128(uint32_t a) {
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 __device__ __forceinline__ void lds_st32(uint32_t a, uint32_t v) { *(lds_u32 *)(size_t)a = v; }
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) u32x2 lds_u64;
+__device__ __forceinline__ uint2 lds_ld64(uint32_t a) {
+    const u32x2 v = *(const lds_u64 *)(size_t)a;
+    return make_uint2(v.x, v.y);
+}
+__device__ __forceinline__ void lds_st64(uint32_t a, uint2 v) {
+    u32x2 t;
+    t.x = v.x; t.y = v.y;
+    *(lds_u64 *)(size_t)a = t;
+}
 __device__ __forceinline__ void lds_st128(uint32_t a, uint4 v) {
     u32x4 t;
     t.x = v.x; t.y = v.y; t.z = v.z; t.w = v.w;

@@ -11,6 +11,7 @@
 //   6 coop256_read: loads only, 16 lanes per packet (256-B chunks, 4 packets per wave instruction)
 //   7 / 8 / 9: nt stores only with 64- / 128- / 256-B chunks; 10 / 11: in-place copy (nt stores) with 128- / 256-B chunks
 //   12: in-place copy, loads in 128-B chunks (8 lanes per packet, two 64-B groups), nt stores in 64-B chunks
+//   13: in-place copy, loads in 64-B chunks, nt stores in 128-B chunks (two groups' outputs at a time)
 // Algorithmic traffic is the same in all modes: 1200 B read + 1200 B written per packet.
 // usage: copy_pattern <mode> [packets] [reps]   (prints mode, ms per launch, algorithmic GB)
 #include <hip/hip_runtime.h>
@@ -49,6 +50,28 @@ __global__ __launch_bounds__(256) void copy_kernel(uint8_t *arena, uint32_t n, u
     }
     const uint32_t first = wave * 64;
     if (first >= n) return;
+    if (MODE == 13) {
+        for (int h = 0; h < (kPay / 16 + 2 + 7) / 8; h++) {
+            uint4 r[8];
+#pragma unroll
+            for (int gg = 0; gg < 2; gg++)
+#pragma unroll
+                for (int i = 0; i < 4; i++) {  // 64-B loads: lane-group of 4 -> packet 16 i + lane / 4
+                    const uint32_t p = first + 16 * i + lane / 4;
+                    const int b = 8 * h + 4 * gg - 2 + (int)(lane & 3);
+                    r[4 * gg + i] = (p < n && b >= 0 && 16 * (b + 1) <= kPay)
+                                        ? ld16(arena + (size_t)p * stride + pay_off + 16 * b) : make_uint4(0, 0, 0, 0);
+                }
+#pragma unroll
+            for (int i = 0; i < 8; i++) {  // 128-B stores: lane-group of 8 -> packet 8 i + lane / 8
+                const uint32_t p = first + 8 * i + lane / 8;
+                const int b = 8 * h - 2 + (int)(lane % 8);
+                if (p >= n || b < 0 || 16 * (b + 1) > kPay) continue;
+                st16_nt(arena + (size_t)p * stride + pay_off + 16 * b, r[i] ^ make_uint4(0x01010101u, 0, 0, p));
+            }
+        }
+        return;
+    }
     if (MODE == 12) {
         for (int h = 0; h < (kPay / 16 + 2 + 7) / 8; h++) {
             uint4 r[8];
@@ -137,6 +160,7 @@ int main(int argc, char **argv) {
         else if (mode == 10) hipLaunchKernelGGL(copy_kernel<10>, grid, block, 0, 0, arena, n, stride, pay_off);
         else if (mode == 11) hipLaunchKernelGGL(copy_kernel<11>, grid, block, 0, 0, arena, n, stride, pay_off);
         else if (mode == 12) hipLaunchKernelGGL(copy_kernel<12>, grid, block, 0, 0, arena, n, stride, pay_off);
+        else if (mode == 13) hipLaunchKernelGGL(copy_kernel<13>, grid, block, 0, 0, arena, n, stride, pay_off);
         else hipLaunchKernelGGL(copy_kernel<2>, grid, block, 0, 0, arena, n, stride, pay_off);
         hipEventRecord(e1, 0);
         hipEventSynchronize(e1);

@@ -54,12 +54,12 @@ def aes_lds_cycles_per_packet(pt, aad, nr, hp=True):
     """LDS-array cycles aes_gcm_kernel spends per packet (MI355X_MICROARCH.md §LDS: ds_read_b32 2, ds_read_b128 4,
     ds_write_b128 8 cycles per wave instruction of 64 packets, so per packet 1/64 of that).  Per counter block: the
     CTR AES with round caching (CtrPage) = 133 T-table lookups for AES-128, 197 for AES-256; counters are issued in
-    groups of NB = 4 from counter 0 (J0 = counter 1); each group block also crosses the staging area (2 ds_read_b128
-    + 2 ds_write_b128).  GHASH: 16 ds_read_b128 per product, one per AAD block, ciphertext block, the length block
-    and the final product.  HP: one uncached AES block.  At P = 1200 this gives 4.68e8 cycles per 1 Mi-packet launch
-    against SQ_LDS_IDX_ACTIVE 4.90e8 incl. 1.8e7 bank-conflict cycles (profiles/r01_prof_c2_summary.txt)."""
+    groups of NB = 4 from J0 (counter 1); each group block also crosses the staging area (2 ds_read_b128 + 2
+    ds_write_b128).  GHASH: 16 ds_read_b128 per product, one per AAD block, ciphertext block, the length block and the
+    final product.  HP: one uncached AES block.  At P = 1200 this gives 4.49e8 cycles per 1 Mi-packet launch against
+    SQ_LDS_IDX_ACTIVE 4.63e8 incl. 1.2e7 bank-conflict cycles (profiles/r02c_prof_summary.txt)."""
     lookups = 133 if nr == 10 else 197
-    ctr_blocks = -(-((pt + 15) // 16 + 2) // 4) * 4
+    ctr_blocks = -(-((pt + 15) // 16 + 1) // 4) * 4
     ghash = (aad + 15) // 16 + (pt + 15) // 16 + 2
     per_wave = 2 * (ctr_blocks * lookups + (16 * nr if hp else 0)) + 4 * 16 * ghash + ctr_blocks * (2 * 4 + 2 * 8)
     return per_wave / 64.0

@@ -121,19 +121,24 @@ __device__ __forceinline__ void apply_mask(uint8_t *base, uint32_t hdr_len, uint
 }
 
 // One lane per packet, software-pipelined over 64-byte chunks: the keystream of chunk c+1 is computed in the same
-// basic block as the Poly1305 steps of chunk c (independent chains).  The payload moves through per-wave LDS
-// staging: loads through Stage<4> (device_common.h; each wave instruction loads 16 packets x 64 contiguous bytes
-// instead of 64 scattered 16-byte pieces, chunk c+1's input one chunk ahead), stores through a 2-chunk output stage
-// that goes out every other chunk as 8 packets x 128 contiguous bytes per wave instruction.  The kernel is bound by
-// this payload I/O (1 Mi x 1200 B seal: 1.10 ms with it, 0.71 ms with the loads and stores cut out, 1.09 ms with the
-// ChaCha20 or the Poly1305 work cut out instead), and 128-B store chunks are what the copy ubench showed cheapest
-// (tools/ubench/copy_pattern.hip: in-place copy 1.09 ms with 64-B chunks, 0.86-0.92 with 128-B stores).
-// Per-wave LDS: input stage 4 KiB | output stage 8 KiB | (payload offset, length) of the wave's 64 packets.
-constexpr uint32_t kChachaInStage = 64u * 16u * 4u;
-constexpr uint32_t kChachaOutStage = 64u * 16u * 8u;
-constexpr uint32_t kChachaWaveLds = kChachaInStage + kChachaOutStage + 64u * 8u;
+// basic block as the Poly1305 steps of chunk c (independent chains).  The payload moves through a per-wave LDS stage
+// that holds a PAIR of chunks (128 B per packet): every other chunk, 8 wave instructions load the next pair as 8
+// packets x 128 contiguous bytes each (into registers, a pair ahead), and 8 more store the finished pair the same
+// way; the owner lane reads its 16-B blocks from the stage and writes its output blocks back in place.  The kernel is
+// bound by this payload I/O (1 Mi x 1200 B seal: 1.10 ms with 64-B chunks both ways, 0.71 ms with the loads and
+// stores cut out, 1.09 ms with the ChaCha20 or the Poly1305 work cut out instead; 0.96 ms with 128-B stores), and
+// 128-B chunks both ways are what the copy ubench showed cheapest (tools/ubench/copy_pattern.hip: in-place copy
+// 1.09 ms with 64-B chunks, 0.86-0.92 with 128-B stores, 0.75-0.79 with 128-B loads and stores).
+// Stage slot of packet p's block j of the pair: 64 (p / 8) + 8 (p % 8) + ((j + p + (p >> 4)) % 8).  A lane-linear
+// access (slot 64 i + l) is packet 8 i + l / 8, so 8 lanes cover one packet's 128 contiguous bytes; the owner's
+// ds_write_b128 (8-lane groups) and ds_read_b128 (16-lane groups) hit distinct bank quads.
+// Per-wave LDS: pair stage 8 KiB | (payload offset, length) of the wave's 64 packets.
+constexpr uint32_t kChachaStage = 64u * 16u * 8u;
+constexpr uint32_t kChachaWaveLds = kChachaStage + 64u * 8u;
+__device__ __forceinline__ uint32_t chacha_rho(uint32_t p) { return (p + (p >> 4)) & 7u; }
+
 template <bool SEAL>
-__global__ __launch_bounds__(256) void chacha_kernel(const DevKey *__restrict__ keys, uint32_t key_cap,
+__global__ __launch_bounds__(256, 3) void chacha_kernel(const DevKey *__restrict__ keys, uint32_t key_cap,
                                                     const qpp_pkt *__restrict__ descs, uint32_t n,
                                                     uint8_t *__restrict__ arena, uint8_t *masks, int8_t *status,
                                                     uint32_t flags) {
@@ -148,10 +153,8 @@ __global__ __launch_bounds__(256) void chacha_kernel(const DevKey *__restrict__ 
     const bool has = pi < n && !refused && key->suite == QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256 &&
                      !(d.flags & QPP_PKT_SKIP);
     if (!__any(has)) return;  // wave-uniform: AES packets go to aes_gcm_kernel
-    Stage<4> st;
-    st.lane = threadIdx.x & 63u;
-    st.base = (threadIdx.x >> 6) * kChachaWaveLds;
-    const uint32_t out_base = st.base + kChachaInStage, tab = out_base + kChachaOutStage;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t stage = (threadIdx.x >> 6) * kChachaWaveLds, tab = stage + kChachaStage;
     uint32_t k[8];
 #pragma unroll
     for (int i = 0; i < 8; i++) k[i] = key->rk[i];
@@ -172,58 +175,52 @@ __global__ __launch_bounds__(256) void chacha_kernel(const DevKey *__restrict__ 
             if (aad_len - off < 16) a = keep_bytes(a, aad_len - off);
             mac.block(a);
         }
-    // cooperative roles: payload offset / length of the packet whose chunk this lane moves in instruction i
     const uint32_t nch = (len + 63) / 64;  // chunks, the partial tail included
     const uint32_t C = wave_max(nch);
-    uint32_t co_off[4], co_len[4], co_k[4];
-    const uint32_t my_off = (uint32_t)(pay - arena);
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        co_off[i] = (uint32_t)__shfl((int)my_off, (int)st.coop_src(i), 64);
-        co_len[i] = (uint32_t)__shfl((int)len, (int)st.coop_src(i), 64);
-        co_k[i] = st.coop_chunk(i);
-    }
-    // block b = 4 c + k of the lane's assigned packet, clamped inside payload||tag (unused when out of range)
-    auto co_load = [&](uint32_t c, uint4 (&v)[4]) {
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const uint32_t o = 16u * (4u * c + co_k[i]);
-            v[i] = ld16(arena + co_off[i] + (o < co_len[i] ? o : 0u));
-        }
+    lds_st64(tab + 8u * lane, make_uint2((uint32_t)(pay - arena), len));
+    wave_lds_sync();
+    // lane-linear role in pair instruction i: packet 8 i + lane / 8, block j of the pair
+    // (lj(i) + rho(p)) % 8 = lane % 8, rho(p) = (lane / 8 + i / 2) % 8
+    auto lj = [&](int i) { return ((lane & 7u) - (lane / 8u + (uint32_t)(i >> 1))) & 7u; };
+    auto own_slot = [&](uint32_t j) {
+        return stage + 16u * (64u * (lane / 8u) + 8u * (lane % 8u) + ((j + chacha_rho(lane)) & 7u));
     };
-    // output stage: packet p's block 8 m + j (of chunk pair m) at slot 64 (p / 8) + 8 (p % 8) + ((j + p) % 8): the
-    // owner's ds_write_b128s hit 8 distinct bank quads per 8-lane group, and a lane-linear read of slot 64 i + l
-    // gives lane l packet 8 i + l / 8, block j = (l - l / 8) % 8: 8 lanes = 128 contiguous bytes of one packet
-    lds_st64(tab + 8u * st.lane, make_uint2(my_off, len));
-    auto out_slot = [&](uint32_t j) {
-        return out_base + 16u * (64u * (st.lane / 8u) + 8u * (st.lane % 8u) + ((j + st.lane) & 7u));
-    };
-    auto pair_store = [&](uint32_t m) {  // the full blocks of chunks 2 m, 2 m + 1 of the wave's 64 packets
+    // pair m = blocks 8 m .. 8 m + 7, clamped inside payload||tag (unused when out of range)
+    auto pair_load = [&](uint32_t m, uint4 (&r)[8]) {
 #pragma unroll
         for (int i = 0; i < 8; i++) {
-            const uint32_t pp = 8u * i + st.lane / 8u, j = (st.lane - st.lane / 8u) & 7u;
-            const uint4 v = lds_ld128(out_base + 16u * (64u * i + st.lane));
-            const uint2 ol = lds_ld64(tab + 8u * pp);
-            const uint32_t o = 16u * (8u * m + j);
+            const uint2 ol = lds_ld64(tab + 8u * (8u * i + lane / 8u));
+            const uint32_t o = 16u * (8u * m + lj(i));
+            r[i] = ld16(arena + ol.x + (o < ol.y ? o : 0u));
+        }
+    };
+    auto pair_store = [&](uint32_t m) {  // the full blocks of pair m of the wave's 64 packets
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const uint4 v = lds_ld128(stage + 16u * (64u * i + lane));
+            const uint2 ol = lds_ld64(tab + 8u * (8u * i + lane / 8u));
+            const uint32_t o = 16u * (8u * m + lj(i));
             if (o + 16 <= ol.y) st16_nt(arena + ol.x + o, v);
         }
     };
-    uint4 cin[4], cb[4];
-    co_load(0, cin);
+    uint4 rin[8], cb[4];
+    pair_load(0, rin);
     chacha_block(k, 1, n0, n1, n2, ks);
     for (uint32_t c = 0; c < C; c++) {
+        if (!(c & 1u)) {  // pair top: the pair's inputs into the stage, the next pair's loads issued
 #pragma unroll
-        for (int i = 0; i < 4; i++) lds_st128(st.coop(i), cin[i]);
-        wave_lds_sync();
+            for (int i = 0; i < 8; i++) lds_st128(stage + 16u * (64u * i + lane), rin[i]);
+            pair_load((c >> 1) + 1, rin);
+            wave_lds_sync();
+        }
         uint4 in[4];
 #pragma unroll
-        for (int q = 0; q < 4; q++) in[q] = lds_ld128(st.own(q));
-        co_load(c + 1, cin);
+        for (int q = 0; q < 4; q++) in[q] = lds_ld128(own_slot(4u * (c & 1u) + q));
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             const uint32_t o = 64 * c + 16 * q;
             uint4 out = in[q] ^ make_uint4(ks[4 * q], ks[4 * q + 1], ks[4 * q + 2], ks[4 * q + 3]);
-            lds_st128(out_slot(4u * (c & 1u) + q), out);  // full blocks leave through the pair store
+            lds_st128(own_slot(4u * (c & 1u) + q), out);  // full blocks leave through the pair store
             cb[q] = SEAL ? out : in[q];
             if (o < len && len - o < 16) {  // the partial last block: this lane stores its bytes
                 const uint32_t r = len - o;
@@ -232,11 +229,10 @@ __global__ __launch_bounds__(256) void chacha_kernel(const DevKey *__restrict__ 
                 cb[q] = SEAL ? out : keep_bytes(in[q], r);
             }
         }
-        wave_lds_sync();
-        // stores are issued after this chunk's prefetch loads (vmcnt counts loads and stores together, in order)
         if ((c & 1u) || c + 1 == C) {
+            wave_lds_sync();
             pair_store(c >> 1);
-            wave_lds_sync();  // the next pair's outputs overwrite the stage
+            wave_lds_sync();  // the next pair's inputs overwrite the stage
         }
         chacha_block(k, c + 2, n0, n1, n2, ks);  // next chunk ...
 #pragma unroll
@@ -616,7 +612,7 @@ hipError_t launch_chacha(bool seal, const DevKey *keys, uint32_t key_cap, const 
         return hipGetLastError();
     }
     const dim3 grid((n + 255) / 256), block(256);
-    const uint32_t lds = 4u * kChachaWaveLds;  // 4 waves (3 workgroups per CU: 150 KiB)
+    const uint32_t lds = 4u * kChachaWaveLds;  // 4 waves, 34 KiB
     if (seal)
         hipLaunchKernelGGL(chacha_kernel<true>, grid, block, lds, s, keys, key_cap, descs, n, arena, masks, status, flags);
     else

@@ -397,11 +397,10 @@ def e2e(args, rank, world, local_rank):
         nonlocal keys, slots
         t0 = time.perf_counter()
         if args.rotate:
-            new = ctx.update_keys(keys)
+            new = ctx.update_keys(keys, slots_out=slots)  # the new slots in one call
             ctx.free_keys(keys)
             keys = new
-            slots = np.array([k.slot for k in keys], dtype=np.uint32)
-            descs["key_idx"] = slots[conn]
+            descs["key_idx"] = slots[conn]  # the transport re-stamps its connections' packets
         t1 = time.perf_counter()
         tickets = [ctx.host_submit(descs[lo:hi], arena, masks[5 * lo:5 * hi], status[lo:hi], flags,
                                    qpp.OP_SEAL | qpp.OP_OPEN) for lo, hi, arena in wins]

@@ -109,6 +109,9 @@ void qpp_key_free(qpp_key *key);
 void qpp_key_free_batch(qpp_key *const *keys, size_t n);
 /* Index of this key in its context's device key table: the value to put in qpp_pkt.key_idx. */
 uint32_t qpp_key_slot(const qpp_key *key);
+/* qpp_key_slot of n keys into slots[i] (UINT32_MAX for NULL): a transport re-stamping its connections' key slots
+ * after a batch rotation reads them in one call. */
+void qpp_key_slot_batch(const qpp_key *const *keys, size_t n, uint32_t *slots);
 int qpp_key_suite(const qpp_key *key);
 /* Key::tag_len (16), HeaderKey::{sealing,opening}_sample_len (16), Key::aead_{confidentiality,integrity}_limit
  * (cipher_suite.rs:158-175, 247-301). */

@@ -935,6 +935,10 @@ void qpp_key_free_batch(qpp_key *const *keys, size_t n) {
 }
 
 uint32_t qpp_key_slot(const qpp_key *key) { return key ? key->slot : UINT32_MAX; }
+void qpp_key_slot_batch(const qpp_key *const *keys, size_t n, uint32_t *slots) {
+    if (!keys || !slots) return;
+    for (size_t i = 0; i < n; i++) slots[i] = keys[i] ? keys[i]->slot : UINT32_MAX;
+}
 int qpp_key_suite(const qpp_key *key) { return key ? key->suite : 0; }
 size_t qpp_tag_len(const qpp_key *) { return 16; }
 size_t qpp_sample_len(const qpp_key *) { return 16; }

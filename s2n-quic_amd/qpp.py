@@ -45,7 +45,7 @@ assert RX_DTYPE.itemsize == 24
 # every symbol include/qpp.h declares (tests/test_abi.py checks the library exports them all)
 EXPORTS = [
     "qpp_abi_version", "qpp_ctx_create", "qpp_ctx_destroy", "qpp_ctx_stream", "qpp_ctx_synchronize",
-    "qpp_ctx_last_error", "qpp_key_new", "qpp_key_new_raw", "qpp_key_update", "qpp_key_free", "qpp_key_free_batch", "qpp_ctx_set_aes_kernel", "qpp_key_slot",
+    "qpp_ctx_last_error", "qpp_key_new", "qpp_key_new_raw", "qpp_key_update", "qpp_key_free", "qpp_key_free_batch", "qpp_ctx_set_aes_kernel", "qpp_key_slot", "qpp_key_slot_batch",
     "qpp_key_suite", "qpp_tag_len", "qpp_sample_len", "qpp_confidentiality_limit", "qpp_integrity_limit",
     "qpp_key_material", "qpp_initial_keys", "qpp_seal", "qpp_seal_scatter", "qpp_open", "qpp_hp_mask",
     "qpp_seal_batch", "qpp_open_batch", "qpp_hp_mask_batch", "qpp_dev_alloc", "qpp_dev_free", "qpp_host_alloc",
@@ -99,6 +99,7 @@ def lib():
             "qpp_key_free_batch": (None, [vp, sz]),
             "qpp_ctx_set_aes_kernel": (ctypes.c_int, [vp, ctypes.c_int]),
             "qpp_key_slot": (u32, [vp]),
+            "qpp_key_slot_batch": (None, [vp, sz, vp]),
             "qpp_key_suite": (ctypes.c_int, [vp]),
             "qpp_tag_len": (sz, [vp]),
             "qpp_sample_len": (sz, [vp]),
@@ -278,14 +279,18 @@ class Context:
             raise QppError(rc, "qpp_header_key_new")
         return HeaderKey(self, h.value)
 
-    def update_keys(self, keys):
-        """qpp_key_update_batch: [k.derive_next_key() for k in keys] in one device pass per suite."""
+    def update_keys(self, keys, slots_out=None):
+        """qpp_key_update_batch: [k.derive_next_key() for k in keys] in one device pass per suite.  slots_out (a
+        uint32 numpy array of len(keys)) receives the new keys' slots (qpp_key_slot_batch, one call)."""
         n = len(keys)
         arr_in = (vp * max(n, 1))(*[k.handle for k in keys])
         arr = (vp * max(n, 1))()
         rc = lib().qpp_key_update_batch(arr_in, n, arr)
         if rc != OK:
             raise QppError(rc, "qpp_key_update_batch")
+        if slots_out is not None:
+            assert slots_out.dtype == np.uint32 and slots_out.size >= n and slots_out.flags["C_CONTIGUOUS"]
+            lib().qpp_key_slot_batch(arr, n, slots_out.ctypes.data)
         return [Key(self, arr[i]) for i in range(n)]
 
     def free_keys(self, keys):

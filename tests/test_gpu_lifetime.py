@@ -225,7 +225,9 @@ def test_key_update_batch_matches_chain(ctx):
         assert u.material() == ref.material() and u.suite == k.suite
         assert u.material()[2] == k.material()[2]  # the header key is carried over
         ref.free()
-    nxt2 = ctx.update_keys(nxt)  # a second rotation from device-made keys
+    slots2 = np.zeros(len(nxt), dtype=np.uint32)
+    nxt2 = ctx.update_keys(nxt, slots_out=slots2)  # a second rotation from device-made keys
+    assert list(slots2) == [k.slot for k in nxt2]  # qpp_key_slot_batch
     for k in keys:
         k.free()
     descs, arena = qpp.make_batch(6000, 500, [k.slot for k in nxt2], seed=91)

@@ -375,21 +375,27 @@ __device__ __forceinline__ void hp_finish(const AesLds &aes, const uint32_t *hp_
 // group's NB x 16 B per packet is moved cooperatively: in wave instruction i, the NB lanes of a lane-group of NB
 // load the NB chunks of ONE packet (p = PPI i + lane / NB, 64 B contiguous at NB = 4), write them to LDS at slot
 // 64 i + lane, and every lane then reads its own packet's NB blocks back.  Outputs go the other way.  The chunk a
-// lane moves is rotated by p / ROT so that the owner's reads (slot(p, k) = 64 (p / PPI) + NB (p % PPI) +
-// ((k + p / ROT) % NB)) hit 16 distinct bank quads per ds_read_b128 lane group (conflict-free).
+// lane moves is rotated by rho(p) so that the owner's accesses (slot(p, k) = 64 (p / PPI) + NB (p % PPI) +
+// ((k + rho(p)) % NB)) hit distinct bank quads per lane group (conflict-free).
 template <int NB>
 struct Stage {
     static constexpr uint32_t PPI = 64 / NB, ROT = 16 / NB;
     uint32_t base;  // this wave's 64 * NB * 16 byte region
     uint32_t lane;
+    // rotation of packet p's chunks: NB = 4: (p/2 + p/16) % 4 keeps both the owner's ds_read_b128 (16-lane groups, 64
+    // banks) and its ds_write_b128 (8-lane groups, 32 banks) conflict-free (p/4 left the writes 2-way;
+    // tests/test_kernel_layouts.py checks both); other NB: p / ROT (reads only)
+    static __device__ __forceinline__ uint32_t rho(uint32_t p) {
+        return NB == 4 ? ((p >> 1) + (p >> 4)) & 3u : p / ROT;
+    }
     __device__ __forceinline__ uint32_t own(uint32_t k) const {  // LDS address of my packet's chunk k
-        return base + 16u * (64u * (lane / PPI) + NB * (lane % PPI) + ((k + lane / ROT) % NB));
+        return base + 16u * (64u * (lane / PPI) + NB * (lane % PPI) + ((k + rho(lane)) % NB));
     }
     __device__ __forceinline__ uint32_t coop(int i) const { return base + 16u * (64u * i + lane); }
     __device__ __forceinline__ uint32_t coop_src(int i) const { return PPI * i + lane / NB; }  // packet lane
     __device__ __forceinline__ uint32_t coop_chunk(int i) const {
         const uint32_t p = coop_src(i);
-        return ((lane % NB) + NB - (p / ROT) % NB) % NB;
+        return ((lane % NB) + NB - rho(p) % NB) % NB;
     }
 };
 

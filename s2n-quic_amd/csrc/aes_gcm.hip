@@ -412,20 +412,29 @@ __device__ __forceinline__ void process_packet(const AesLds &aes, const GH &gh, 
 // the last quarter round ran alone.  meta (plan_scan): {items, AES-128 items, AES-128 packets, AES-256 packets};
 // work[] holds one item per key (begin = its first perm index), AES-128 keys first.
 template <bool SEAL, int NB, int WG, int NR>
+// single: a context with one live AES key (its slot; meta, perm and work unused): descs[0, n_single) in slices
+// without a plan, packets of any other slot refused.
 __global__ __launch_bounds__(WG) void aes_gcm_kernel(const DevKey *__restrict__ keys, const qpp_pkt *__restrict__ descs,
                                                     const uint32_t *__restrict__ perm, const WorkItem *__restrict__ work,
                                                     const uint32_t *__restrict__ meta, uint8_t *__restrict__ arena,
-                                                    uint8_t *masks, int8_t *status, uint32_t flags) {
+                                                    uint8_t *masks, int8_t *status, uint32_t flags, uint32_t single,
+                                                    uint32_t n_single) {
     // dynamic LDS (tables + this variant's staging, reserved by the launch), addressed by offset (lds_ld32 / lds_ld128)
-    const uint32_t items = meta[0], i10 = meta[1], n10 = meta[2], n14 = meta[3];
-    const uint32_t i_lo = NR == 10 ? 0 : i10, i_hi = NR == 10 ? i10 : items;
-    const uint32_t p0 = NR == 10 ? 0 : n10, n = NR == 10 ? n10 : n14;
+    const bool one = single != 0xffffffffu;  // uniform
+    uint32_t i_lo = 0, i_hi = 1, p0 = 0, n = n_single;
+    if (!one) {
+        const uint32_t items = meta[0], i10 = meta[1], n10 = meta[2], n14 = meta[3];
+        i_lo = NR == 10 ? 0 : i10;
+        i_hi = NR == 10 ? i10 : items;
+        p0 = NR == 10 ? 0 : n10;
+        n = NR == 10 ? n10 : n14;
+    }
     const uint32_t P = ((n + gridDim.x - 1) / gridDim.x + 63u) & ~63u;  // whole waves per slice
     uint32_t lo = p0 + min(n, blockIdx.x * P);
     const uint32_t hi = p0 + min(n, (blockIdx.x + 1) * P);
     if (lo >= hi) return;  // uniform
     uint32_t i = i_lo, j = i_hi;  // the item holding lo: largest i with work[i].begin <= lo
-    while (j - i > 1) {
+    while (!one && j - i > 1) {
         const uint32_t m = (i + j) >> 1;
         if (work[m].begin <= lo) i = m; else j = m;
     }
@@ -435,7 +444,7 @@ __global__ __launch_bounds__(WG) void aes_gcm_kernel(const DevKey *__restrict__ 
     st.lane = threadIdx.x & 63u;
     st.base = kLdsStage + (threadIdx.x >> 6) * (64u * 16u * NB);
     for (; lo < hi; i++) {  // key segments of the slice
-        const WorkItem w = work[i];
+        const WorkItem w = one ? WorkItem{single, 0u, n, (uint32_t)NR} : work[i];
         const uint32_t end = min(hi, w.begin + w.count);
         const DevKey *__restrict__ key = keys + w.key;
         __syncthreads();  // every wave is done with the previous segment's tables
@@ -447,9 +456,13 @@ __global__ __launch_bounds__(WG) void aes_gcm_kernel(const DevKey *__restrict__ 
         for (uint32_t t0 = lo; t0 < end; t0 += WG) {
             const uint32_t t = t0 + threadIdx.x;
             const bool real = t < end;
-            const uint32_t pi = perm[real ? t : lo];
+            const uint32_t pi = one ? (real ? t : lo) : perm[real ? t : lo];
             const qpp_pkt d = descs[pi];  // (any valid descriptor for helper lanes)
-            const bool has = real && !(d.flags & QPP_PKT_SKIP);
+            bool has = real && !(d.flags & QPP_PKT_SKIP);
+            if (one && has && d.key_idx != single) {  // not the live key: refused, untouched
+                if (status) status[pi] = QPP_INTERNAL_ERROR;
+                has = false;
+            }
             process_packet<NR, NB, SEAL>(aes, gh, st, key, rk, has, d, pi, arena, masks, status, flags);
         }
         lo = end;
@@ -575,11 +588,12 @@ constexpr uint32_t lds_bytes(int nb, int wg) {
 
 template <bool SEAL, int NR>
 void launch_variant(int v, dim3 grid, hipStream_t s, const DevKey *keys, const qpp_pkt *descs, const PlanBuffers &pb,
-                    uint8_t *arena, uint8_t *masks, int8_t *status, uint32_t flags) {
+                    uint8_t *arena, uint8_t *masks, int8_t *status, uint32_t flags, uint32_t single = 0xffffffffu,
+                    uint32_t n_single = 0) {
 #define QPP_AES_LAUNCH(NB, WG)                                                                                    \
     static_assert(lds_bytes(NB, WG) <= kLdsMax, "LDS budget");                                                 \
     hipLaunchKernelGGL((aes_gcm_kernel<SEAL, NB, WG, NR>), grid, dim3(WG), lds_bytes(NB, WG), s, keys, descs,   \
-                       pb.perm, pb.work, pb.n_work, arena, masks, status, flags)
+                       pb.perm, pb.work, pb.n_work, arena, masks, status, flags, single, n_single)
     switch (v) {
         case 1: { QPP_AES_LAUNCH(2, 1024); break; }
         case 2: { QPP_AES_LAUNCH(2, 512); break; }
@@ -599,6 +613,24 @@ int aes_variant() {
     return v;
 }
 }  // namespace
+
+hipError_t launch_aes_gcm_single(bool seal, const DevKey *keys, const qpp_pkt *descs, uint32_t slot, uint32_t nr,
+                                 uint32_t n, uint32_t n_cu, uint8_t *arena, uint8_t *masks, int8_t *status,
+                                 uint32_t flags, hipStream_t s) {
+    if (!n) return hipSuccess;
+    const uint32_t waves = (n + 63) / 64;
+    const dim3 grid(waves < n_cu ? waves : n_cu);
+    const int v = aes_variant();
+    const PlanBuffers none{};
+    if (nr == 10) {
+        if (seal) launch_variant<true, 10>(v, grid, s, keys, descs, none, arena, masks, status, flags, slot, n);
+        else launch_variant<false, 10>(v, grid, s, keys, descs, none, arena, masks, status, flags, slot, n);
+    } else {
+        if (seal) launch_variant<true, 14>(v, grid, s, keys, descs, none, arena, masks, status, flags, slot, n);
+        else launch_variant<false, 14>(v, grid, s, keys, descs, none, arena, masks, status, flags, slot, n);
+    }
+    return hipGetLastError();
+}
 
 hipError_t launch_aes_gcm_wave(bool seal, const DevKey *keys, const qpp_pkt *descs, const PlanBuffers &pb, uint32_t n,
                                uint32_t key_cap, uint32_t n_cu, uint8_t *arena, uint8_t *masks, int8_t *status,

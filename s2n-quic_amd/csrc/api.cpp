@@ -93,6 +93,7 @@ struct qpp_ctx {
     std::vector<uint32_t> retire_pending; // freed, host copy zeroized, device zeroing not yet enqueued
     uint32_t retired_slots = 0;           // slots in `retired`
     uint32_t live_by_suite[4] = {0, 0, 0, 0};  // live packet keys per suite: which kernels a batch can need
+    uint32_t live_slot_xor = 0;                  // XOR of the live packet keys' slots: THE slot when only one is live
     uint32_t next_slot = 0;
     // per-stream state (plan scratch, last-batch event); [0] is the context stream
     std::vector<StreamState *> streams;
@@ -423,6 +424,7 @@ int install(qpp_key *k) {
     }
     mark_dirty(ctx, k->slot);
     ctx->live_by_suite[k->suite]++;
+    ctx->live_slot_xor ^= k->slot;
     return QPP_OK;
 }
 
@@ -486,15 +488,31 @@ hipError_t launch_aes(const qpp_ctx *ctx, AesPath p, bool seal, const qpp_pkt *d
     }
 }
 
+// The one live packet key of the context when there is exactly one and it is an AES key: then a lane-kernel batch
+// needs no plan (every AES packet is that key's; any other slot is refused in the kernel), saving the three plan
+// launches (~25 us per 1 Mi batch).
+uint32_t single_aes_slot(const qpp_ctx *ctx) {
+    const uint32_t live = ctx->live_by_suite[1] + ctx->live_by_suite[2] + ctx->live_by_suite[3];
+    if (live != 1 || ctx->live_by_suite[QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256]) return UINT32_MAX;
+    const uint32_t slot = ctx->live_slot_xor;
+    return slot < ctx->key_cap && ctx->h_keys[slot].live == 1 ? slot : UINT32_MAX;
+}
+
 // Batch bodies: plan (AES) + kernels on st's stream; keys already flushed.
 int enqueue_seal(qpp_ctx *ctx, StreamState *st, const qpp_pkt *descs, uint32_t n, uint8_t *arena, uint8_t *masks,
                  int8_t *status, uint32_t flags) {
     hipStream_t s = st->stream;
     if (!(flags & QPP_ONLY_CHACHA) && (suite_mask(ctx) & kAesSuites)) {
-        RC_TRY(ensure_plan(ctx, st, n));
         const AesPath path = aes_path(ctx, n);
-        HIP_TRY(ctx, launch_plan(ctx->d_keys, ctx->key_cap, descs, n, st->plan, aes_per_item(ctx, path, n), s));
-        HIP_TRY(ctx, launch_aes(ctx, path, true, descs, st->plan, n, arena, masks, status, flags, s));
+        const uint32_t one = path == AesPath::lane ? single_aes_slot(ctx) : UINT32_MAX;
+        if (one != UINT32_MAX) {
+            HIP_TRY(ctx, launch_aes_gcm_single(true, ctx->d_keys, descs, one, ctx->h_keys[one].nr, n, ctx->n_cu, arena,
+                                               masks, status, flags, s));
+        } else {
+            RC_TRY(ensure_plan(ctx, st, n));
+            HIP_TRY(ctx, launch_plan(ctx->d_keys, ctx->key_cap, descs, n, st->plan, aes_per_item(ctx, path, n), s));
+            HIP_TRY(ctx, launch_aes(ctx, path, true, descs, st->plan, n, arena, masks, status, flags, s));
+        }
     }
     if (!(flags & QPP_ONLY_AES))
         HIP_TRY(ctx, launch_chacha(true, ctx->d_keys, ctx->key_cap, descs, n, arena, masks, status, flags,
@@ -506,10 +524,16 @@ int enqueue_open(qpp_ctx *ctx, StreamState *st, const qpp_pkt *descs, uint32_t n
                  uint32_t flags) {
     hipStream_t s = st->stream;
     if (!(flags & QPP_ONLY_CHACHA) && (suite_mask(ctx) & kAesSuites)) {
-        RC_TRY(ensure_plan(ctx, st, n));
         const AesPath path = aes_path(ctx, n);
-        HIP_TRY(ctx, launch_plan(ctx->d_keys, ctx->key_cap, descs, n, st->plan, aes_per_item(ctx, path, n), s));
-        HIP_TRY(ctx, launch_aes(ctx, path, false, descs, st->plan, n, arena, nullptr, status, 0, s));
+        const uint32_t one = path == AesPath::lane ? single_aes_slot(ctx) : UINT32_MAX;
+        if (one != UINT32_MAX) {
+            HIP_TRY(ctx, launch_aes_gcm_single(false, ctx->d_keys, descs, one, ctx->h_keys[one].nr, n, ctx->n_cu, arena,
+                                               nullptr, status, 0, s));
+        } else {
+            RC_TRY(ensure_plan(ctx, st, n));
+            HIP_TRY(ctx, launch_plan(ctx->d_keys, ctx->key_cap, descs, n, st->plan, aes_per_item(ctx, path, n), s));
+            HIP_TRY(ctx, launch_aes(ctx, path, false, descs, st->plan, n, arena, nullptr, status, 0, s));
+        }
     }
     if (!(flags & QPP_ONLY_AES))
         HIP_TRY(ctx, launch_chacha(false, ctx->d_keys, ctx->key_cap, descs, n, arena, nullptr, status, 0,
@@ -643,6 +667,7 @@ int derive_batch(qpp_ctx *ctx, int suite, const uint8_t *secrets, const uint8_t 
         r.suite = (uint32_t)suite;
         r.nr = r.hp_nr = nr;
         r.live = 1;
+        ctx->live_slot_xor ^= slots[i];
         out[i] = k;
     }
     ctx->live_by_suite[suite] += (uint32_t)n;
@@ -923,6 +948,7 @@ void qpp_key_free(qpp_key *key) {
     qpp_ctx *ctx = key->ctx;
     if (ctx && key->slot < ctx->key_cap && ctx->h_keys[key->slot].live == 1) {
         ctx->live_by_suite[key->suite]--;
+        ctx->live_slot_xor ^= key->slot;
         retire_slot(ctx, key->slot);
     }
     secure_zero(key, sizeof *key);

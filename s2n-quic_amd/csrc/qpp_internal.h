@@ -144,6 +144,11 @@ hipError_t launch_pow_setup(const DevKey *keys, const uint32_t *slots, uint32_t 
 hipError_t launch_aes_gcm(bool seal, const DevKey *keys, const qpp_pkt *descs, const PlanBuffers &pb, uint32_t n,
                           uint32_t n_cu, uint8_t *arena, uint8_t *masks, int8_t *status, uint32_t flags,
                           uint32_t suites, hipStream_t s);
+// one live AES key (slot, nr): the lane kernel over descs[0, n) without a plan; packets of any other slot are refused
+// (status INTERNAL_ERROR)
+hipError_t launch_aes_gcm_single(bool seal, const DevKey *keys, const qpp_pkt *descs, uint32_t slot, uint32_t nr,
+                                 uint32_t n, uint32_t n_cu, uint8_t *arena, uint8_t *masks, int8_t *status,
+                                 uint32_t flags, hipStream_t s);
 // many keys: work items of <= kWavePacketsPerItem packets (plan with per = kWavePacketsPerItem), one wave each
 hipError_t launch_aes_gcm_wave(bool seal, const DevKey *keys, const qpp_pkt *descs, const PlanBuffers &pb, uint32_t n,
                                uint32_t key_cap, uint32_t n_cu, uint8_t *arena, uint8_t *masks, int8_t *status,

@@ -353,3 +353,44 @@ def test_host_pipeline(ctx, ops):
         ctx.set_host_pipe(65536, 96 << 20, 4)
         for k in keys:
             k.free()
+
+
+@pytest.mark.parametrize("suite", [1, 2])
+def test_single_live_key_batches_run_without_a_plan(suite):
+    """With exactly one live packet key (an AES one) the lane kernel runs without the plan launches
+    (api.cpp single_aes_slot); packets naming any other slot are still refused with INTERNAL_ERROR and left untouched,
+    the rest are bit-exact, and open round-trips."""
+    c = qpp.Context(0)
+    try:
+        c.set_burst_max(0)  # the lane kernel, not the wave-per-packet one
+        rng = np.random.default_rng(70 + suite)
+        k = c.key(suite, _secret(rng, suite))
+        n = 4096
+        descs, arena = qpp.make_batch(n, 600, [k.slot], seed=71 + suite)
+        bad = np.zeros(n, bool)
+        bad[3::53] = True
+        descs["key_idx"][bad] = k.slot + 1  # not a live slot
+        d = [c.alloc(descs.nbytes), c.alloc(arena.nbytes), c.alloc(5 * n), c.alloc(n)]
+        d[0].upload(descs)
+        d[1].upload(arena)
+        c.seal_batch(d[0], n, d[1], d[2], d[3], qpp.HP_MASK_OUT)
+        c.sync()
+        st, got = d[3].download(dtype=np.int8), d[1].download()
+        assert (st[bad] == qpp.INTERNAL_ERROR).all() and (st[~bad] == 0).all()
+        stride = arena.size // n
+        ok = np.nonzero(~bad)[0][::7]
+        sub_d, sub_a = _sample(descs, arena, ok)
+        want, _ = _oracle_seal(_mat([k]), sub_d, sub_a, 0)
+        assert (_gather(got, ok, stride) == want).all()
+        assert (_gather(got, np.nonzero(bad)[0], stride) == _gather(arena, np.nonzero(bad)[0], stride)).all()
+        c.open_batch(d[0], n, d[1], d[3], 0)
+        c.sync()
+        st2, back = d[3].download(dtype=np.int8), d[1].download()
+        assert (st2[~bad] == 0).all()
+        for i in np.nonzero(~bad)[0][::11]:  # the payloads are the plaintext again (the tags stay sealed ones)
+            a = int(descs["off"][i]) + int(descs["aad_len"][i])
+            b = a + int(descs["pt_len"][i])
+            assert (back[a:b] == arena[a:b]).all()
+        k.free()
+    finally:
+        c.close()

@@ -258,7 +258,10 @@ def test_batch_seal_open_ragged(ctx, specs, path):
         k.free()
 
 
-def test_jumbo_and_edges(ctx, path):
+@pytest.mark.parametrize("flags", [0, qpp.HP_MASK_OUT | qpp.HP_APPLY], ids=["nohp", "hp"])
+def test_jumbo_and_edges(ctx, path, flags):
+    """C4's 8000-B jumbo payload next to empty, 1-B, 4-B and near-64 KiB ones, with and without header protection
+    (pn_len 4: the sample of an empty payload is the tag, payload.rs:151-169)."""
     keys, okeys = _keys(ctx, [1, 2, 3], seed=99)
     slots = [k.slot for k in keys]
     lens = [0, 1, 4, 8000, 8000, 1452, 300, 65535 - 100]
@@ -270,10 +273,12 @@ def test_jumbo_and_edges(ctx, path):
         descs[i] = (2**32 + 7 * i if i % 2 else i, slots[i // len(lens)], off, 21, L, 4, 0, 0)
         off += 21 + L + 16 + 3
     arena = np.random.default_rng(5).integers(0, 256, off + 64, dtype=np.uint8)
-    got, _, st = _run_seal(ctx, descs, arena, 0)
+    got, masks, st = _run_seal(ctx, descs, arena, flags)
     want = arena.copy()
-    orc.seal_batch(okeys, _oracle_keys_for(okeys, descs, slots), want, 0)
+    want_masks = orc.seal_batch(okeys, _oracle_keys_for(okeys, descs, slots), want, flags)
     assert (st == 0).all() and (got == want).all()
+    if flags:
+        assert masks.tobytes() == want_masks
 
 
 def test_hp_mask_batch_receive_side(ctx):

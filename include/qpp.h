@@ -75,6 +75,16 @@ int qpp_ctx_set_burst_max(qpp_ctx *ctx, size_t max_packets);
 #define QPP_AES_KERNEL_LANE 1
 #define QPP_AES_KERNEL_WAVE 2
 int qpp_ctx_set_aes_kernel(qpp_ctx *ctx, int kernel);
+/* FIPS mode: the s2n-quic-crypto `fips` cargo feature (cipher_suite/ring.rs:13-31, aead/fips.rs:13-60).  AES packet
+ * keys created while it is on (qpp_key_new*, _update*, _raw) seal like aws-lc's TLS 1.3 record AEAD
+ * (TlsRecordSealingKey, aws-lc-rs 1.12): a key's first seal fixes mask = its pn, and every seal needs
+ * given = pn ^ mask >= the previous accepted given + 1 (and given != 2^64 - 1); a refused packet is not sealed, its
+ * bytes are left untouched and its status is QPP_INTERNAL_ERROR (qpp_seal returns it; a qpp_txq flush with refused
+ * packets reports it to qpp_txq_wait / qpp_txq_poll).  A batch applies the rule in batch order, per key.
+ * ChaCha20-Poly1305 keys have no FIPS form (ring.rs:116-121); opening is never gated.  Keys created before the call
+ * keep their mode. */
+int qpp_ctx_set_fips(qpp_ctx *ctx, int on);
+int qpp_key_fips(const qpp_key *key);  /* 1: the key seals in FIPS mode */
 int qpp_abi_version(void);
 /* Key-table occupancy (diagnostics / tests): slots allocated, high-water slot index, slots retired but not yet
  * reusable (their zeroization is still behind in-flight batches). */

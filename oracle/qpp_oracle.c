@@ -580,6 +580,41 @@ void orc_seal_batch(const orc_key *keys, const orc_pkt *pkts, size_t n, uint8_t 
     }
 }
 
+/* ---- FIPS mode: the sealing nonce order of aws-lc's TLS 1.3 AES-GCM AEAD (EVP_aead_aes_*_gcm_tls13 behind aws-lc-rs
+ * 1.12 TlsRecordSealingKey, which s2n-quic-crypto's `fips` feature uses: aead/fips.rs:13-60, cipher_suite/ring.rs:13-31).
+ * aws-lc is not vendored in the reference; this restates its published seal check on the nonce bytes themselves:
+ * given = big-endian u64 of nonce[4..12]; the first seal sets mask = given; given ^= mask; refuse if
+ * given == 2^64 - 1 or given < min_next; else min_next = given + 1.  Parity unpinned: the reference holds no vectors. */
+int orc_fips_seal_ok(orc_fips_state *st, const uint8_t nonce[12]) {
+    uint64_t given = 0;
+    for (int i = 4; i < 12; i++) given = (given << 8) | nonce[i];
+    if (!st->seen) {
+        st->mask = given;
+        st->seen = 1;
+    }
+    given ^= st->mask;
+    if (given == UINT64_MAX || given < st->min_next) return 0;
+    st->min_next = given + 1;
+    return 1;
+}
+
+/* orc_seal_batch, one packet after the other, with the FIPS check for keys whose fips[key] is set: a refused packet
+ * is left untouched with status 3 (INTERNAL_ERROR), the others get status 0. */
+void orc_seal_batch_fips(const orc_key *keys, const uint8_t *fips, orc_fips_state *states, const orc_pkt *pkts,
+                         size_t n, uint8_t *arena, uint8_t *masks, int flags, int8_t *status) {
+    for (size_t i = 0; i < n; i++) {
+        const orc_pkt *p = &pkts[i];
+        uint8_t nonce[12];
+        orc_nonce(keys[p->key_idx].iv, p->pn, nonce);
+        if (fips[p->key_idx] && !orc_fips_seal_ok(&states[p->key_idx], nonce)) {
+            status[i] = 3;
+            continue;
+        }
+        status[i] = 0;
+        orc_seal_batch(keys, p, 1, arena, masks ? masks + 5 * i : NULL, flags);
+    }
+}
+
 void orc_open_batch(const orc_key *keys, const orc_pkt *pkts, size_t n, uint8_t *arena, int8_t *status) {
     for (size_t i = 0; i < n; i++) {
         const orc_pkt *p = &pkts[i];

@@ -121,6 +121,14 @@ typedef struct orc_key {
 void orc_seal_batch(const orc_key *keys, const orc_pkt *pkts, size_t n, uint8_t *arena,
                     uint8_t *masks, int flags);
 void orc_open_batch(const orc_key *keys, const orc_pkt *pkts, size_t n, uint8_t *arena, int8_t *status);
+/* FIPS mode (aws-lc TLS 1.3 AEAD sealing nonce order, see qpp_oracle.c) */
+typedef struct orc_fips_state {
+    uint64_t mask, min_next;
+    int seen, pad;
+} orc_fips_state;
+int orc_fips_seal_ok(orc_fips_state *st, const uint8_t nonce[12]);
+void orc_seal_batch_fips(const orc_key *keys, const uint8_t *fips, orc_fips_state *states, const orc_pkt *pkts,
+                         size_t n, uint8_t *arena, uint8_t *masks, int flags, int8_t *status);
 
 /* ---- packet numbers (quic/s2n-quic-core/src/packet/number) ---- */
 /* RFC 9000 A.3 DecodePacketNumber, as rfc_decoder in packet/number/tests.rs:108-159 states it, clamped to

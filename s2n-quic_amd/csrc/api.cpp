@@ -37,6 +37,11 @@ struct StreamState {
     hipEvent_t last = nullptr;  // after this stream's latest batch
     bool used = false;          // `last` has been recorded at least once
     uint64_t key_gen = 0;       // the latest key install this stream has waited for
+    // FIPS-mode nonce-order gate scratch (fips.hip): sort keys, scans, the gated descriptor copy, rocPRIM temp
+    void *fips_buf = nullptr;
+    size_t fips_bytes = 0;
+    uint32_t fips_n_cap = 0;
+    uint32_t *fips_refused = nullptr;  // device word: packets the gate refused (txq flushes report it)
 };
 
 struct Retired {
@@ -94,6 +99,8 @@ struct qpp_ctx {
     uint32_t retired_slots = 0;           // slots in `retired`
     uint32_t live_by_suite[4] = {0, 0, 0, 0};  // live packet keys per suite: which kernels a batch can need
     uint32_t live_slot_xor = 0;                  // XOR of the live packet keys' slots: THE slot when only one is live
+    bool fips = false;                           // qpp_ctx_set_fips: AES packet keys created now seal in FIPS mode
+    uint32_t fips_live = 0;                      // live FIPS keys: seal batches run the nonce-order gate
     uint32_t next_slot = 0;
     // per-stream state (plan scratch, last-batch event); [0] is the context stream
     std::vector<StreamState *> streams;
@@ -169,6 +176,13 @@ void put_event(qpp_ctx *ctx, hipEvent_t e) {
 void free_plan(PlanBuffers &p) {
     hipFree(p.counts); hipFree(p.cursor); hipFree(p.istart); hipFree(p.perm); hipFree(p.work); hipFree(p.n_work);
     p = PlanBuffers{};
+}
+void free_stream_state(StreamState *st) {
+    free_plan(st->plan);
+    hipFree(st->fips_buf);
+    hipFree(st->fips_refused);
+    if (st->last) hipEventDestroy(st->last);
+    delete st;
 }
 
 StreamState *stream_state(qpp_ctx *ctx, hipStream_t s) {
@@ -319,6 +333,36 @@ int ensure_plan(qpp_ctx *ctx, StreamState *st, uint32_t n) {
     return QPP_OK;
 }
 
+// FIPS gate scratch for batches of up to n packets on st (plus its refused-packet counter)
+int ensure_fips(qpp_ctx *ctx, StreamState *st, uint32_t n) {
+    if (!st->fips_refused) {
+        HIP_TRY(ctx, hipMalloc(&st->fips_refused, 256));
+        HIP_TRY(ctx, hipMemsetAsync(st->fips_refused, 0, 4, st->stream));
+    }
+    if (n <= st->fips_n_cap) return QPP_OK;
+    HIP_TRY(ctx, hipStreamSynchronize(st->stream));  // the old scratch is no longer read
+    hipFree(st->fips_buf);
+    st->fips_buf = nullptr;
+    st->fips_n_cap = 0;
+    const uint32_t cap = std::max<uint32_t>(n, 1024);
+    st->fips_bytes = fips_scratch_bytes(cap);
+    HIP_TRY(ctx, hipMalloc(&st->fips_buf, st->fips_bytes));
+    st->fips_n_cap = cap;
+    return QPP_OK;
+}
+
+// FIPS mode: the descriptors the seal kernels read instead of descs (refused packets skipped; status / refused count
+// written).  Unchanged when no FIPS key is live.
+int fips_gate(qpp_ctx *ctx, StreamState *st, const qpp_pkt *&descs, uint32_t n, int8_t *status, uint32_t *refused) {
+    if (!ctx->fips_live || !n) return QPP_OK;
+    RC_TRY(ensure_fips(ctx, st, n));
+    qpp_pkt *gated = nullptr;
+    HIP_TRY(ctx, launch_fips_gate(ctx->d_keys, ctx->key_cap, descs, n, st->fips_buf, st->fips_bytes, &gated, status,
+                                  refused, st->stream));
+    descs = gated;
+    return QPP_OK;
+}
+
 int ensure_stage(qpp_ctx *ctx, size_t bytes) {
     if (bytes <= ctx->stage_cap) return QPP_OK;
     size_t cap = std::max<size_t>(4096, ctx->stage_cap);
@@ -422,6 +466,8 @@ int install(qpp_key *k) {
         d.nr = (uint32_t)aes_expand_key(k->key, kl, d.rk);
         d.hp_nr = (uint32_t)aes_expand_key(k->hp, kl, d.hp_rk);
     }
+    d.fips = ctx->fips && is_aes(k->suite) ? 1u : 0u;  // no FIPS ChaCha20-Poly1305 (cipher_suite/ring.rs:116-121)
+    ctx->fips_live += d.fips;
     mark_dirty(ctx, k->slot);
     ctx->live_by_suite[k->suite]++;
     ctx->live_slot_xor ^= k->slot;
@@ -500,8 +546,9 @@ uint32_t single_aes_slot(const qpp_ctx *ctx) {
 
 // Batch bodies: plan (AES) + kernels on st's stream; keys already flushed.
 int enqueue_seal(qpp_ctx *ctx, StreamState *st, const qpp_pkt *descs, uint32_t n, uint8_t *arena, uint8_t *masks,
-                 int8_t *status, uint32_t flags) {
+                 int8_t *status, uint32_t flags, uint32_t *refused = nullptr) {
     hipStream_t s = st->stream;
+    if (!(flags & QPP_ONLY_CHACHA)) RC_TRY(fips_gate(ctx, st, descs, n, status, refused));
     if (!(flags & QPP_ONLY_CHACHA) && (suite_mask(ctx) & kAesSuites)) {
         const AesPath path = aes_path(ctx, n);
         const uint32_t one = path == AesPath::lane ? single_aes_slot(ctx) : UINT32_MAX;
@@ -580,6 +627,9 @@ int run_one(const qpp_key *k, bool seal, uint64_t pn, const uint8_t *header, siz
     hipStream_t s = ctx->stream;
     const qpp_pkt *vd = (const qpp_pkt *)v;
     int8_t *vst = (int8_t *)(v + 72);
+    if (seal && ctx->h_keys[k->slot].fips) {  // FIPS mode: the nonce-order gate (refused: status INTERNAL_ERROR)
+        RC_TRY(fips_gate(ctx, st, vd, 1, vst, nullptr));
+    }
     if (is_aes(k->suite)) {
         // key_cap = 0: grid = plan_max_work(1, 0, per) = 1; only work item 0 exists
         if (ctx->burst_max)
@@ -594,9 +644,13 @@ int run_one(const qpp_key *k, bool seal, uint64_t pn, const uint8_t *header, siz
     }
     RC_TRY(note_work(ctx, st));
     HIP_TRY(ctx, hipStreamSynchronize(s));
+    *status_out = (int8_t)h[72];
+    if (seal && *status_out != QPP_OK) {  // refused (FIPS nonce order): the caller's buffer stays untouched
+        secure_zero(h, total);
+        return QPP_OK;
+    }
     memcpy(out, pkt + 16 + header_len, payload_len);
     if (seal) memcpy(tag_out, pkt + 16 + header_len + payload_len, 16);
-    *status_out = (int8_t)h[72];
     secure_zero(h, total);
     return QPP_OK;
 }
@@ -643,7 +697,7 @@ int derive_batch(qpp_ctx *ctx, int suite, const uint8_t *secrets, const uint8_t 
     hipStream_t s = ctx->kstream;
     HIP_TRY(ctx, hipMemcpyAsync(d, h, o_slot + 4 * n, hipMemcpyHostToDevice, s));
     HIP_TRY(ctx, launch_key_derive(ctx->d_keys, (const uint32_t *)(d + o_slot), (uint32_t)n, suite, d,
-                                   hp_in ? d + o_hp : nullptr, updates, d + o_mat, ctx->pow, s));
+                                   hp_in ? d + o_hp : nullptr, updates, d + o_mat, ctx->fips ? 1u : 0u, ctx->pow, s));
     HIP_TRY(ctx, hipMemcpyAsync(h + o_mat, d + o_mat, n * mb, hipMemcpyDeviceToHost, s));
     HIP_TRY(ctx, hipMemsetAsync(d, 0, total, s));
     HIP_TRY(ctx, hipEventRecord(ctx->keys_ready, s));
@@ -667,6 +721,8 @@ int derive_batch(qpp_ctx *ctx, int suite, const uint8_t *secrets, const uint8_t 
         r.suite = (uint32_t)suite;
         r.nr = r.hp_nr = nr;
         r.live = 1;
+        r.fips = ctx->fips && is_aes(suite) ? 1u : 0u;  // as key_derive_kernel sets it on the device
+        ctx->fips_live += r.fips;
         ctx->live_slot_xor ^= slots[i];
         out[i] = k;
     }
@@ -765,6 +821,17 @@ int qpp_ctx_set_aes_kernel(qpp_ctx *ctx, int kernel) {
     return QPP_OK;
 }
 
+int qpp_ctx_set_fips(qpp_ctx *ctx, int on) {
+    if (!ctx) return QPP_INTERNAL_ERROR;
+    ctx->fips = on != 0;
+    return QPP_OK;
+}
+
+int qpp_key_fips(const qpp_key *key) {
+    if (!key || !key->ctx || key->slot >= key->ctx->key_cap) return 0;
+    return key->ctx->h_keys[key->slot].fips ? 1 : 0;
+}
+
 int qpp_ctx_set_burst_max(qpp_ctx *ctx, size_t max_packets) {
     if (!ctx) return QPP_INTERNAL_ERROR;
     ctx->burst_max = max_packets > UINT32_MAX ? UINT32_MAX : (uint32_t)max_packets;
@@ -787,11 +854,7 @@ void qpp_ctx_destroy(qpp_ctx *ctx) {
         hipStreamSynchronize(ctx->stream);
         hipFree(ctx->pow.base);
     }
-    for (StreamState *st : ctx->streams) {
-        free_plan(st->plan);
-        if (st->last) hipEventDestroy(st->last);
-        delete st;
-    }
+    for (StreamState *st : ctx->streams) free_stream_state(st);
     for (Retired &r : ctx->retired) hipEventDestroy(r.done);
     for (hipEvent_t e : ctx->event_pool) hipEventDestroy(e);
     if (ctx->pipe) {
@@ -949,6 +1012,7 @@ void qpp_key_free(qpp_key *key) {
     if (ctx && key->slot < ctx->key_cap && ctx->h_keys[key->slot].live == 1) {
         ctx->live_by_suite[key->suite]--;
         ctx->live_slot_xor ^= key->slot;
+        ctx->fips_live -= ctx->h_keys[key->slot].fips;
         retire_slot(ctx, key->slot);
     }
     secure_zero(key, sizeof *key);
@@ -1417,9 +1481,7 @@ void qpp_stream_destroy(qpp_ctx *ctx, void *stream) {
         for (size_t i = 0; i < ctx->streams.size(); i++) {
             StreamState *st = ctx->streams[i];
             if (st->stream != s) continue;
-            free_plan(st->plan);
-            if (st->last) hipEventDestroy(st->last);
-            delete st;
+            free_stream_state(st);
             ctx->streams.erase(ctx->streams.begin() + (long)i);
             break;
         }
@@ -1470,6 +1532,7 @@ struct TxqSlot {
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
     uint64_t first = 0, last = 0;  // tickets (bursts) of the flush that last used this slot (0: never)
+    uint32_t *h_refused = nullptr;  // pinned: packets of the flush the FIPS nonce-order gate refused
     bool busy = false;    // `done` recorded and not yet seen complete
     size_t lo = 0, hi = 0;  // ring span of that flush (DMA path)
 };
@@ -1536,8 +1599,10 @@ int qpp_txq_create_async(qpp_ctx *ctx, size_t ring_bytes, size_t max_packets, si
             bad(hipMalloc(&sl.d_desc, sizeof(qpp_pkt) * max_packets), "txq descs") ||
             bad(hipHostMalloc(&sl.h_perm, 4 * (max_packets + 4) + sizeof(WorkItem) * (max_packets + 1),
                               hipHostMallocDefault), "txq plan") ||
-            bad(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming), "txq event"))
+            bad(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming), "txq event") ||
+            bad(hipHostMalloc(&sl.h_refused, 64, hipHostMallocDefault), "txq refused count"))
             return QPP_DEVICE_ERROR;
+        *sl.h_refused = 0;
         sl.h_nwork = sl.h_perm + max_packets;
         sl.h_work = (WorkItem *)(sl.h_perm + max_packets + 4);  // 16-byte aligned
         if (bad(hipHostGetDevicePointer(&v, sl.h_desc, 0), "txq desc view")) return QPP_DEVICE_ERROR;
@@ -1570,6 +1635,7 @@ void qpp_txq_destroy(qpp_txq *q) {
         if (sl.d_desc) hipFree(sl.d_desc);
         if (sl.h_perm) hipHostFree(sl.h_perm);
         if (sl.done) hipEventDestroy(sl.done);
+        if (sl.h_refused) hipHostFree(sl.h_refused);
     }
     for (hipStream_t st : q->streams) {
         // the stream's StreamState (plan scratch of the DMA path) goes with it
@@ -1628,9 +1694,11 @@ int qpp_txq_push_descs(qpp_txq *q, const qpp_pkt *descs, size_t n) {
 
 // Zero-copy flush: host plan (AES packets grouped by key, work items of whole waves) in the slot's pinned memory,
 // then the burst kernel (AES) and the ChaCha kernel on the pinned ring itself; one launch per suite family.
-static int txq_enqueue_zero_copy(qpp_txq *q, TxqSlot &sl, uint32_t n) {
+static int txq_enqueue_zero_copy(qpp_txq *q, TxqSlot &sl, StreamState *st, uint32_t n) {
     qpp_ctx *ctx = q->ctx;
     hipStream_t s = sl.stream;
+    const qpp_pkt *descs = sl.v_desc;
+    RC_TRY(fips_gate(ctx, st, descs, n, nullptr, st->fips_refused));
     if (q->suites & kAesSuites) {
         std::vector<uint32_t> &ord = q->order;
         ord.clear();
@@ -1651,12 +1719,12 @@ static int txq_enqueue_zero_copy(qpp_txq *q, TxqSlot &sl, uint32_t n) {
         }
         std::copy(ord.begin(), ord.end(), sl.h_perm);
         *sl.h_nwork = items;
-        HIP_TRY(ctx, launch_aes_gcm_burst(true, ctx->d_keys, sl.v_desc, sl.v_plan, (uint32_t)ord.size(), keys, per,
+        HIP_TRY(ctx, launch_aes_gcm_burst(true, ctx->d_keys, descs, sl.v_plan, (uint32_t)ord.size(), keys, per,
                                           q->v_ring, nullptr, nullptr, QPP_HP_APPLY, q->suites & kAesSuites, ctx->pow,
                                           s));
     }
     if (q->suites & ~kAesSuites)
-        HIP_TRY(ctx, launch_chacha(true, ctx->d_keys, ctx->key_cap, sl.v_desc, n, q->v_ring, nullptr, nullptr,
+        HIP_TRY(ctx, launch_chacha(true, ctx->d_keys, ctx->key_cap, descs, n, q->v_ring, nullptr, nullptr,
                                    QPP_HP_APPLY, true, s));
     return QPP_OK;
 }
@@ -1667,6 +1735,13 @@ static int txq_slot_drain(qpp_txq *q, TxqSlot &sl) {
     HIP_TRY(q->ctx, hipEventSynchronize(sl.done));
     sl.busy = false;
     return QPP_OK;
+}
+// A completed flush whose packets the FIPS nonce-order gate refused (left unsealed in the ring) reports
+// QPP_INTERNAL_ERROR once: to the first wait / poll of one of its tickets, or else to the flush that reuses its slot.
+static int txq_refused(TxqSlot &sl) {
+    if (!*sl.h_refused) return QPP_OK;
+    *sl.h_refused = 0;
+    return QPP_INTERNAL_ERROR;
 }
 
 // Sends slots[cur] (every burst flushed into it) and moves on to the next slot, once that one's last flush is over.
@@ -1679,8 +1754,13 @@ static int txq_submit(qpp_txq *q) {
     const uint32_t n = (uint32_t)q->count;
     StreamState *st = nullptr;
     RC_TRY(batch_stream(ctx, sl.stream, &st));  // sees the latest key install
+    const bool gate = ctx->fips_live > 0;
+    if (gate) {
+        RC_TRY(ensure_fips(ctx, st, n));
+        HIP_TRY(ctx, hipMemsetAsync(st->fips_refused, 0, 4, sl.stream));
+    }
     if (n <= q->zc_max) {
-        RC_TRY(txq_enqueue_zero_copy(q, sl, n));
+        RC_TRY(txq_enqueue_zero_copy(q, sl, st, n));
     } else {
         hipStream_t s = sl.stream;
         const size_t span = q->hi - q->lo;
@@ -1689,9 +1769,10 @@ static int txq_submit(qpp_txq *q) {
         uint32_t flags = QPP_HP_APPLY;
         if (!(q->suites & ~kAesSuites)) flags |= QPP_ONLY_AES;
         else if (!(q->suites & kAesSuites)) flags |= QPP_ONLY_CHACHA;
-        RC_TRY(enqueue_seal(ctx, st, sl.d_desc, n, q->d_ring, nullptr, nullptr, flags));
+        RC_TRY(enqueue_seal(ctx, st, sl.d_desc, n, q->d_ring, nullptr, nullptr, flags, st->fips_refused));
         HIP_TRY(ctx, hipMemcpyAsync(q->h_ring + q->lo, q->d_ring + q->lo, span, hipMemcpyDeviceToHost, s));
     }
+    if (gate) HIP_TRY(ctx, hipMemcpyAsync(sl.h_refused, st->fips_refused, 4, hipMemcpyDeviceToHost, sl.stream));
     RC_TRY(note_work(ctx, st));  // key retirement orders behind this flush
     HIP_TRY(ctx, hipEventRecord(sl.done, sl.stream));
     sl.busy = true;
@@ -1707,7 +1788,8 @@ static int txq_submit(qpp_txq *q) {
     q->suites = 0;
     // the next batch fills the next slot, once that slot's previous flush is over (back-pressure)
     q->cur = (q->cur + 1) % q->slots.size();
-    return txq_slot_drain(q, q->slots[q->cur]);
+    RC_TRY(txq_slot_drain(q, q->slots[q->cur]));
+    return txq_refused(q->slots[q->cur]);
 }
 
 int qpp_txq_set_coalesce(qpp_txq *q, size_t bursts) {
@@ -1746,13 +1828,14 @@ int qpp_txq_poll(qpp_txq *q, uint64_t ticket, int *done) {
     if (ticket >= q->next_ticket) return QPP_INTERNAL_ERROR;
     TxqSlot *sl = nullptr;
     RC_TRY(txq_slot_of(q, ticket, &sl));
-    if (!sl || !sl->busy) { *done = 1; return QPP_OK; }
+    if (!sl) { *done = 1; return QPP_OK; }
+    if (!sl->busy) { *done = 1; return txq_refused(*sl); }
     const hipError_t e = hipEventQuery(sl->done);
     if (e == hipErrorNotReady) { *done = 0; return QPP_OK; }
     HIP_TRY(q->ctx, e);
     sl->busy = false;
     *done = 1;
-    return QPP_OK;
+    return txq_refused(*sl);
 }
 
 int qpp_txq_wait(qpp_txq *q, uint64_t ticket) {
@@ -1761,7 +1844,8 @@ int qpp_txq_wait(qpp_txq *q, uint64_t ticket) {
     TxqSlot *sl = nullptr;
     RC_TRY(txq_slot_of(q, ticket, &sl));
     if (!sl) return QPP_OK;
-    return txq_slot_drain(q, *sl);
+    RC_TRY(txq_slot_drain(q, *sl));
+    return txq_refused(*sl);
 }
 
 int qpp_txq_flush(qpp_txq *q) {

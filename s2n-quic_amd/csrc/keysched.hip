@@ -173,7 +173,7 @@ constexpr int kMatSecret = 0, kMatKey = 48, kMatIv = 80, kMatHp = 96, kMatBytes 
 __global__ __launch_bounds__(64) void key_derive_kernel(DevKey *keys, const uint32_t *__restrict__ slots, uint32_t n,
                                                        int suite, const uint8_t *__restrict__ secrets,
                                                        const uint8_t *__restrict__ hp_in, uint32_t updates,
-                                                       uint8_t *material) {
+                                                       uint8_t *material, uint32_t fips) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const int hl = suite == QPP_SUITE_TLS_AES_256_GCM_SHA384 ? 48 : 32;
@@ -212,6 +212,10 @@ __global__ __launch_bounds__(64) void key_derive_kernel(DevKey *keys, const uint
         k->hp_nr = (uint32_t)aes_expand(hp, kl, k->hp_rk);
     }
     k->live = 1;
+    k->fips = fips && suite != QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256 ? 1u : 0u;  // no FIPS ChaCha (ring.rs:116-121)
+    k->fips_seen = 0;
+    k->fips_mask = 0;
+    k->fips_min_next = 0;
     uint8_t *m = material + (size_t)i * kMatBytes;
     for (int j = 0; j < hl; j++) m[kMatSecret + j] = s[j];
     for (int j = 0; j < kl; j++) m[kMatKey + j] = key[j];
@@ -225,11 +229,11 @@ __global__ __launch_bounds__(64) void key_derive_kernel(DevKey *keys, const uint
 uint32_t key_material_bytes() { return kMatBytes; }
 
 hipError_t launch_key_derive(DevKey *keys, const uint32_t *slots, uint32_t n, int suite, const uint8_t *secrets,
-                             const uint8_t *hp_in, uint32_t updates, uint8_t *material, const PowTables &pow,
-                             hipStream_t s) {
+                             const uint8_t *hp_in, uint32_t updates, uint8_t *material, uint32_t fips,
+                             const PowTables &pow, hipStream_t s) {
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(key_derive_kernel, dim3((n + 63) / 64), dim3(64), 0, s, keys, slots, n, suite, secrets, hp_in,
-                       updates, material);
+                       updates, material, fips);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     return launch_key_install(keys, slots, nullptr, n, pow, s);

@@ -75,8 +75,14 @@ struct alignas(16) DevKey {
     uint32_t hp_rk[60];  // AES HP round keys                | ChaCha HP key in hp_rk[0..8)
     uint32_t H[4];       // GHASH key E_K(0^128)                  (filled on device by key setup)
     uint32_t V[128][4];  // V[m] = H * x^m in GCM bit order      (filled on device by key setup)
+    // FIPS mode (fips.hip): the sealing nonce-order state of aws-lc's TLS 1.3 AEAD, kept and advanced on the device
+    uint32_t fips;           // 1: seals are gated (an AES packet key created with qpp_ctx_set_fips on)
+    uint32_t fips_seen;      // 1 once the key's first seal fixed fips_mask
+    uint64_t fips_mask;      // pn of the key's first seal (given = pn ^ mask)
+    uint64_t fips_min_next;  // the smallest given the next seal may use
+    uint64_t fips_pad;
 };
-static_assert(sizeof(DevKey) == 2576, "DevKey layout");
+static_assert(sizeof(DevKey) == 2608, "DevKey layout");
 
 // Grouping of an AES batch by key (GHASH tables are per key and live in LDS).
 struct WorkItem {
@@ -124,9 +130,10 @@ hipError_t launch_key_install(DevKey *keys, const uint32_t *slots, const DevKey 
 // keysched.hip: n secrets -> updates x "quic ku" -> key/iv -> DevKey records keys[slots[i]] and per-key material
 // (secret' | key | iv | hp, key_material_bytes() each); then key install.  The header key is derived from the given
 // secret ("quic hp") when hp_in is nullptr, else taken from hp_in (suite key length per key: update batches).
+// fips: the new keys seal in FIPS mode (AES suites only; see DevKey::fips)
 hipError_t launch_key_derive(DevKey *keys, const uint32_t *slots, uint32_t n, int suite, const uint8_t *secrets,
-                             const uint8_t *hp_in, uint32_t updates, uint8_t *material, const PowTables &pow,
-                             hipStream_t s);
+                             const uint8_t *hp_in, uint32_t updates, uint8_t *material, uint32_t fips,
+                             const PowTables &pow, hipStream_t s);
 uint32_t key_material_bytes();
 hipError_t launch_plan(const DevKey *keys, uint32_t key_cap, const qpp_pkt *descs, uint32_t n, PlanBuffers pb,
                        uint32_t per, hipStream_t s);
@@ -162,6 +169,13 @@ hipError_t launch_unprotect(const DevKey *keys, uint32_t key_cap, const qpp_rx_p
                             qpp_pkt *descs_out, int8_t *status, hipStream_t s);
 hipError_t launch_hp_mask(const DevKey *keys, uint32_t key_cap, const qpp_pkt *descs, uint32_t n,
                           const uint8_t *arena, uint8_t *masks, hipStream_t s);
+// FIPS mode (fips.hip): copies descs[0, n) to *descs_out (in scratch) with QPP_PKT_SKIP on every packet of a FIPS key
+// whose nonce does not come strictly after its key's previous seal (batch order), status[j] = QPP_INTERNAL_ERROR for
+// them (status may be nullptr) and *refused += their count (may be nullptr); advances the keys' nonce state.
+size_t fips_scratch_bytes(uint32_t n);
+hipError_t launch_fips_gate(DevKey *keys, uint32_t key_cap, const qpp_pkt *descs, uint32_t n, void *scratch,
+                            size_t scratch_bytes, qpp_pkt **descs_out, int8_t *status, uint32_t *refused,
+                            hipStream_t s);
 
 // ---------------------------------------------------------------- host key schedule (kdf.cpp)
 size_t suite_key_len(int suite);

@@ -58,7 +58,7 @@ EXPORTS = [
     "qpp_dc_open_in_place", "qpp_ctx_key_slots", "qpp_key_new_pair", "qpp_key_update_batch", "qpp_initial_keys_pair",
     "qpp_header_key_new", "qpp_header_key_new_raw", "qpp_header_key_free", "qpp_header_key_slot",
     "qpp_header_key_suite", "qpp_header_key_sample_len", "qpp_header_key_mask", "qpp_host_batch_submit",
-    "qpp_host_batch_query", "qpp_host_batch_wait", "qpp_ctx_set_host_pipe",
+    "qpp_host_batch_query", "qpp_host_batch_wait", "qpp_ctx_set_host_pipe", "qpp_ctx_set_fips", "qpp_key_fips",
 ]
 OP_SEAL, OP_OPEN = 0x1, 0x2
 
@@ -98,6 +98,8 @@ def lib():
             "qpp_key_free": (None, [vp]),
             "qpp_key_free_batch": (None, [vp, sz]),
             "qpp_ctx_set_aes_kernel": (ctypes.c_int, [vp, ctypes.c_int]),
+            "qpp_ctx_set_fips": (ctypes.c_int, [vp, ctypes.c_int]),
+            "qpp_key_fips": (ctypes.c_int, [vp]),
             "qpp_key_slot": (u32, [vp]),
             "qpp_key_slot_batch": (None, [vp, sz, vp]),
             "qpp_key_suite": (ctypes.c_int, [vp]),
@@ -247,6 +249,11 @@ class Context:
     def set_aes_kernel(self, kernel):
         """AES_KERNEL_AUTO / _LANE / _WAVE for batches above burst_max (identical outputs; A/B and tests)."""
         self._check(lib().qpp_ctx_set_aes_kernel(self.handle, int(kernel)), "set_aes_kernel")
+
+    def set_fips(self, on=True):
+        """FIPS mode (the s2n-quic-crypto `fips` feature): AES packet keys created from now on seal with aws-lc's TLS 1.3
+        nonce-order rule (qpp.h qpp_ctx_set_fips); refused packets get status INTERNAL_ERROR and stay untouched."""
+        self._check(lib().qpp_ctx_set_fips(self.handle, 1 if on else 0), "set_fips")
 
     def sync(self, stream=None):
         self._check(lib().qpp_stream_synchronize(self.handle, stream), "sync")
@@ -456,6 +463,11 @@ class Key:
     @property
     def suite(self):
         return lib().qpp_key_suite(self.handle)
+
+    @property
+    def fips(self):
+        """True when the key seals in FIPS mode (Context.set_fips was on when it was created; AES suites only)."""
+        return bool(lib().qpp_key_fips(self.handle))
 
     def tag_len(self):
         return lib().qpp_tag_len(self.handle)

@@ -162,6 +162,27 @@ def seal_batch(keys, pkts, arena, flags=0):
     return bytes(masks[:5 * n])
 
 
+class OrcFipsState(ctypes.Structure):
+    _fields_ = [("mask", ctypes.c_uint64), ("min_next", ctypes.c_uint64), ("seen", ctypes.c_int), ("pad", ctypes.c_int)]
+
+
+def fips_states(nkeys):
+    """per-key FIPS nonce-order state, kept across batches (orc_fips_seal_ok)"""
+    return (OrcFipsState * max(nkeys, 1))()
+
+
+def seal_batch_fips(keys, fips, states, pkts, arena, flags=0):
+    """orc_seal_batch in batch order with aws-lc's TLS 1.3 nonce-order check on keys with fips[k]: returns (masks,
+    status); refused packets stay untouched with status 3 (INTERNAL_ERROR)."""
+    n = len(pkts)
+    masks = (ctypes.c_uint8 * (5 * n + 1))()
+    status = (ctypes.c_int8 * (n + 1))()
+    on = (ctypes.c_uint8 * max(len(fips), 1))(*[1 if f else 0 for f in fips])
+    lib().orc_seal_batch_fips(keys, on, states, pkts.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(n),
+                              arena.ctypes.data_as(ctypes.c_void_p), masks, flags, status)
+    return bytes(masks[:5 * n]), list(status[:n])
+
+
 def open_batch(keys, pkts, arena):
     n = len(pkts)
     status = (ctypes.c_int8 * (n + 1))()

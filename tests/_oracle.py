@@ -6,6 +6,8 @@ import ctypes
 import os
 import subprocess
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_DIR = os.path.join(ROOT, "oracle")
 SUITES = {"aes128gcm": 1, "aes256gcm": 2, "chacha20poly1305": 3}
@@ -160,6 +162,27 @@ def seal_batch(keys, pkts, arena, flags=0):
     lib().orc_seal_batch(keys, pkts.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(n),
                          arena.ctypes.data_as(ctypes.c_void_p), masks, flags)
     return bytes(masks[:5 * n])
+
+
+_fc = None
+
+
+def fast_seal_batch(keys, pkts, arena, flags=0, threads=16):
+    """seal_batch through oracle/libfastcheck.so (OpenSSL EVP on up to 16 threads; same semantics, checked against the
+    restatement in tests/test_fastcheck.py): for comparing EVERY packet of a full-size GPU batch."""
+    global _fc
+    if _fc is None:
+        path = os.path.join(ORACLE_DIR, "libfastcheck.so")
+        if not os.path.exists(path):
+            subprocess.check_call(["make", "-s", "-C", ORACLE_DIR, "libfastcheck.so"])
+        _fc = ctypes.CDLL(path)
+    n = len(pkts)
+    masks = np.zeros(5 * n + 1, dtype=np.uint8)
+    ok = _fc.fc_seal_batch(keys, pkts.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(n),
+                           arena.ctypes.data_as(ctypes.c_void_p), masks.ctypes.data_as(ctypes.c_void_p), flags,
+                           threads)
+    assert ok == 1, "OpenSSL refused a call in fc_seal_batch"
+    return masks[:5 * n]
 
 
 class OrcFipsState(ctypes.Structure):

@@ -185,6 +185,27 @@ def fast_seal_batch(keys, pkts, arena, flags=0, threads=16):
     return masks[:5 * n]
 
 
+def check_full_seal(keys, slots, descs, arena_in, sealed, masks=None, flags=0):
+    """every packet of a GPU-sealed batch against fast_seal_batch: keys = OrcKey array indexed like `slots` (device
+    slots); returns the number of packets compared (asserts on the first mismatch, naming it)"""
+    lut = np.full(int(max(slots)) + 1, -1, dtype=np.int64)
+    lut[np.asarray(slots, dtype=np.int64)] = np.arange(len(slots))
+    d = descs.copy()
+    d["key_idx"] = lut[descs["key_idx"].astype(np.int64)]
+    assert (d["key_idx"] >= 0).all()
+    want = arena_in.copy()
+    want_masks = fast_seal_batch(keys, d, want, flags)
+    if not (sealed == want).all():
+        bad = int(np.flatnonzero(sealed != want)[0])
+        i = int(np.searchsorted(descs["off"].astype(np.int64), bad, side="right")) - 1
+        raise AssertionError(f"sealed bytes differ from the checker, first at arena byte {bad} (packet ~{i})")
+    if masks is not None and flags & 1:
+        m = np.asarray(masks, dtype=np.uint8)[:5 * len(descs)]
+        if not (m == want_masks).all():
+            raise AssertionError(f"HP mask differs, first at packet {int(np.flatnonzero(m != want_masks)[0]) // 5}")
+    return len(descs)
+
+
 class OrcFipsState(ctypes.Structure):
     _fields_ = [("mask", ctypes.c_uint64), ("min_next", ctypes.c_uint64), ("seen", ctypes.c_int), ("pad", ctypes.c_int)]
 

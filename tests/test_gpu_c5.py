@@ -7,7 +7,8 @@ update): the 4096 keys are built on the device by qpp_key_new_batch from 4096 se
 batch A (first 1 Mi packets) is submitted; while it is in flight half the keys are rotated (qpp_key_update_batch)
 and the OLD keys of that half are freed; batch B (second 1 Mi packets) names the new keys for that half.  Checks:
   * a seeded sample of 4096 packets of A and B (ciphertext, tag, HP mask) is bit-exact with the oracle, using the
-    keys each packet was sealed with (A: all old keys, freed mid-flight; B: rotated or kept);
+    keys each packet was sealed with (A: all old keys, freed mid-flight; B: rotated or kept), and EVERY packet is
+    bit-exact with the full-size checker (oracle/fastcheck.c, itself checked against the oracle);
   * every packet round-trips: A is opened with the old keys re-created from their material, B with its own keys;
     every status is OK and every payload equals the original plaintext.
 """
@@ -85,6 +86,20 @@ def _run(ctx):
     got = np.concatenate([host[i * stride:(i + 1) * stride] for i in pick])
     assert (got == sub_arena).all(), "ciphertext/tag differ from the oracle"
     assert np.concatenate([masks[5 * i:5 * i + 5] for i in pick]).tobytes() == want_masks
+
+    # every packet against the full-size checker (oracle/fastcheck.c): oracle keys 0..4095 = the old keys,
+    # 4096 + c = connection c's rotated key (batch B only)
+    all_keys = orc.make_keys([(suite, *old_mat[c]) for c in range(N_KEYS)] +
+                             [(suite, *new_mat[int(c)]) for c in rot])
+    full = descs.copy()
+    kk = conn.copy()
+    rotated_b = (np.arange(N) >= half) & np.isin(conn, rot)
+    kk[rotated_b] = N_KEYS + conn[rotated_b]
+    full["key_idx"] = kk
+    want_all = arena.copy()
+    want_all_masks = orc.fast_seal_batch(all_keys, full, want_all, qpp.HP_MASK_OUT)
+    assert (host == want_all).all(), "a packet differs from the full-size checker"
+    assert (masks == want_all_masks).all()
 
     # full round trip: A with its (freed) old keys re-created from their material, B with its own keys
     recreated = {int(i): ctx.raw_key(suite, *old_mat[i]) for i in rot}

@@ -307,7 +307,8 @@ def test_hp_mask_batch_receive_side(ctx):
 @pytest.mark.parametrize("suite", [1, 2, 3])
 def test_full_size_round_trip(ctx, suite):
     """BASELINE configs 2/3 size (1 Mi x 1200 B): seal -> open round trip restores every payload, every
-    status is OK, and a seeded sample of packets is bit-exact against the oracle."""
+    status is OK, a seeded sample of packets is bit-exact against the oracle and every packet against the full-size
+    checker."""
     n, pt_len = 1 << 20, 1200
     keys, okeys = _keys(ctx, [suite] * (1 if suite == 1 else 64), seed=suite)
     slots = [k.slot for k in keys]
@@ -329,6 +330,8 @@ def test_full_size_round_trip(ctx, suite):
     sub_got = np.concatenate([sealed[i * stride:(i + 1) * stride] for i in pick])
     assert (sub_got == sub_want).all()
     assert np.concatenate([masks[5 * i:5 * i + 5] for i in pick]).tobytes() == want_masks
+    # and EVERY packet (ciphertext, tag, mask) against the full-size checker (oracle/fastcheck.c)
+    assert orc.check_full_seal(okeys, slots, descs, arena, sealed, masks, qpp.HP_MASK_OUT) == n
     ctx.open_batch(d_desc, n, d_arena, d_status)
     st = d_status.download(dtype=np.int8)
     opened = d_arena.download()
@@ -378,6 +381,7 @@ def test_full_size_many_keys(ctx, kernel):
         want_masks = orc.seal_batch(okeys, _oracle_keys_for(okeys, sub_d, slots), want, qpp.HP_MASK_OUT)
         assert (np.concatenate([sealed[i * stride:(i + 1) * stride] for i in pick]) == want).all()
         assert np.concatenate([masks[5 * i:5 * i + 5] for i in pick]).tobytes() == want_masks
+        assert orc.check_full_seal(okeys, slots, descs, arena, sealed, masks, qpp.HP_MASK_OUT) == n  # every packet
         ctx.open_batch(d_desc, n, d_arena, d_status)
         assert (d_status.download(dtype=np.int8) == 0).all()
         v, a = d_arena.download().reshape(n, stride), arena.reshape(n, stride)

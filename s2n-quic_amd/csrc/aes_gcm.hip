@@ -469,6 +469,51 @@ __global__ __launch_bounds__(WG) void aes_gcm_kernel(const DevKey *__restrict__ 
     }
 }
 
+// Fused receive path (unprotect -> PN expand -> open in ONE launch) for a context whose only live
+// packet key is the AES key `single` (one connection, or a server process per key; the plan-free case of
+// aes_gcm_kernel): each lane removes its packet's header protection, expands the PN and picks the key by the phase bit
+// (rx_unprotect_one, as unprotect_kernel does), writes the qpp_pkt the two-launch path would have written, and opens
+// the packet with the workgroup's tables.  Packets whose chosen key is not `single` are refused (INTERNAL_ERROR) as
+// the plan-free open refuses them.  Saves the separate unprotect launch (its own AES table build per 1024 packets) and
+// the re-read of the descriptors.  Outputs (arena, descs_out, status) equal the two-launch path's bit for bit
+// (tests/test_gpu_rx_fused.py).
+template <int NB, int WG, int NR>
+__global__ __launch_bounds__(WG) void aes_gcm_rx_kernel(const DevKey *__restrict__ keys, uint32_t key_cap,
+                                                       const qpp_rx_pkt *__restrict__ rx, uint32_t n, uint32_t single,
+                                                       uint8_t *__restrict__ arena, qpp_pkt *__restrict__ descs_out,
+                                                       int8_t *status) {
+    const uint32_t P = ((n + gridDim.x - 1) / gridDim.x + 63u) & ~63u;  // whole waves per slice
+    const uint32_t lo = min(n, blockIdx.x * P), hi = min(n, (blockIdx.x + 1) * P);
+    if (lo >= hi) return;  // uniform
+    const AesLds aes = make_aes(kLdsAes);
+    const GhashT<NR == 10> gh = GhashT<NR == 10>::make();
+    Stage<NB> st;
+    st.lane = threadIdx.x & 63u;
+    st.base = kLdsStage + (threadIdx.x >> 6) * (64u * 16u * NB);
+    const DevKey *__restrict__ key = keys + single;
+    build_tables(key);
+    uint32_t rk[4 * (NR + 1)];
+#pragma unroll
+    for (int r = 0; r < 4 * (NR + 1); r++) rk[r] = __builtin_amdgcn_readfirstlane(key->rk[r]);
+    for (uint32_t t0 = lo; t0 < hi; t0 += WG) {
+        const uint32_t t = t0 + threadIdx.x;
+        const bool real = t < hi;
+        const uint32_t pi = real ? t : lo;
+        qpp_pkt d{};  // helper lanes: an empty packet at offset 0 (only its pointer arithmetic is used)
+        bool has = false;
+        if (real) {
+            d = rx_unprotect_one(aes, keys, key_cap, rx[pi], arena, status, pi);
+            descs_out[pi] = d;
+            has = !(d.flags & QPP_PKT_SKIP);
+            if (has && d.key_idx != single) {  // the phase's key is not the live one: refused, payload untouched
+                status[pi] = QPP_INTERNAL_ERROR;
+                has = false;
+            }
+        }
+        process_packet<NR, NB, false>(aes, gh, st, key, rk, has, d, pi, arena, nullptr, status, 0u);
+    }
+}
+
 // Many keys, few packets per key (key churn, a chunk of a host batch): work items of <= 64 packets of one key (a
 // wave), each wave with its own key's Ghash4 tables and round keys, the AES T-tables shared by the workgroup.  A
 // workgroup loops over items (grid-stride over waves), so every lane has a packet whenever its key has >= 64 packets
@@ -629,6 +674,23 @@ hipError_t launch_aes_gcm_single(bool seal, const DevKey *keys, const qpp_pkt *d
         if (seal) launch_variant<true, 14>(v, grid, s, keys, descs, none, arena, masks, status, flags, slot, n);
         else launch_variant<false, 14>(v, grid, s, keys, descs, none, arena, masks, status, flags, slot, n);
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_aes_gcm_rx(const DevKey *keys, uint32_t key_cap, const qpp_rx_pkt *rx, uint32_t n, uint32_t slot,
+                             uint32_t nr, uint32_t n_cu, uint8_t *arena, qpp_pkt *descs_out, int8_t *status,
+                             hipStream_t s) {
+    if (!n) return hipSuccess;
+    const uint32_t waves = (n + 63) / 64;
+    const dim3 grid(waves < n_cu ? waves : n_cu);
+    constexpr uint32_t lds = lds_bytes(4, 512);
+    static_assert(lds <= kLdsMax, "LDS budget");
+    if (nr == 10)
+        hipLaunchKernelGGL((aes_gcm_rx_kernel<4, 512, 10>), grid, dim3(512), lds, s, keys, key_cap, rx, n, slot, arena,
+                           descs_out, status);
+    else
+        hipLaunchKernelGGL((aes_gcm_rx_kernel<4, 512, 14>), grid, dim3(512), lds, s, keys, key_cap, rx, n, slot, arena,
+                           descs_out, status);
     return hipGetLastError();
 }
 

@@ -1275,6 +1275,18 @@ int qpp_unprotect_open_batch(qpp_ctx *ctx, const qpp_rx_pkt *rx, size_t n, uint8
     RC_TRY(flush_keys(ctx));
     StreamState *st = nullptr;
     RC_TRY(batch_stream(ctx, stream, &st));
+    // One live AES packet key and a lane-kernel batch: ONE fused launch (unprotect -> PN expand -> open; the same
+    // outputs).  QPP_RX_FUSED=0 forces the two-launch path (A/B, tests).
+    const char *fz = getenv("QPP_RX_FUSED");
+    const uint32_t one = !(flags & QPP_ONLY_CHACHA) && !(fz && fz[0] == '0') &&
+                                 aes_path(ctx, (uint32_t)n) == AesPath::lane
+                             ? single_aes_slot(ctx)
+                             : UINT32_MAX;
+    if (one != UINT32_MAX) {
+        HIP_TRY(ctx, launch_aes_gcm_rx(ctx->d_keys, ctx->key_cap, rx, (uint32_t)n, one, ctx->h_keys[one].nr, ctx->n_cu,
+                                       arena, descs_out, status, st->stream));
+        return note_work(ctx, st);
+    }
     // 1. header unprotection + PN expansion + key-phase choice -> descs_out (device); 2. the open kernels on them,
     // grouped by the chosen key like any batch (skipped packets keep their DECODE_ERROR status)
     HIP_TRY(ctx, launch_unprotect(ctx->d_keys, ctx->key_cap, rx, (uint32_t)n, arena, descs_out, status, st->stream));

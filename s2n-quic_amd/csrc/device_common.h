@@ -368,6 +368,108 @@ __device__ __forceinline__ void hp_finish(const AesLds &aes, const uint32_t *hp_
     hp.finish(aes, sample, base, hdr_len, pn_len, mask_out, flags);
 }
 
+// ---------------------------------------------------------------- ChaCha20 block (RFC 8439 §2.3) and the ChaCha HP mask
+__device__ __forceinline__ uint32_t rotl(uint32_t v, int c) { return __builtin_amdgcn_alignbit(v, v, 32 - c); }
+
+#define QR(a, b, c, d)                \
+    a += b; d ^= a; d = rotl(d, 16);  \
+    c += d; b ^= c; b = rotl(b, 12);  \
+    a += b; d ^= a; d = rotl(d, 8);   \
+    c += d; b ^= c; b = rotl(b, 7);
+
+// RFC 8439 §2.3 block function: out[16] = keystream words
+__device__ __forceinline__ void chacha_block(const uint32_t k[8], uint32_t ctr, uint32_t n0, uint32_t n1, uint32_t n2,
+                                             uint32_t out[16]) {
+    uint32_t x[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u, k[0], k[1], k[2], k[3],
+                      k[4], k[5], k[6], k[7], ctr, n0, n1, n2};
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+        QR(x[0], x[4], x[8], x[12]);
+        QR(x[1], x[5], x[9], x[13]);
+        QR(x[2], x[6], x[10], x[14]);
+        QR(x[3], x[7], x[11], x[15]);
+        QR(x[0], x[5], x[10], x[15]);
+        QR(x[1], x[6], x[11], x[12]);
+        QR(x[2], x[7], x[8], x[13]);
+        QR(x[3], x[4], x[9], x[14]);
+    }
+    const uint32_t in[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u, k[0], k[1], k[2], k[3],
+                             k[4], k[5], k[6], k[7], ctr, n0, n1, n2};
+#pragma unroll
+    for (int i = 0; i < 16; i++) out[i] = x[i] + in[i];
+}
+
+__device__ __forceinline__ uint32_t chacha_hp_word(const uint32_t hk[8], uint4 sample, uint32_t *w1) {
+    uint32_t ks[16];
+    chacha_block(hk, sample.x, sample.y, sample.z, sample.w, ks);
+    *w1 = ks[1];
+    return ks[0];
+}
+
+// ---------------------------------------------------------------- receive-side header unprotection of one packet
+//  for unprotect_kernel and the fused receive kernel (aes_gcm.hip aes_gcm_rx_kernel):
+//   sample at header_len + 4 (payload.rs:151-169) -> mask (header_key.rs:52-56) -> remove_header_protection in place
+//   (header_crypto.rs:98-123: first byte, pn_len = (b0 & 3) + 1, PN bytes) -> expand the PN against the space's
+//   largest acknowledged PN (packet/number/mod.rs:191-238) -> the packet key by the key-phase bit 0x04
+//   (key_phase.rs:12,46; KeySet::decrypt_packet, keyset.rs:113-143; long headers: key_idx[0]) -> the qpp_pkt the
+//   open consumes.  A packet too short for the sample is DECODE_ERROR and marked QPP_PKT_SKIP; key slots outside the
+//   table are INTERNAL_ERROR (never read).  `aes` views T-tables already in LDS.
+__device__ __forceinline__ qpp_pkt rx_unprotect_one(const AesLds &aes, const DevKey *__restrict__ keys, uint32_t key_cap,
+                                                    const qpp_rx_pkt &r, uint8_t *__restrict__ arena, int8_t *status,
+                                                    uint32_t i) {
+    qpp_pkt d{};
+    d.off = r.off;
+    d.key_idx = r.key_idx[0];
+    d.aad_len = r.header_len;
+    uint8_t *base = arena + r.off;
+    const uint32_t hdr = r.header_len;
+    if ((uint32_t)r.len < hdr + 4 + 16) {
+        d.flags = QPP_PKT_SKIP;
+        status[i] = QPP_DECODE_ERROR;
+        return d;
+    }
+    if (r.key_idx[0] >= key_cap || r.key_idx[1] >= key_cap) {  // slots outside the key table: refused, never read
+        d.flags = QPP_PKT_SKIP;
+        d.key_idx = 0;
+        status[i] = QPP_INTERNAL_ERROR;
+        return d;
+    }
+    const DevKey *__restrict__ hk = keys + r.key_idx[0];
+    // All three packet loads are issued before the mask is computed (no dependent byte loads after it): byte 0,
+    // the 4 bytes that may hold the PN (len >= hdr + 20 was checked above) and the sample.
+    const uint4 smp = ld16(base + hdr + 4);
+    uint32_t pnw;
+    __builtin_memcpy(&pnw, base + hdr, 4);
+    uint8_t b0 = base[0];
+    uint32_t m0, m1;
+    if (hk->suite == QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256) {
+        uint32_t k[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) k[j] = hk->hp_rk[j];
+        m0 = chacha_hp_word(k, smp, &m1);
+    } else {
+        const uint4 m = hk->hp_nr == 10 ? aes.encrypt<10>(smp, hk->hp_rk) : aes.encrypt<14>(smp, hk->hp_rk);
+        m0 = m.x;
+        m1 = m.y;
+    }
+    const bool is_long = (b0 & 0x80) != 0;
+    b0 ^= (uint8_t)m0 & (is_long ? 0x0f : 0x1f);
+    base[0] = b0;
+    const uint32_t pn_len = (b0 & 3u) + 1u;
+    const uint32_t mm = (m0 >> 8) | (m1 << 24);  // mask bytes 1..4, byte j of the PN at bits 8j
+    if (hdr == 0) pnw = (pnw & 0xffffff00u) | b0;  // PN byte 0 is byte 0, already unmasked above
+    // unmask PN bytes [0, pn_len); bytes past pn_len are written back unchanged (this lane owns the packet)
+    pnw ^= pn_len == 4u ? mm : (mm & ((1u << (8u * pn_len)) - 1u));
+    __builtin_memcpy(base + hdr, &pnw, 4);
+    const uint64_t trunc = bswap32(pnw) >> (8u * (4u - pn_len));  // PN bytes big-endian
+    d.pn = decode_packet_number(r.largest_pn & kPnMask, trunc, 8 * pn_len);
+    d.key_idx = (!is_long && (b0 & 0x04)) ? r.key_idx[1] : r.key_idx[0];
+    d.aad_len = (uint16_t)(hdr + pn_len);
+    d.pt_len = (uint16_t)(r.len - hdr - pn_len - 16);
+    d.pn_len = (uint8_t)pn_len;
+    return d;
+}
+
 // ---------------------------------------------------------------- per-wave payload staging
 // Coalesced payload I/O through a per-wave LDS staging area.  A lane-per-packet load touches 64 scattered lines
 // per wave instruction (packets are ~1.2 KB apart) and thrashes L1 (measured: with the payload I/O confined to an

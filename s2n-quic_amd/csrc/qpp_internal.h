@@ -165,6 +165,10 @@ hipError_t launch_aes_gcm_wave(bool seal, const DevKey *keys, const qpp_pkt *des
 hipError_t launch_chacha(bool seal, const DevKey *keys, uint32_t key_cap, const qpp_pkt *descs, uint32_t n,
                          uint8_t *arena, uint8_t *masks, int8_t *status, uint32_t flags, bool burst, hipStream_t s);
 // receive side: remove header protection, expand the PN, choose the key by key phase -> descs_out (chacha.hip)
+// fused unprotect -> PN expand -> open for a context whose only live packet key is the AES key `slot` (aes_gcm.hip)
+hipError_t launch_aes_gcm_rx(const DevKey *keys, uint32_t key_cap, const qpp_rx_pkt *rx, uint32_t n, uint32_t slot,
+                             uint32_t nr, uint32_t n_cu, uint8_t *arena, qpp_pkt *descs_out, int8_t *status,
+                             hipStream_t s);
 hipError_t launch_unprotect(const DevKey *keys, uint32_t key_cap, const qpp_rx_pkt *rx, uint32_t n, uint8_t *arena,
                             qpp_pkt *descs_out, int8_t *status, hipStream_t s);
 hipError_t launch_hp_mask(const DevKey *keys, uint32_t key_cap, const qpp_pkt *descs, uint32_t n,

@@ -1,0 +1,117 @@
+"""The fused receive kernel (aes_gcm.hip aes_gcm_rx_kernel: unprotect -> PN expand -> open in one launch, used when
+the context's only live packet key is an AES key) against the two-launch path (unprotect_kernel + the plan-free open,
+QPP_RX_FUSED=0) and against the oracle (orc_unprotect_open_batch).
+
+The batch is what a receiver sees during a key update (quic/s2n-quic-core/src/crypto/application/keyset.rs:113-143):
+short headers of both key phases and long headers, PNs truncated against the largest acknowledged PN, tampered tags,
+packets too short for the HP sample.  The phase-1 key has already been dropped, so its packets are refused
+(INTERNAL_ERROR) with their header unprotected and their payload untouched.  Bar: the two paths equal bit for bit
+(arena, descriptors out, status), and every packet the oracle opens is bit-exact with it.
+"""
+import numpy as np
+import pytest
+
+import _oracle as orc
+import qpp
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = qpp.Context(0)
+    yield c
+    c.close()
+
+
+def _batch(rng, okeys_mat, slots, n):
+    chunks, rx, orx = [], [], []
+    off = 0
+    for i in range(n):
+        largest = int(rng.integers(0, 2**62 - 2**20)) if i % 3 else int(rng.integers(0, 300))
+        pn = largest + int(rng.integers(0, 400))
+        _, _, pn_len = orc.truncate_pn(pn, largest)
+        pn_len = min(4, pn_len + int(rng.integers(0, 2)))
+        long_hdr = i % 5 == 0
+        phase = 0 if long_hdr else int(i % 4 == 1)
+        if long_hdr:
+            first = 0xc0 | (int(rng.integers(0, 4)) << 4) | (pn_len - 1)
+            rest = rng.integers(0, 256, int(rng.integers(6, 40)), dtype=np.uint8).tobytes()
+        else:
+            first = 0x40 | (phase << 2) | (pn_len - 1)
+            rest = rng.integers(0, 256, int(rng.integers(0, 21)), dtype=np.uint8).tobytes()
+        header = bytes([first]) + rest
+        pt = int(rng.integers(max(0, 4 - pn_len), 1400)) if i % 7 else max(0, 4 - pn_len)
+        payload = rng.integers(0, 256, pt, dtype=np.uint8).tobytes()
+        suite, k, iv, hp = okeys_mat[phase]
+        rc, pkt = orc.protect_packet(suite, k, iv, hp, pn, header, pn_len, payload)
+        assert rc == 0
+        pkt = bytearray(pkt)
+        if i % 11 == 3:
+            pkt[-1 - i % 16] ^= 0x20  # tampered -> DECRYPT_ERROR
+        length = len(pkt)
+        if i % 13 == 5:
+            length = len(header) + 19  # no room for the sample -> DECODE_ERROR
+            pkt = pkt[:length]
+        chunks.append(bytes(pkt) + bytes(int(rng.integers(0, 7))))
+        rx.append((largest, (slots[0], slots[1]), off, len(header), length))
+        orx.append((largest, (0, 1), off, len(header), length))
+        off += len(chunks[-1])
+    arena = np.frombuffer(b"".join(chunks) + bytes(64), dtype=np.uint8).copy()
+    return np.array(rx, dtype=qpp.RX_DTYPE), np.array(orx, dtype=qpp.RX_DTYPE), arena
+
+
+def _run(ctx, rx, arena, monkeypatch, fused):
+    monkeypatch.setenv("QPP_RX_FUSED", "1" if fused else "0")
+    n = len(rx)
+    d_rx, d_arena = ctx.alloc(rx.nbytes), ctx.alloc(arena.nbytes)
+    d_out, d_status = ctx.alloc(n * qpp.PKT_DTYPE.itemsize), ctx.alloc(n)
+    d_rx.upload(rx)
+    d_arena.upload(arena)
+    d_status.upload(np.full(n, 99, dtype=np.int8))
+    ctx.unprotect_open_batch(d_rx, n, d_arena, d_out, d_status)
+    ctx.sync()
+    out = d_arena.download(), d_out.download(dtype=qpp.PKT_DTYPE), d_status.download(dtype=np.int8)
+    for b in (d_rx, d_arena, d_out, d_status):
+        b.free()
+    return out
+
+
+@pytest.mark.parametrize("suite", [1, 2])
+def test_fused_rx_equals_two_launch_path_and_oracle(ctx, suite, monkeypatch):
+    rng = np.random.default_rng(40 + suite)
+    ctx.set_burst_max(0)  # lane-kernel batches at test size (the fused path is the lane kernel's)
+    try:
+        k0 = ctx.key(suite, rng.integers(0, 256, qpp.HASH_LEN[suite], dtype=np.uint8).tobytes())
+        k1 = k0.derive_next_key()
+        mats = [(suite, *k0.material()), (suite, *k1.material())]
+        slots = [k0.slot, k1.slot]
+        n = 3000
+        rx, orx, arena = _batch(rng, mats, slots, n)
+        k1.free()  # the old phase's key is gone: k0 is the context's only live packet key -> the fused kernel
+        a_f, o_f, s_f = _run(ctx, rx, arena, monkeypatch, fused=True)
+        a_2, o_2, s_2 = _run(ctx, rx, arena, monkeypatch, fused=False)
+        assert (s_f == s_2).all(), "status differs between the fused and the two-launch path"
+        assert (a_f == a_2).all(), "arena differs between the fused and the two-launch path"
+        assert (o_f.view(np.uint8) == o_2.view(np.uint8)).all(), "descriptors differ"
+
+        want_arena = arena.copy()
+        want_out, want_st = orc.unprotect_open_batch(orc.make_keys(mats), orx, want_arena)
+        want_st = np.array(want_st, dtype=np.int8)
+        phase1 = (want_out["key_idx"] == 1) & (want_st != qpp.DECODE_ERROR)
+        assert phase1.sum() > 100 and (s_f[phase1] == qpp.INTERNAL_ERROR).all()
+        assert (s_f[~phase1] == want_st[~phase1]).all()
+        assert (s_f == 0).sum() > n // 2 and (s_f == qpp.DECRYPT_ERROR).any() and (s_f == qpp.DECODE_ERROR).any()
+        for f in ("pn", "aad_len", "pt_len", "pn_len", "flags", "off"):
+            assert (o_f[f] == want_out[f]).all(), f
+        assert (o_f["key_idx"] == np.where(want_out["key_idx"] == 1, slots[1], slots[0])).all()
+        for i in range(n):
+            o, ln, aad = int(rx[i]["off"]), int(rx[i]["len"]), int(want_out[i]["aad_len"])
+            if phase1[i]:  # header unprotected as the oracle did, payload || tag as received
+                assert (a_f[o:o + aad] == want_arena[o:o + aad]).all()
+                assert (a_f[o + aad:o + ln] == arena[o + aad:o + ln]).all()
+            else:
+                assert (a_f[o:o + ln] == want_arena[o:o + ln]).all(), i
+        k0.free()
+    finally:
+        ctx.set_burst_max(16384)

@@ -262,8 +262,23 @@ __device__ __forceinline__ void process_packet(const AesLds &aes, const GH &gh, 
         co_len[i] = (uint32_t)__shfl((int)p.len, (int)st.coop_src(i), 64);
         co_k[i] = st.coop_chunk(i);
     }
+    // Interior groups (wave-uniform test): every chunk the wave moves in group g is a whole payload block of its packet
+    // (g >= 1 and NB g + NB - 2 < the wave's shortest payload in blocks), so loads and stores need no clamp and no
+    // branch, and address from a uniform base (SGPRs) + a per-lane 32-bit offset fixed for the whole packet.  Edge
+    // groups (the first, the last ones of the shortest packet) keep the clamped, predicated form.
+    const uint32_t min_full = __builtin_amdgcn_readfirstlane(wave_min(has ? (p.len >> 4) : 0u));  // uniform: a scalar branch
+    auto interior = [&](int g) { return g >= 1 && (uint32_t)(NB * g + NB - 1) <= min_full; };
+    uint32_t co_vo[NB];  // chunk k of the role's packet at group g: arena + (16 NB g - 16) + co_vo
+#pragma unroll
+    for (int i = 0; i < NB; i++) co_vo[i] = co_off[i] + 16u * co_k[i];
     // chunk of block b = NB g - 1 + k, clamped inside payload||tag (its value is unused when out of range)
     auto co_load = [&](int g, uint4 (&v)[NB]) {
+        if (interior(g)) {
+            const uint8_t *gb = arena + (16u * NB * (uint32_t)g - 16u);
+#pragma unroll
+            for (int i = 0; i < NB; i++) v[i] = ld16(gb + co_vo[i]);
+            return;
+        }
 #pragma unroll
         for (int i = 0; i < NB; i++) {
             const int b = NB * g - 1 + (int)co_k[i];
@@ -277,6 +292,12 @@ __device__ __forceinline__ void process_packet(const AesLds &aes, const GH &gh, 
     // have been consumed: vmcnt counts loads and stores together, so a store issued behind a prefetch would make
     // the next wait for that prefetch also wait for the store's write acknowledgement.
     auto co_store = [&](int g, const uint4 (&v)[NB]) {
+        if (interior(g)) {
+            uint8_t *gb = arena + (16u * NB * (uint32_t)g - 16u);
+#pragma unroll
+            for (int i = 0; i < NB; i++) st16_nt(gb + co_vo[i], v[i]);
+            return;
+        }
 #pragma unroll
         for (int i = 0; i < NB; i++) {
             const int b = NB * g - 1 + (int)co_k[i];
@@ -329,6 +350,7 @@ __device__ __forceinline__ void process_packet(const AesLds &aes, const GH &gh, 
             }
         }
         const int b0 = NB * g - 1;  // data block of slot 0
+        const bool inner = interior(g);  // uniform: every lane's NB blocks are whole payload blocks
         uint4 cg[NB];               // the group's ciphertext blocks, for GHASH
 #pragma unroll
         for (int j = 0; j < NB; j++) {
@@ -336,7 +358,7 @@ __device__ __forceinline__ void process_packet(const AesLds &aes, const GH &gh, 
             const uint4 out = in[j] ^ ks[j];
             lds_st128(st.own(j), out);  // full blocks leave through the cooperative store below
             cg[j] = SEAL ? out : in[j];  // (unused unless 0 <= b < nblk)
-            if (b == nfull && rem) {
+            if (!inner && b == nfull && rem) {
                 const uint4 o = keep_bytes(out, rem);
                 st_bytes(pay + 16 * b, o, rem);
                 cg[j] = SEAL ? o : keep_bytes(in[j], rem);
@@ -346,7 +368,7 @@ __device__ __forceinline__ void process_packet(const AesLds &aes, const GH &gh, 
         // uniform batch) the steps run branch-free, so the word rotation is a select and no exec-mask bookkeeping
         // surrounds each step.  (Deferring them behind the next group's keystream kept 16 more VGPRs live for no
         // overlap: the keystream pipeline is fenced by scheduling barriers.)
-        if (__all(b0 >= 0 && b0 + NB <= nblk)) {
+        if (inner || __all(b0 >= 0 && b0 + NB <= nblk)) {
 #pragma unroll
             for (int j = 0; j < NB; j++) z = gh.mulx(z, cg[j]);
         } else {

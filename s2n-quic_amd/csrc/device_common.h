@@ -506,6 +506,11 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
     for (int o = 1; o < 64; o <<= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
     return v;
 }
+__device__ __forceinline__ uint32_t wave_min(uint32_t v) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
+    return v;
+}
 __device__ __forceinline__ void wave_lds_sync() {
     // the wave's own LDS traffic is in order; this keeps the compiler from moving LDS accesses across the exchange
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

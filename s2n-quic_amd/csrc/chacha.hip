@@ -148,8 +148,20 @@ __global__ __launch_bounds__(256, 3) void chacha_kernel(const DevKey *__restrict
     auto own_slot = [&](uint32_t j) {
         return stage + 16u * (64u * (lane / 8u) + 8u * (lane % 8u) + ((j + chacha_rho(lane)) & 7u));
     };
+    // Interior pairs (wave-uniform test): all 8 blocks of pair m are whole payload blocks of every packet of the wave,
+    // so the pair moves without clamps or predicated stores (as the AES kernels' interior groups)
+    const uint32_t min_full = __builtin_amdgcn_readfirstlane(wave_min(has ? (len >> 4) : 0u));
+    auto inner_pair = [&](uint32_t m) { return 8u * m + 8u <= min_full; };
     // pair m = blocks 8 m .. 8 m + 7, clamped inside payload||tag (unused when out of range)
     auto pair_load = [&](uint32_t m, uint4 (&r)[8]) {
+        if (inner_pair(m)) {
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                const uint32_t ox = lds_ld32(tab + 8u * (8u * i + lane / 8u));
+                r[i] = ld16(arena + ox + 16u * (8u * m + lj(i)));
+            }
+            return;
+        }
 #pragma unroll
         for (int i = 0; i < 8; i++) {
             const uint2 ol = lds_ld64(tab + 8u * (8u * i + lane / 8u));
@@ -158,6 +170,15 @@ __global__ __launch_bounds__(256, 3) void chacha_kernel(const DevKey *__restrict
         }
     };
     auto pair_store = [&](uint32_t m) {  // the full blocks of pair m of the wave's 64 packets
+        if (inner_pair(m)) {
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                const uint4 v = lds_ld128(stage + 16u * (64u * i + lane));
+                const uint32_t ox = lds_ld32(tab + 8u * (8u * i + lane / 8u));
+                st16_nt(arena + ox + 16u * (8u * m + lj(i)), v);
+            }
+            return;
+        }
 #pragma unroll
         for (int i = 0; i < 8; i++) {
             const uint4 v = lds_ld128(stage + 16u * (64u * i + lane));
@@ -185,7 +206,7 @@ __global__ __launch_bounds__(256, 3) void chacha_kernel(const DevKey *__restrict
             uint4 out = in[q] ^ make_uint4(ks[4 * q], ks[4 * q + 1], ks[4 * q + 2], ks[4 * q + 3]);
             lds_st128(own_slot(4u * (c & 1u) + q), out);  // full blocks leave through the pair store
             cb[q] = SEAL ? out : in[q];
-            if (o < len && len - o < 16) {  // the partial last block: this lane stores its bytes
+            if (!inner_pair(c >> 1) && o < len && len - o < 16) {  // the partial last block: this lane stores its bytes
                 const uint32_t r = len - o;
                 out = keep_bytes(out, r);
                 st_bytes(pay + o, out, r);
@@ -200,7 +221,7 @@ __global__ __launch_bounds__(256, 3) void chacha_kernel(const DevKey *__restrict
         chacha_block(k, c + 2, n0, n1, n2, ks);  // next chunk ...
 #pragma unroll
         for (int q = 0; q < 4; q++)
-            if (64 * c + 16 * q < len) mac.block(cb[q]);  // ... beside this chunk's MAC
+            if (inner_pair(c >> 1) || 64 * c + 16 * q < len) mac.block(cb[q]);  // ... beside this chunk's MAC
     }
     if (!has) return;
     mac.block(make_uint4(aad_len, 0, len, 0));  // le64(aad_len) || le64(ct_len)

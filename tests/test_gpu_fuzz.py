@@ -1,0 +1,154 @@
+"""A seeded random sequence of engine operations, as a busy endpoint issues them: seal and open batches of every size
+class (one-wave burst, lane and wave-item kernels, ChaCha), over random mixes of the three suites, with and without
+header protection, on two streams of one context, interleaved with key updates, frees and new keys while earlier
+batches are still in flight, and with the kernel-choice knobs changed between batches.
+
+Every batch is checked against the full-size checker (oracle/fastcheck.c, itself checked against the restatement in
+tests/test_fastcheck.py) with the key material it was ENQUEUED with: the stream-ordered key retirement
+(include/qpp.h) must keep freed and rotated keys valid for the work already queued.  Opened batches carry tampered
+packets (DECRYPT_ERROR, payload zeroed).  Bit-exact on every byte, mask and status.
+"""
+import numpy as np
+import pytest
+
+import _oracle as orc
+import qpp
+
+pytestmark = pytest.mark.gpu
+
+SIZES = [1, 7, 64, 300, 2000, 5000, 20000]
+
+
+def _secret(rng, suite):
+    return rng.integers(0, 256, qpp.HASH_LEN[suite], dtype=np.uint8).tobytes()
+
+
+def _batch(rng, n, nkeys, hp):
+    descs = np.zeros(n, dtype=qpp.PKT_DTYPE)
+    pn_len = rng.integers(1, 5, n)
+    aad = pn_len + rng.integers(0, 40, n)
+    pt = rng.integers(4 if hp else 0, 1500, n)
+    big = rng.random(n) < 0.01
+    pt[big] = rng.integers(1500, 8000, int(big.sum()))
+    size = aad + pt + 16
+    descs["off"] = np.concatenate([[0], np.cumsum(size + rng.integers(0, 9, n))[:-1]])
+    descs["pn"] = rng.integers(0, 2**62, n, dtype=np.uint64)
+    descs["aad_len"], descs["pt_len"], descs["pn_len"] = aad, pt, pn_len
+    which = rng.integers(0, nkeys, n)
+    arena = rng.integers(0, 256, int(descs["off"][-1] + size[-1]) + 64, dtype=np.uint8)
+    return descs, which, arena
+
+
+class _Pending:
+    def __init__(self, kind, bufs, want, want_masks, want_status, n, tag):
+        self.kind, self.bufs, self.want, self.want_masks, self.want_status, self.n, self.tag = (
+            kind, bufs, want, want_masks, want_status, n, tag)
+
+    def check(self, ctx):
+        d_desc, d_arena, d_mask, d_status = self.bufs
+        ctx.synchronize()
+        got = d_arena.download()
+        st = d_status.download(dtype=np.int8)
+        assert (st == self.want_status).all(), f"{self.tag}: status"
+        assert (got == self.want).all(), f"{self.tag}: arena bytes differ"
+        if self.want_masks is not None:
+            m = d_mask.download()[:5 * self.n]
+            assert (m == self.want_masks).all(), f"{self.tag}: HP masks"
+        for b in self.bufs:
+            if b is not None:
+                b.free()
+
+
+@pytest.mark.parametrize("seed", [0xF022, 0xF023, 0xF024, 0xF025])
+def test_random_operation_sequence(seed):
+    rng = np.random.default_rng(seed)
+    ctx = qpp.Context(0)
+    side = ctx.new_stream()
+    keys = []  # [Key, (suite, key, iv, hp)] -- the material a batch is checked with is taken when it is enqueued
+
+    def new_key():
+        s = int(rng.choice([1, 2, 3]))
+        k = ctx.key(s, _secret(rng, s))
+        keys.append([k, (s, *k.material())])
+
+    for _ in range(6):
+        new_key()
+    pending, counts = [], {"seal": 0, "open": 0, "update": 0, "free": 0}
+    try:
+        for step in range(160):
+            op = rng.choice(["seal", "open", "update", "free", "new", "knob", "check"],
+                            p=[0.36, 0.24, 0.12, 0.08, 0.08, 0.07, 0.05])
+            if op in ("seal", "open"):
+                if not keys:
+                    new_key()
+                pick = rng.choice(len(keys), int(rng.integers(1, len(keys) + 1)), replace=False)
+                chosen = [keys[i] for i in pick]
+                n = int(rng.choice(SIZES))
+                hp = op == "seal" and rng.random() < 0.7
+                flags = (qpp.HP_MASK_OUT | (qpp.HP_APPLY if rng.random() < 0.5 else 0)) if hp else 0
+                descs, which, arena = _batch(rng, n, len(chosen), hp)
+                descs["key_idx"] = np.array([c[0].slot for c in chosen], dtype=np.uint32)[which]
+                okeys = orc.make_keys([c[1] for c in chosen])
+                odescs = descs.copy()
+                odescs["key_idx"] = which
+                stream = side if rng.random() < 0.5 else None
+                d_desc, d_arena, d_status = ctx.alloc(descs.nbytes), ctx.alloc(arena.nbytes), ctx.alloc(n)
+                d_mask = ctx.alloc(5 * n) if op == "seal" else None
+                d_desc.upload(descs)
+                if op == "seal":
+                    want = arena.copy()
+                    want_masks = orc.fast_seal_batch(okeys, odescs, want, flags)
+                    d_arena.upload(arena)
+                    ctx.seal_batch(d_desc, n, d_arena, d_mask, d_status, flags, stream=stream)
+                    pending.append(_Pending("seal", (d_desc, d_arena, d_mask, d_status), want,
+                                            want_masks if flags & qpp.HP_MASK_OUT else None,
+                                            np.zeros(n, np.int8), n, f"step {step} seal n={n} flags={flags}"))
+                else:
+                    sealed = arena.copy()
+                    orc.fast_seal_batch(okeys, odescs, sealed, 0)
+                    bad = rng.random(n) < 0.05
+                    want = arena.copy()  # opened: plaintext back, tag left in place
+                    for i in range(n):
+                        o, a, p = int(descs["off"][i]), int(descs["aad_len"][i]), int(descs["pt_len"][i])
+                        want[o + a + p:o + a + p + 16] = sealed[o + a + p:o + a + p + 16]
+                        if bad[i]:
+                            j = o + a + int(rng.integers(0, p + 16))
+                            sealed[j] ^= 0x10
+                            want[o + a:o + a + p] = 0  # no unauthenticated plaintext is released
+                            if j >= o + a + p:
+                                want[j] = sealed[j]  # the flipped tag byte stays as received
+                    d_arena.upload(sealed)
+                    ctx.open_batch(d_desc, n, d_arena, d_status, stream=stream)
+                    pending.append(_Pending("open", (d_desc, d_arena, None, d_status), want, None,
+                                            np.where(bad, qpp.DECRYPT_ERROR, qpp.OK).astype(np.int8), n,
+                                            f"step {step} open n={n}"))
+                counts[op] += 1
+            elif op == "update" and keys:
+                pick = sorted(rng.choice(len(keys), int(rng.integers(1, len(keys) + 1)), replace=False))
+                nxt = ctx.update_keys([keys[i][0] for i in pick])
+                for i, k in zip(pick, nxt):
+                    keys[i][0].free()  # the old key goes at once: batches queued with it still use it
+                    keys[i] = [k, (k.suite, *k.material())]
+                counts["update"] += 1
+            elif op == "free" and len(keys) > 1:
+                k, _ = keys.pop(int(rng.integers(0, len(keys))))
+                k.free()
+                counts["free"] += 1
+            elif op == "new" and len(keys) < 12:
+                new_key()
+            elif op == "knob":
+                ctx.set_burst_max(int(rng.choice([0, 64, 16384])))
+                ctx.set_aes_kernel(int(rng.choice([qpp.AES_KERNEL_AUTO, qpp.AES_KERNEL_LANE, qpp.AES_KERNEL_WAVE])))
+            elif op == "check":
+                for p in pending:
+                    p.check(ctx)
+                pending = []
+        for p in pending:
+            p.check(ctx)
+        assert counts["seal"] > 30 and counts["open"] > 20 and counts["update"] > 5 and counts["free"] > 3, counts
+    finally:
+        for k, _ in keys:
+            k.free()
+        ctx.set_burst_max(16384)
+        ctx.set_aes_kernel(qpp.AES_KERNEL_AUTO)
+        ctx.close()

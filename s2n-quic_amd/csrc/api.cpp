@@ -98,6 +98,7 @@ struct qpp_ctx {
     std::vector<uint32_t> retire_pending; // freed, host copy zeroized, device zeroing not yet enqueued
     uint32_t retired_slots = 0;           // slots in `retired`
     uint32_t live_by_suite[4] = {0, 0, 0, 0};  // live packet keys per suite: which kernels a batch can need
+    uint32_t hdr_live_by_suite[4] = {0, 0, 0, 0};  // live header-key-only records per suite (the fused ChaCha receive)
     uint32_t live_slot_xor = 0;                  // XOR of the live packet keys' slots: THE slot when only one is live
     bool fips = false;                           // qpp_ctx_set_fips: AES packet keys created now seal in FIPS mode
     uint32_t fips_live = 0;                      // live FIPS keys: seal batches run the nonce-order gate
@@ -483,6 +484,7 @@ int install_header(qpp_header_key *h) {
     d.live = 2;  // header key only: no packet key, never planned or sealed with
     if (h->suite == QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256) memcpy(d.hp_rk, h->hp, 32);
     else d.hp_nr = (uint32_t)aes_expand_key(h->hp, suite_key_len(h->suite), d.hp_rk);
+    ctx->hdr_live_by_suite[h->suite & 3]++;
     mark_dirty(ctx, h->slot);
     return QPP_OK;
 }
@@ -1084,7 +1086,10 @@ int qpp_header_key_new(qpp_ctx *ctx, int suite, const uint8_t *secret, size_t se
 void qpp_header_key_free(qpp_header_key *hk) {
     if (!hk) return;
     qpp_ctx *ctx = hk->ctx;
-    if (ctx && hk->slot < ctx->key_cap && ctx->h_keys[hk->slot].live == 2) retire_slot(ctx, hk->slot);
+    if (ctx && hk->slot < ctx->key_cap && ctx->h_keys[hk->slot].live == 2) {
+        ctx->hdr_live_by_suite[ctx->h_keys[hk->slot].suite & 3]--;
+        retire_slot(ctx, hk->slot);
+    }
     secure_zero(hk, sizeof *hk);
     delete hk;
 }
@@ -1285,6 +1290,16 @@ int qpp_unprotect_open_batch(qpp_ctx *ctx, const qpp_rx_pkt *rx, size_t n, uint8
     if (one != UINT32_MAX) {
         HIP_TRY(ctx, launch_aes_gcm_rx(ctx->d_keys, ctx->key_cap, rx, (uint32_t)n, one, ctx->h_keys[one].nr, ctx->n_cu,
                                        arena, descs_out, status, st->stream));
+        return note_work(ctx, st);
+    }
+    // No AES record live at all (packet or header keys): every header and packet key a packet can name is ChaCha20,
+    // so the ChaCha lane kernel unprotects and opens in ONE launch, whatever the key mix (per-lane keys, no plan).
+    const bool no_aes = !ctx->live_by_suite[QPP_SUITE_TLS_AES_128_GCM_SHA256] &&
+                        !ctx->live_by_suite[QPP_SUITE_TLS_AES_256_GCM_SHA384] &&
+                        !ctx->hdr_live_by_suite[QPP_SUITE_TLS_AES_128_GCM_SHA256] &&
+                        !ctx->hdr_live_by_suite[QPP_SUITE_TLS_AES_256_GCM_SHA384];
+    if (no_aes && !(flags & QPP_ONLY_AES) && !(fz && fz[0] == '0') && n > (ctx->burst_max >> kChachaBurstShift)) {
+        HIP_TRY(ctx, launch_chacha_rx(ctx->d_keys, ctx->key_cap, rx, (uint32_t)n, arena, descs_out, status, st->stream));
         return note_work(ctx, st);
     }
     // 1. header unprotection + PN expansion + key-phase choice -> descs_out (device); 2. the open kernels on them,

@@ -100,13 +100,29 @@ constexpr uint32_t kChachaStage = 64u * 16u * 8u;
 constexpr uint32_t kChachaWaveLds = kChachaStage + 64u * 8u;
 __device__ __forceinline__ uint32_t chacha_rho(uint32_t p) { return (p + (p >> 4)) & 7u; }
 
-template <bool SEAL>
+// RX (open only): the fused receive path for a context with no live AES record -- each lane first unprotects its
+// packet of rx[] (rx_unprotect_one: HP removal, PN expansion, key phase; ChaCha20 header keys only), writes the
+// qpp_pkt to descs_out and opens it with the key the phase picked.  Same outputs as unprotect_kernel + this kernel.
+template <bool SEAL, bool RX = false>
 __global__ __launch_bounds__(256, 3) void chacha_kernel(const DevKey *__restrict__ keys, uint32_t key_cap,
                                                     const qpp_pkt *__restrict__ descs, uint32_t n,
                                                     uint8_t *__restrict__ arena, uint8_t *masks, int8_t *status,
-                                                    uint32_t flags) {
+                                                    uint32_t flags, const qpp_rx_pkt *__restrict__ rx = nullptr,
+                                                    qpp_pkt *__restrict__ descs_out = nullptr) {
     const uint32_t pi = blockIdx.x * blockDim.x + threadIdx.x;
-    const qpp_pkt d = descs[pi < n ? pi : n - 1];  // (any valid descriptor for helper lanes)
+    qpp_pkt d;
+    if constexpr (RX) {
+        static_assert(!SEAL, "the receive path opens");
+        if (pi < n) {
+            d = rx_unprotect_one<false>(AesLds{0}, keys, key_cap, rx[pi], arena, status, pi);
+            descs_out[pi] = d;
+        } else {
+            d = qpp_pkt{};
+            d.flags = QPP_PKT_SKIP;  // helper lane
+        }
+    } else {
+        d = descs[pi < n ? pi : n - 1];  // (any valid descriptor for helper lanes)
+    }
     const bool bad_slot = d.key_idx >= key_cap;    // never dereferenced: the packet is refused
     const DevKey *__restrict__ key = keys + (bad_slot ? 0u : d.key_idx);
     // a slot outside the table, a freed slot or a header-key-only slot holds no packet key: refused (no AES kernel
@@ -544,9 +560,21 @@ hipError_t launch_chacha(bool seal, const DevKey *keys, uint32_t key_cap, const 
     const dim3 grid((n + 255) / 256), block(256);
     const uint32_t lds = 4u * kChachaWaveLds;  // 4 waves, 34 KiB
     if (seal)
-        hipLaunchKernelGGL(chacha_kernel<true>, grid, block, lds, s, keys, key_cap, descs, n, arena, masks, status, flags);
+        hipLaunchKernelGGL(chacha_kernel<true>, grid, block, lds, s, keys, key_cap, descs, n, arena, masks, status, flags,
+                           nullptr, nullptr);
     else
-        hipLaunchKernelGGL(chacha_kernel<false>, grid, block, lds, s, keys, key_cap, descs, n, arena, masks, status, flags);
+        hipLaunchKernelGGL(chacha_kernel<false>, grid, block, lds, s, keys, key_cap, descs, n, arena, masks, status, flags,
+                           nullptr, nullptr);
+    return hipGetLastError();
+}
+
+hipError_t launch_chacha_rx(const DevKey *keys, uint32_t key_cap, const qpp_rx_pkt *rx, uint32_t n, uint8_t *arena,
+                            qpp_pkt *descs_out, int8_t *status, hipStream_t s) {
+    if (!n) return hipSuccess;
+    const dim3 grid((n + 255) / 256), block(256);
+    const uint32_t lds = 4u * kChachaWaveLds;
+    hipLaunchKernelGGL((chacha_kernel<false, true>), grid, block, lds, s, keys, key_cap, nullptr, n, arena, nullptr,
+                       status, 0u, rx, descs_out);
     return hipGetLastError();
 }
 

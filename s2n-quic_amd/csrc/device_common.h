@@ -414,6 +414,10 @@ __device__ __forceinline__ uint32_t chacha_hp_word(const uint32_t hk[8], uint4 s
 //   (key_phase.rs:12,46; KeySet::decrypt_packet, keyset.rs:113-143; long headers: key_idx[0]) -> the qpp_pkt the
 //   open consumes.  A packet too short for the sample is DECODE_ERROR and marked QPP_PKT_SKIP; key slots outside the
 //   table are INTERNAL_ERROR (never read).  `aes` views T-tables already in LDS.
+// AES_HP = false (the fused ChaCha receive, no T-tables in LDS): a header key that is not a ChaCha20 key is refused
+// (INTERNAL_ERROR) -- the host launches that kernel only when no AES record is live.  A header-key slot that holds no
+// key at all (freed) is refused by both forms, before any header byte is touched.
+template <bool AES_HP = true>
 __device__ __forceinline__ qpp_pkt rx_unprotect_one(const AesLds &aes, const DevKey *__restrict__ keys, uint32_t key_cap,
                                                     const qpp_rx_pkt &r, uint8_t *__restrict__ arena, int8_t *status,
                                                     uint32_t i) {
@@ -435,6 +439,11 @@ __device__ __forceinline__ qpp_pkt rx_unprotect_one(const AesLds &aes, const Dev
         return d;
     }
     const DevKey *__restrict__ hk = keys + r.key_idx[0];
+    if (hk->live == 0 || (!AES_HP && hk->suite != QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256)) {
+        d.flags = QPP_PKT_SKIP;
+        status[i] = QPP_INTERNAL_ERROR;
+        return d;
+    }
     // All three packet loads are issued before the mask is computed (no dependent byte loads after it): byte 0,
     // the 4 bytes that may hold the PN (len >= hdr + 20 was checked above) and the sample.
     const uint4 smp = ld16(base + hdr + 4);
@@ -447,10 +456,12 @@ __device__ __forceinline__ qpp_pkt rx_unprotect_one(const AesLds &aes, const Dev
 #pragma unroll
         for (int j = 0; j < 8; j++) k[j] = hk->hp_rk[j];
         m0 = chacha_hp_word(k, smp, &m1);
-    } else {
+    } else if constexpr (AES_HP) {
         const uint4 m = hk->hp_nr == 10 ? aes.encrypt<10>(smp, hk->hp_rk) : aes.encrypt<14>(smp, hk->hp_rk);
         m0 = m.x;
         m1 = m.y;
+    } else {
+        m0 = m1 = 0;  // unreachable: refused above
     }
     const bool is_long = (b0 & 0x80) != 0;
     b0 ^= (uint8_t)m0 & (is_long ? 0x0f : 0x1f);

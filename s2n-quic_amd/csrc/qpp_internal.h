@@ -169,6 +169,9 @@ hipError_t launch_chacha(bool seal, const DevKey *keys, uint32_t key_cap, const 
 hipError_t launch_aes_gcm_rx(const DevKey *keys, uint32_t key_cap, const qpp_rx_pkt *rx, uint32_t n, uint32_t slot,
                              uint32_t nr, uint32_t n_cu, uint8_t *arena, qpp_pkt *descs_out, int8_t *status,
                              hipStream_t s);
+// fused unprotect -> PN expand -> open for a context with no live AES record (chacha.hip)
+hipError_t launch_chacha_rx(const DevKey *keys, uint32_t key_cap, const qpp_rx_pkt *rx, uint32_t n, uint8_t *arena,
+                            qpp_pkt *descs_out, int8_t *status, hipStream_t s);
 hipError_t launch_unprotect(const DevKey *keys, uint32_t key_cap, const qpp_rx_pkt *rx, uint32_t n, uint8_t *arena,
                             qpp_pkt *descs_out, int8_t *status, hipStream_t s);
 hipError_t launch_hp_mask(const DevKey *keys, uint32_t key_cap, const qpp_pkt *descs, uint32_t n,

@@ -115,3 +115,72 @@ def test_fused_rx_equals_two_launch_path_and_oracle(ctx, suite, monkeypatch):
         k0.free()
     finally:
         ctx.set_burst_max(16384)
+
+
+def test_fused_chacha_rx_many_keys(monkeypatch):
+    """No AES record live: the ChaCha lane kernel unprotects and opens in one launch whatever the key mix (per-lane
+    keys).  Three connections, each with both key phases; connection 1 has dropped its phase-1 key (its phase-1
+    packets are refused), and some packets name a freed header-key slot (refused before any byte is touched).  The
+    fused launch equals the two-launch path bit for bit and the oracle on every packet it opens."""
+    rng = np.random.default_rng(77)
+    ctx = qpp.Context(0)  # a context of its own: no AES key may be live
+    ctx.set_burst_max(0)
+    try:
+        conns = []
+        for _ in range(3):
+            k0 = ctx.key(3, rng.integers(0, 256, 32, dtype=np.uint8).tobytes())
+            conns.append((k0, k0.derive_next_key()))
+        gone = ctx.key(3, rng.integers(0, 256, 32, dtype=np.uint8).tobytes())
+        gone_slot = gone.slot
+        mats = [(3, *k.material()) for pair in conns for k in pair]
+        n = 4000
+        chunks, rx, orx = [], [], []
+        off = 0
+        for i in range(n):
+            c = int(rng.integers(0, 3))
+            largest = int(rng.integers(0, 2**40))
+            pn = largest + int(rng.integers(0, 300))
+            _, _, pn_len = orc.truncate_pn(pn, largest)
+            phase = int(rng.integers(0, 2))
+            header = bytes([0x40 | (phase << 2) | (pn_len - 1)]) + rng.integers(0, 256, 16, dtype=np.uint8).tobytes()
+            payload = rng.integers(0, 256, int(rng.integers(1, 1400)), dtype=np.uint8).tobytes()
+            _, k, iv, hp = mats[2 * c + phase]
+            rc, pkt = orc.protect_packet(3, k, iv, hp, pn, header, pn_len, payload)
+            pkt = bytearray(pkt)
+            if i % 17 == 4:
+                pkt[-3] ^= 1  # tampered tag
+            chunks.append(bytes(pkt) + bytes(int(rng.integers(0, 5))))
+            slots = (conns[c][0].slot, conns[c][1].slot)
+            if i % 29 == 7:
+                slots = (gone_slot, slots[1])  # a header-key slot that was freed
+            rx.append((largest, slots, off, len(header), len(pkt)))
+            orx.append((largest, (2 * c, 2 * c + 1), off, len(header), len(pkt)))
+            off += len(chunks[-1])
+        arena = np.frombuffer(b"".join(chunks) + bytes(64), dtype=np.uint8).copy()
+        rx, orx = np.array(rx, dtype=qpp.RX_DTYPE), np.array(orx, dtype=qpp.RX_DTYPE)
+        gone.free()
+        conns[1][1].free()  # connection 1 dropped its phase-1 key
+        a_f, o_f, s_f = _run(ctx, rx, arena, monkeypatch, fused=True)
+        a_2, o_2, s_2 = _run(ctx, rx, arena, monkeypatch, fused=False)
+        assert (s_f == s_2).all() and (a_f == a_2).all() and (o_f.view(np.uint8) == o_2.view(np.uint8)).all()
+        want_arena = arena.copy()
+        want_out, want_st = orc.unprotect_open_batch(orc.make_keys(mats), orx, want_arena)
+        want_st = np.array(want_st, dtype=np.int8)
+        freed_hdr = np.arange(n) % 29 == 7
+        dropped = ~freed_hdr & (want_out["key_idx"] == 3)  # connection 1, phase 1
+        assert freed_hdr.sum() > 100 and dropped.sum() > 300
+        assert (s_f[freed_hdr | dropped] == qpp.INTERNAL_ERROR).all()
+        ok = ~(freed_hdr | dropped)
+        assert (s_f[ok] == want_st[ok]).all() and (s_f == qpp.DECRYPT_ERROR).any() and (s_f == 0).sum() > n // 2
+        for i in np.flatnonzero(ok | freed_hdr):
+            o, ln = int(rx[i]["off"]), int(rx[i]["len"])
+            src = arena if freed_hdr[i] else want_arena  # a freed header key: nothing touched
+            assert (a_f[o:o + ln] == src[o:o + ln]).all(), i
+        for f in ("pn", "aad_len", "pt_len", "pn_len", "off"):
+            assert (o_f[f][ok] == want_out[f][ok]).all(), f
+        for k0, k1 in conns:
+            k0.free()
+            if k1.handle:
+                k1.free()
+    finally:
+        ctx.close()

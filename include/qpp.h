@@ -337,7 +337,10 @@ typedef struct qpp_rx_pkt {
  * unmasked first byte) -> expand the packet number against largest_pn (packet/number/mod.rs:191-238) -> choose the
  * key by the key phase -> open in place.  descs_out[i] receives the resulting qpp_pkt (pn = expanded packet number,
  * key_idx = chosen slot, aad_len = header_len + pn_len, pt_len, pn_len; flags = QPP_PKT_SKIP when rejected);
- * status[i] = QPP_OK, QPP_DECODE_ERROR (no room for the sample, short.rs / payload.rs) or QPP_DECRYPT_ERROR.
+ * status[i] = QPP_OK, QPP_DECODE_ERROR (no room for the sample, short.rs / payload.rs), QPP_DECRYPT_ERROR, or
+ * QPP_INTERNAL_ERROR (a slot outside the table, a key_idx[0] slot holding no key -- nothing touched -- or a chosen
+ * packet key that is not live).  One launch (HP removal inside the open kernel) when the context's only live packet
+ * key is AES or no AES record is live; identical outputs either way (env QPP_RX_FUSED=0 forces two launches).
  * rx, descs_out, arena and status are device pointers.  Asynchronous. */
 int qpp_unprotect_open_batch(qpp_ctx *ctx, const qpp_rx_pkt *rx, size_t n, uint8_t *arena, qpp_pkt *descs_out,
                              int8_t *status, uint32_t flags, void *stream);

@@ -72,8 +72,8 @@ struct GhashT {
     // (Z * H) ^ c in natural word order, from W = rot(Z).
     // PIPE: 9 reads in flight, the xor tree consuming them 3 at a time and each consumed triple's registers taking the
     // next reads (left alone, the scheduler issued 3, waited for them, and so on: six LDS round trips per product).
-    // AES-128 seal 1.389 -> 1.362 ms; all 16 reads in flight spilled VGPRs (1.459 ms); the AES-256 kernels (60 round
-    // key SGPRs) spill with it too and keep the plain form.
+    // AES-128 seal 1.389 -> 1.362 ms; all 16 reads in flight spilled VGPRs (1.459 ms).  The AES-256 kernels use it
+    // too since the interior-group I/O freed registers (no VGPR spills; AES-256 1 key seal 1.737 -> 1.721 ms).
     __device__ __forceinline__ uint4 prod(const uint4 &w, uint4 c) const {
         if constexpr (!PIPE) {
             const uint4 a = xor3(look<0, 0>(w), look<0, 1>(w), look<0, 2>(w));
@@ -461,7 +461,7 @@ __global__ __launch_bounds__(WG) void aes_gcm_kernel(const DevKey *__restrict__ 
         if (work[m].begin <= lo) i = m; else j = m;
     }
     const AesLds aes = make_aes(kLdsAes);
-    const GhashT<NR == 10> gh = GhashT<NR == 10>::make();
+    const GhashT<true> gh = GhashT<true>::make();
     Stage<NB> st;
     st.lane = threadIdx.x & 63u;
     st.base = kLdsStage + (threadIdx.x >> 6) * (64u * 16u * NB);
@@ -508,7 +508,7 @@ __global__ __launch_bounds__(WG) void aes_gcm_rx_kernel(const DevKey *__restrict
     const uint32_t lo = min(n, blockIdx.x * P), hi = min(n, (blockIdx.x + 1) * P);
     if (lo >= hi) return;  // uniform
     const AesLds aes = make_aes(kLdsAes);
-    const GhashT<NR == 10> gh = GhashT<NR == 10>::make();
+    const GhashT<true> gh = GhashT<true>::make();
     Stage<NB> st;
     st.lane = threadIdx.x & 63u;
     st.base = kLdsStage + (threadIdx.x >> 6) * (64u * 16u * NB);

@@ -686,6 +686,12 @@ int derive_batch(qpp_ctx *ctx, int suite, const uint8_t *secrets, const uint8_t 
     const size_t hl = suite_hash_len(suite), kl = suite_key_len(suite), mb = key_material_bytes();
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     RC_TRY(flush_keys(ctx));  // pending host records first
+    // The pinned key stage is reused below: the records that flush just queued are copied from it asynchronously, so
+    // wait for that copy before overwriting the stage (found by tests/test_gpu_fuzz.py: a key created just before a
+    // batched update was installed from the secrets written over its record -- a non-live slot, INTERNAL_ERROR).
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->kstream));
+    if (ctx->kstage_pending) secure_zero(ctx->h_kstage, ctx->kstage_pending);
+    ctx->kstage_pending = 0;
     std::vector<uint32_t> slots(n);
     for (size_t i = 0; i < n; i++) RC_TRY(alloc_slot(ctx, &slots[i]));
     // key stage: secrets | hp_in | slots | material

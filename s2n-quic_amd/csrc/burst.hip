@@ -74,10 +74,10 @@ __device__ __forceinline__ void burst_powers() {
     }
 }
 
-// AES tables + T_0 .. T_6 for one key.  T_1 .. T_6 come from the key's precomputed slot when it has one
-// (pow.cap > slot: filled by pow_setup_kernel at install), else they are built here.  Ends with a barrier.
+// T_0 .. T_6 for one key (the AES tables are built by the caller, before the work item is even read).  T_1 .. T_6
+// come from the key's precomputed slot when it has one (pow.cap > slot: filled by pow_setup_kernel at install), else
+// they are built here.  Ends with a barrier.
 __device__ void burst_tables(const DevKey *__restrict__ key, uint32_t slot, const PowTables pow) {
-    build_aes_tables(kBurstAes);
     burst_t0(key);
     if (slot < pow.cap) {
         const uint4 *src = (const uint4 *)(pow.base + (size_t)slot * kPowBytes);
@@ -122,20 +122,31 @@ __device__ __forceinline__ void burst_packet(const AesLds &aes, const DevKey *__
     const uint32_t lane = threadIdx.x & 63u;
     const PacketView p = load_packet(d, key, arena);
     uint8_t *pay = p.base + p.aad_len;
+    // header-protection round keys and header bytes: issued now, used after the GHASH tree (one memory round trip
+    // off the end of the chain)
+    constexpr int HNR = NR == 10 ? 10 : 14;
+    HpPrefetch<HNR> hpk;
+    if (SEAL && (flags & (QPP_HP_MASK_OUT | QPP_HP_APPLY)) && lane == 0 && p.pn_len >= 1 && p.pn_len <= 4)
+        hpk.load(key->hp_rk, p.base, p.aad_len - p.pn_len, flags);
     const uint32_t a = (p.aad_len + 15u) >> 4, c = (p.len + 15u) >> 4, m = a + c + 1;
     const uint32_t K = (m + 63u) >> 6, pad = 64u * K - m;
     uint4 acc = make_uint4(0, 0, 0, 0), ct0 = acc, ct1 = acc;  // ct0/ct1: ciphertext blocks 0/1 where owned
     uint4 ek = acc;  // E_K(J0), computed in pass 0 by the idle lane pad - 1 inside the data lanes' AES stream
+    // payload block of pass k for this lane (zero when the lane holds no data block in that pass); the next pass's
+    // block is loaded while this pass computes (for a zero-copy flush each load is a PCIe round trip)
+    auto load_pass = [&](uint32_t k) {
+        const int i = (int)(lane + 64u * k) - (int)pad;
+        return (i >= (int)a && i < (int)(a + c)) ? ld16(pay + 16u * ((uint32_t)i - a)) : make_uint4(0, 0, 0, 0);
+    };
+    uint4 nxt = load_pass(0);
     for (uint32_t k = 0; k < K; k++) {
         const int i = (int)(lane + 64u * k) - (int)pad;  // block index in the GHASH sequence
         const bool data = i >= (int)a && i < (int)(a + c);
         const bool j0 = k == 0 && i == -1;
         const uint32_t b = (uint32_t)i - a;  // data block b uses counter b + 2
-        uint4 in = make_uint4(0, 0, 0, 0), ks = in;
-        if (data || j0) {
-            if (data) in = ld16(pay + 16u * b);
-            ks = aes.encrypt<NR>(make_uint4(p.n0, p.n1, p.n2, bswap32(data ? b + 2u : 1u)), rk);
-        }
+        uint4 in = nxt, ks = make_uint4(0, 0, 0, 0);
+        if (k + 1 < K) nxt = load_pass(k + 1);
+        if (data || j0) ks = aes.encrypt<NR>(make_uint4(p.n0, p.n1, p.n2, bswap32(data ? b + 2u : 1u)), rk);
         uint4 x = make_uint4(0, 0, 0, 0);
         if (j0) ek = ks;
         if (i >= 0 && i < (int)a) {
@@ -193,9 +204,7 @@ __device__ __forceinline__ void burst_packet(const AesLds &aes, const DevKey *__
                     }
                     smp = make_uint4(w[0], w[1], w[2], w[3]);
                 }
-                if (lane == 0)
-                    hp_finish<NR == 10 ? 10 : 14>(aes, key->hp_rk, smp, p.base, p.aad_len - p.pn_len, p.pn_len,
-                                                  masks + 5 * (size_t)pi, flags);
+                if (lane == 0) hpk.finish(aes, smp, p.base, p.aad_len - p.pn_len, p.pn_len, masks + 5 * (size_t)pi, flags);
             }
         }
         if (status && lane == 0) status[pi] = st;
@@ -226,19 +235,30 @@ __global__ __launch_bounds__(kBurstWG) void aes_gcm_burst_kernel(const DevKey *_
                                                                   const uint32_t *__restrict__ n_work,
                                                                   uint8_t *__restrict__ arena, uint8_t *masks,
                                                                   int8_t *status, uint32_t flags, const PowTables pow) {
-    if (blockIdx.x >= *n_work) return;  // uniform: grid is sized for the worst case
+    // A burst's latency is a chain of memory round trips (pinned host memory for a zero-copy txq flush), so the
+    // independent ones overlap: the AES tables (S-box) are built while the work count is read, and each wave's first
+    // descriptor is fetched while the key's GHASH tables load.
+    const uint32_t nw = *n_work;
+    build_aes_tables(kBurstAes);
+    if (blockIdx.x >= nw) return;  // uniform: grid is sized for the worst case
     const WorkItem w = work[blockIdx.x];
     if (w.nr != NR) return;
     const DevKey *__restrict__ key = keys + w.key;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint32_t pi0 = 0;
+    qpp_pkt d0{};
+    if (wave < w.count) {
+        pi0 = perm[w.begin + wave];
+        d0 = descs[pi0];
+    }
     burst_tables(key, w.key, pow);
     const AesLds aes = make_aes(kBurstAes);
     uint32_t rk[4 * (NR + 1)];
 #pragma unroll
     for (int i = 0; i < 4 * (NR + 1); i++) rk[i] = __builtin_amdgcn_readfirstlane(key->rk[i]);
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     for (uint32_t q = wave; q < w.count; q += kBurstWG / 64) {
-        const uint32_t pi = perm[w.begin + q];
-        const qpp_pkt d = descs[pi];
+        const uint32_t pi = q == wave ? pi0 : perm[w.begin + q];
+        const qpp_pkt d = q == wave ? d0 : descs[pi];
         if (d.flags & QPP_PKT_SKIP) continue;
         burst_packet<NR, SEAL>(aes, key, rk, d, pi, arena, masks, status, flags);
     }

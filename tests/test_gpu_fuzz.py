@@ -49,7 +49,14 @@ class _Pending:
         ctx.synchronize()
         got = d_arena.download()
         st = d_status.download(dtype=np.int8)
-        assert (st == self.want_status).all(), f"{self.tag}: status"
+        bad = np.flatnonzero(st != self.want_status)
+        if len(bad):
+            desc = d_desc.download(dtype=qpp.PKT_DTYPE)
+            print("HISTORY", *HISTORY[-40:], sep="\n", flush=True)
+            print("bad key slots", sorted(set(int(x) for x in desc["key_idx"][bad])), "batch slots",
+                  sorted(set(int(x) for x in desc["key_idx"])), flush=True)
+        assert not len(bad), f"{self.tag}: status of {len(bad)} packets, first {bad[:8].tolist()}: " \
+                             f"got {st[bad[:8]].tolist()} want {self.want_status[bad[:8]].tolist()}"
         assert (got == self.want).all(), f"{self.tag}: arena bytes differ"
         if self.want_masks is not None:
             m = d_mask.download()[:5 * self.n]
@@ -59,9 +66,15 @@ class _Pending:
                 b.free()
 
 
-@pytest.mark.parametrize("seed", [0xF022, 0xF023, 0xF024, 0xF025])
+HISTORY = []
+TRACE = bool(__import__("os").environ.get("QPP_FUZZ_TRACE"))
+SEEDS = [0xF022, 0xF023, 0xF024, 0xF025] + [0xF100 + i for i in range(int(__import__("os").environ.get("QPP_FUZZ_EXTRA", "0")))]
+
+
+@pytest.mark.parametrize("seed", SEEDS)
 def test_random_operation_sequence(seed):
     rng = np.random.default_rng(seed)
+    HISTORY.clear()
     ctx = qpp.Context(0)
     side = ctx.new_stream()
     keys = []  # [Key, (suite, key, iv, hp)] -- the material a batch is checked with is taken when it is enqueued
@@ -74,10 +87,14 @@ def test_random_operation_sequence(seed):
     for _ in range(6):
         new_key()
     pending, counts = [], {"seal": 0, "open": 0, "update": 0, "free": 0}
+    knobs = [16384, qpp.AES_KERNEL_AUTO]
     try:
         for step in range(160):
             op = rng.choice(["seal", "open", "update", "free", "new", "knob", "check"],
                             p=[0.36, 0.24, 0.12, 0.08, 0.08, 0.07, 0.05])
+            HISTORY.append((step, str(op), [(k.slot, m[0]) for k, m in keys], ctx.key_slots(), tuple(knobs)))
+            if TRACE:
+                print(*HISTORY[-1], flush=True)
             if op in ("seal", "open"):
                 if not keys:
                     new_key()
@@ -92,9 +109,12 @@ def test_random_operation_sequence(seed):
                 odescs = descs.copy()
                 odescs["key_idx"] = which
                 stream = side if rng.random() < 0.5 else None
+                knob_tag = f"burst_max={knobs[0]} aes_kernel={knobs[1]} stream={'side' if stream else 'ctx'} " \
+                           f"suites={sorted({c[1][0] for c in chosen})}"
                 d_desc, d_arena, d_status = ctx.alloc(descs.nbytes), ctx.alloc(arena.nbytes), ctx.alloc(n)
                 d_mask = ctx.alloc(5 * n) if op == "seal" else None
                 d_desc.upload(descs)
+                d_status.upload(np.full(n, 0x55, dtype=np.uint8))  # every status must be written by the engine
                 if op == "seal":
                     want = arena.copy()
                     want_masks = orc.fast_seal_batch(okeys, odescs, want, flags)
@@ -102,7 +122,7 @@ def test_random_operation_sequence(seed):
                     ctx.seal_batch(d_desc, n, d_arena, d_mask, d_status, flags, stream=stream)
                     pending.append(_Pending("seal", (d_desc, d_arena, d_mask, d_status), want,
                                             want_masks if flags & qpp.HP_MASK_OUT else None,
-                                            np.zeros(n, np.int8), n, f"step {step} seal n={n} flags={flags}"))
+                                            np.zeros(n, np.int8), n, f"step {step} seal n={n} flags={flags} {knob_tag}"))
                 else:
                     sealed = arena.copy()
                     orc.fast_seal_batch(okeys, odescs, sealed, 0)
@@ -121,7 +141,7 @@ def test_random_operation_sequence(seed):
                     ctx.open_batch(d_desc, n, d_arena, d_status, stream=stream)
                     pending.append(_Pending("open", (d_desc, d_arena, None, d_status), want, None,
                                             np.where(bad, qpp.DECRYPT_ERROR, qpp.OK).astype(np.int8), n,
-                                            f"step {step} open n={n}"))
+                                            f"step {step} open n={n} {knob_tag}"))
                 counts[op] += 1
             elif op == "update" and keys:
                 pick = sorted(rng.choice(len(keys), int(rng.integers(1, len(keys) + 1)), replace=False))
@@ -137,8 +157,10 @@ def test_random_operation_sequence(seed):
             elif op == "new" and len(keys) < 12:
                 new_key()
             elif op == "knob":
-                ctx.set_burst_max(int(rng.choice([0, 64, 16384])))
-                ctx.set_aes_kernel(int(rng.choice([qpp.AES_KERNEL_AUTO, qpp.AES_KERNEL_LANE, qpp.AES_KERNEL_WAVE])))
+                knobs[0] = int(rng.choice([0, 64, 16384]))
+                knobs[1] = int(rng.choice([qpp.AES_KERNEL_AUTO, qpp.AES_KERNEL_LANE, qpp.AES_KERNEL_WAVE]))
+                ctx.set_burst_max(knobs[0])
+                ctx.set_aes_kernel(knobs[1])
             elif op == "check":
                 for p in pending:
                     p.check(ctx)

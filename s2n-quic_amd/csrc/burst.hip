@@ -132,21 +132,16 @@ __device__ __forceinline__ void burst_packet(const AesLds &aes, const DevKey *__
     const uint32_t K = (m + 63u) >> 6, pad = 64u * K - m;
     uint4 acc = make_uint4(0, 0, 0, 0), ct0 = acc, ct1 = acc;  // ct0/ct1: ciphertext blocks 0/1 where owned
     uint4 ek = acc;  // E_K(J0), computed in pass 0 by the idle lane pad - 1 inside the data lanes' AES stream
-    // payload block of pass k for this lane (zero when the lane holds no data block in that pass); the next pass's
-    // block is loaded while this pass computes (for a zero-copy flush each load is a PCIe round trip)
-    auto load_pass = [&](uint32_t k) {
-        const int i = (int)(lane + 64u * k) - (int)pad;
-        return (i >= (int)a && i < (int)(a + c)) ? ld16(pay + 16u * ((uint32_t)i - a)) : make_uint4(0, 0, 0, 0);
-    };
-    uint4 nxt = load_pass(0);
     for (uint32_t k = 0; k < K; k++) {
         const int i = (int)(lane + 64u * k) - (int)pad;  // block index in the GHASH sequence
         const bool data = i >= (int)a && i < (int)(a + c);
         const bool j0 = k == 0 && i == -1;
         const uint32_t b = (uint32_t)i - a;  // data block b uses counter b + 2
-        uint4 in = nxt, ks = make_uint4(0, 0, 0, 0);
-        if (k + 1 < K) nxt = load_pass(k + 1);
-        if (data || j0) ks = aes.encrypt<NR>(make_uint4(p.n0, p.n1, p.n2, bswap32(data ? b + 2u : 1u)), rk);
+        uint4 in = make_uint4(0, 0, 0, 0), ks = in;
+        if (data || j0) {
+            if (data) in = ld16(pay + 16u * b);
+            ks = aes.encrypt<NR>(make_uint4(p.n0, p.n1, p.n2, bswap32(data ? b + 2u : 1u)), rk);
+        }
         uint4 x = make_uint4(0, 0, 0, 0);
         if (j0) ek = ks;
         if (i >= 0 && i < (int)a) {

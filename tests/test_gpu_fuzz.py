@@ -1,7 +1,8 @@
 """A seeded random sequence of engine operations, as a busy endpoint issues them: seal and open batches of every size
 class (one-wave burst, lane and wave-item kernels, ChaCha), over random mixes of the three suites, with and without
-header protection, on two streams of one context, interleaved with key updates, frees and new keys while earlier
-batches are still in flight, and with the kernel-choice knobs changed between batches.
+header protection, on two streams of one context; receive batches (unprotect -> PN expand -> open); GSO bursts through
+the transmit queue's asynchronous flushes (its own streams); all interleaved with key updates, frees, new keys and
+device key batches while earlier work is still in flight, and with the kernel-choice knobs changed between batches.
 
 Every batch is checked against the full-size checker (oracle/fastcheck.c, itself checked against the restatement in
 tests/test_fastcheck.py) with the key material it was ENQUEUED with: the stream-ordered key retirement
@@ -71,6 +72,92 @@ TRACE = bool(__import__("os").environ.get("QPP_FUZZ_TRACE"))
 SEEDS = [0xF022, 0xF023, 0xF024, 0xF025] + [0xF100 + i for i in range(int(__import__("os").environ.get("QPP_FUZZ_EXTRA", "0")))]
 
 
+TXQ_REGIONS, TXQ_REGION = 8, 1 << 17
+
+
+class _Check:
+    """a deferred check: fn() asserts, then releases what it holds"""
+
+    def __init__(self, fn):
+        self.fn = fn
+
+    def check(self, ctx):
+        self.fn()
+
+
+def _rx_op(ctx, rng, chosen, stream, tag):
+    """a GRO batch of protected short-header packets (phase 0) -> qpp_unprotect_open_batch, some tampered"""
+    n = int(rng.integers(1, 150))
+    chunks, rx, orx, off = [], [], [], 0
+    for i in range(n):
+        j = int(rng.integers(0, len(chosen)))
+        suite, k, iv, hp = chosen[j][1]
+        largest = int(rng.integers(0, 2**40))
+        pn = largest + int(rng.integers(0, 300))
+        _, _, pn_len = orc.truncate_pn(pn, largest)
+        header = bytes([0x40 | (pn_len - 1)]) + rng.integers(0, 256, int(rng.integers(0, 20)), dtype=np.uint8).tobytes()
+        payload = rng.integers(0, 256, int(rng.integers(4, 1400)), dtype=np.uint8).tobytes()
+        _, pkt = orc.protect_packet(suite, k, iv, hp, pn, header, pn_len, payload)
+        pkt = bytearray(pkt)
+        if rng.random() < 0.05:
+            pkt[-1] ^= 4
+        chunks.append(bytes(pkt) + bytes(int(rng.integers(0, 5))))
+        slot = chosen[j][0].slot
+        rx.append((largest, (slot, slot), off, len(header), len(pkt)))
+        orx.append((largest, (j, j), off, len(header), len(pkt)))
+        off += len(chunks[-1])
+    arena = np.frombuffer(b"".join(chunks) + bytes(64), dtype=np.uint8).copy()
+    rx, orx = np.array(rx, dtype=qpp.RX_DTYPE), np.array(orx, dtype=qpp.RX_DTYPE)
+    want = arena.copy()
+    want_out, want_st = orc.unprotect_open_batch(orc.make_keys([c[1] for c in chosen]), orx, want)
+    bufs = [ctx.alloc(rx.nbytes), ctx.alloc(arena.nbytes), ctx.alloc(n * qpp.PKT_DTYPE.itemsize), ctx.alloc(n)]
+    d_rx, d_arena, d_out, d_st = bufs
+    d_rx.upload(rx)
+    d_arena.upload(arena)
+    d_st.upload(np.full(n, 0x55, dtype=np.uint8))
+    ctx.unprotect_open_batch(d_rx, n, d_arena, d_out, d_st, stream=stream)
+
+    def fn():
+        ctx.synchronize()
+        st = d_st.download(dtype=np.int8)
+        assert list(st) == want_st, f"{tag}: status"
+        assert (d_arena.download() == want).all(), f"{tag}: arena"
+        out = d_out.download(dtype=qpp.PKT_DTYPE)
+        for f in ("pn", "aad_len", "pt_len", "pn_len", "off"):
+            assert (out[f] == want_out[f]).all(), f"{tag}: {f}"
+        for b in bufs:
+            b.free()
+    return _Check(fn)
+
+
+def _txq_op(txq, rng, chosen, region, tickets, tag):
+    """one GSO-sized burst pushed into the transmit queue's ring region and flushed asynchronously"""
+    base, off, expect = region * TXQ_REGION, 0, []
+    for _ in range(int(rng.integers(1, 65))):
+        j = int(rng.integers(0, len(chosen)))
+        key, (suite, k, iv, hp) = chosen[j]
+        pn = int(rng.integers(0, 2**40))
+        pn_len = int(rng.integers(1, 5))
+        header = bytes([0x40 | (pn_len - 1)]) + rng.integers(0, 256, int(rng.integers(0, 20)), dtype=np.uint8).tobytes()
+        payload = rng.integers(0, 256, int(rng.integers(4, 1400)), dtype=np.uint8).tobytes()
+        pkt = header + (pn & ((1 << (8 * pn_len)) - 1)).to_bytes(pn_len, "big") + payload
+        if off + len(pkt) + 16 > TXQ_REGION:
+            break
+        o = base + off
+        txq.ring[o:o + len(pkt)] = np.frombuffer(pkt, dtype=np.uint8)
+        txq.push(key, pn, o, len(header), pn_len, len(payload))
+        expect.append((o, orc.protect_packet(suite, k, iv, hp, pn, header, pn_len, payload)[1]))
+        off += len(pkt) + 16 + int(rng.integers(0, 9))
+    t = txq.flush_async()
+    tickets[region] = t
+
+    def fn():
+        txq.wait(t)
+        for o, prot in expect:
+            assert txq.ring[o:o + len(prot)].tobytes() == prot, f"{tag}: packet at ring offset {o}"
+    return _Check(fn)
+
+
 @pytest.mark.parametrize("seed", SEEDS)
 def test_random_operation_sequence(seed):
     rng = np.random.default_rng(seed)
@@ -86,12 +173,14 @@ def test_random_operation_sequence(seed):
 
     for _ in range(6):
         new_key()
-    pending, counts = [], {"seal": 0, "open": 0, "update": 0, "free": 0}
+    pending, counts = [], {"seal": 0, "open": 0, "update": 0, "free": 0, "rx": 0, "txq": 0}
+    txq = qpp.TxQueue(ctx, TXQ_REGIONS * TXQ_REGION, 512, in_flight=4)
+    txq_tickets, txq_next, txq_checks = [0] * TXQ_REGIONS, [0], [None] * TXQ_REGIONS
     knobs = [16384, qpp.AES_KERNEL_AUTO]
     try:
         for step in range(160):
-            op = rng.choice(["seal", "open", "update", "free", "new", "knob", "check"],
-                            p=[0.36, 0.24, 0.12, 0.08, 0.08, 0.07, 0.05])
+            op = rng.choice(["seal", "open", "update", "free", "new", "knob", "check", "rx", "txq", "newbatch"],
+                            p=[0.28, 0.18, 0.10, 0.07, 0.05, 0.06, 0.05, 0.09, 0.09, 0.03])
             HISTORY.append((step, str(op), [(k.slot, m[0]) for k, m in keys], ctx.key_slots(), tuple(knobs)))
             if TRACE:
                 print(*HISTORY[-1], flush=True)
@@ -143,6 +232,27 @@ def test_random_operation_sequence(seed):
                                             np.where(bad, qpp.DECRYPT_ERROR, qpp.OK).astype(np.int8), n,
                                             f"step {step} open n={n} {knob_tag}"))
                 counts[op] += 1
+            elif op == "rx" and keys:
+                chosen = [keys[i] for i in rng.choice(len(keys), int(rng.integers(1, len(keys) + 1)), replace=False)]
+                stream = side if rng.random() < 0.5 else None
+                pending.append(_rx_op(ctx, rng, chosen, stream, f"step {step} rx"))
+                counts["rx"] += 1
+            elif op == "txq" and keys:
+                chosen = [keys[i] for i in rng.choice(len(keys), int(rng.integers(1, len(keys) + 1)), replace=False)]
+                region = txq_next[0] % TXQ_REGIONS
+                txq_next[0] += 1
+                prev = txq_checks[region]
+                if prev is not None and prev in pending:  # the region's previous burst: checked before its bytes go
+                    prev.check(ctx)
+                    pending.remove(prev)
+                txq_checks[region] = _txq_op(txq, rng, chosen, region, txq_tickets, f"step {step} txq")
+                pending.append(txq_checks[region])
+                counts["txq"] += 1
+            elif op == "newbatch" and len(keys) < 10:
+                s_ = int(rng.choice([1, 2, 3]))
+                made = ctx.keys_batch(s_, [_secret(rng, s_) for _ in range(int(rng.integers(1, 3)))],
+                                      int(rng.integers(0, 3)))
+                keys.extend([k, (s_, *k.material())] for k in made)
             elif op == "update" and keys:
                 pick = sorted(rng.choice(len(keys), int(rng.integers(1, len(keys) + 1)), replace=False))
                 nxt = ctx.update_keys([keys[i][0] for i in pick])
@@ -167,8 +277,10 @@ def test_random_operation_sequence(seed):
                 pending = []
         for p in pending:
             p.check(ctx)
-        assert counts["seal"] > 30 and counts["open"] > 20 and counts["update"] > 5 and counts["free"] > 3, counts
+        assert counts["seal"] > 20 and counts["open"] > 12 and counts["update"] > 5 and counts["rx"] > 5 and \
+            counts["txq"] > 5, counts
     finally:
+        txq.close()
         for k, _ in keys:
             k.free()
         ctx.set_burst_max(16384)

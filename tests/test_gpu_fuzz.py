@@ -1,7 +1,8 @@
 """A seeded random sequence of engine operations, as a busy endpoint issues them: seal and open batches of every size
 class (one-wave burst, lane and wave-item kernels, ChaCha), over random mixes of the three suites, with and without
 header protection, on two streams of one context; receive batches (unprotect -> PN expand -> open); GSO bursts through
-the transmit queue's asynchronous flushes (its own streams); all interleaved with key updates, frees, new keys and
+the transmit queue's asynchronous flushes (its own streams); host-memory batches through the chunked H2D -> seal ->
+D2H pipeline (re-chunked at random); all interleaved with key updates, frees, new keys and
 device key batches while earlier work is still in flight, and with the kernel-choice knobs changed between batches.
 
 Every batch is checked against the full-size checker (oracle/fastcheck.c, itself checked against the restatement in
@@ -130,6 +131,30 @@ def _rx_op(ctx, rng, chosen, stream, tag):
     return _Check(fn)
 
 
+def _host_op(ctx, rng, chosen, tag):
+    """a batch in pinned host memory through the host pipeline (chunked H2D -> seal + HP mask -> D2H)"""
+    n = int(rng.choice([1, 50, 3000, 30000]))
+    descs, which, arena = _batch(rng, n, len(chosen), True)
+    descs["key_idx"] = np.array([c[0].slot for c in chosen], dtype=np.uint32)[which]
+    odescs = descs.copy()
+    odescs["key_idx"] = which
+    want = arena.copy()
+    want_masks = orc.fast_seal_batch(orc.make_keys([c[1] for c in chosen]), odescs, want, qpp.HP_MASK_OUT)
+    host = ctx.host_alloc(arena.nbytes)
+    host[:] = arena
+    masks = np.zeros(5 * n, np.uint8)
+    st = np.full(n, 0x55, np.int8)
+    t = ctx.host_submit(descs, host, masks, st, qpp.HP_MASK_OUT, qpp.OP_SEAL)
+
+    def fn():
+        ctx.host_wait(t)
+        assert (st == 0).all(), f"{tag}: status"
+        assert (host == want).all(), f"{tag}: arena"
+        assert (masks == want_masks).all(), f"{tag}: masks"
+        ctx.host_free(host)
+    return _Check(fn)
+
+
 def _txq_op(txq, rng, chosen, region, tickets, tag):
     """one GSO-sized burst pushed into the transmit queue's ring region and flushed asynchronously"""
     base, off, expect = region * TXQ_REGION, 0, []
@@ -173,14 +198,14 @@ def test_random_operation_sequence(seed):
 
     for _ in range(6):
         new_key()
-    pending, counts = [], {"seal": 0, "open": 0, "update": 0, "free": 0, "rx": 0, "txq": 0}
+    pending, counts = [], {"seal": 0, "open": 0, "update": 0, "free": 0, "rx": 0, "txq": 0, "host": 0}
     txq = qpp.TxQueue(ctx, TXQ_REGIONS * TXQ_REGION, 512, in_flight=4)
     txq_tickets, txq_next, txq_checks = [0] * TXQ_REGIONS, [0], [None] * TXQ_REGIONS
     knobs = [16384, qpp.AES_KERNEL_AUTO]
     try:
         for step in range(160):
-            op = rng.choice(["seal", "open", "update", "free", "new", "knob", "check", "rx", "txq", "newbatch"],
-                            p=[0.28, 0.18, 0.10, 0.07, 0.05, 0.06, 0.05, 0.09, 0.09, 0.03])
+            op = rng.choice(["seal", "open", "update", "free", "new", "knob", "check", "rx", "txq", "newbatch", "host"],
+                            p=[0.26, 0.16, 0.10, 0.07, 0.05, 0.06, 0.05, 0.08, 0.08, 0.03, 0.06])
             HISTORY.append((step, str(op), [(k.slot, m[0]) for k, m in keys], ctx.key_slots(), tuple(knobs)))
             if TRACE:
                 print(*HISTORY[-1], flush=True)
@@ -248,6 +273,13 @@ def test_random_operation_sequence(seed):
                 txq_checks[region] = _txq_op(txq, rng, chosen, region, txq_tickets, f"step {step} txq")
                 pending.append(txq_checks[region])
                 counts["txq"] += 1
+            elif op == "host" and keys:
+                chosen = [keys[i] for i in rng.choice(len(keys), int(rng.integers(1, len(keys) + 1)), replace=False)]
+                if rng.random() < 0.3:  # re-chunk the pipeline (small chunks: many chunks per batch)
+                    ctx.set_host_pipe(int(rng.choice([64, 1000, 65536])), int(rng.choice([1, 4, 64])) << 20,
+                                      int(rng.integers(2, 5)))
+                pending.append(_host_op(ctx, rng, chosen, f"step {step} host"))
+                counts["host"] += 1
             elif op == "newbatch" and len(keys) < 10:
                 s_ = int(rng.choice([1, 2, 3]))
                 made = ctx.keys_batch(s_, [_secret(rng, s_) for _ in range(int(rng.integers(1, 3)))],

@@ -318,3 +318,94 @@ def test_random_operation_sequence(seed):
         ctx.set_burst_max(16384)
         ctx.set_aes_kernel(qpp.AES_KERNEL_AUTO)
         ctx.close()
+
+
+@pytest.mark.parametrize("seed", [0xF1F5, 0xF1F6])
+def test_random_fips_sequence(seed):
+    """FIPS mode under churn (aead/fips.rs:13-60): AES keys created with the mode on refuse seals whose nonce does not
+    come after the key's previous one (aws-lc's TLS 1.3 rule, state carried across batches), ChaCha keys never do.
+    Random seal batches (one stream: the rule is defined in submission order) over random key subsets, packet numbers
+    mostly increasing with repeats and steps back, interleaved with key updates (fresh FIPS state), frees, new keys and
+    kernel-path flips; statuses, refused-untouched bytes and sealed bytes against orc_seal_batch_fips."""
+    rng = np.random.default_rng(seed)
+    ctx = qpp.Context(0)
+    ctx.set_fips(True)
+    keys = []  # [Key, material, OrcFipsState (the oracle's copy of the key's device state), next pn]
+
+    def add(k):
+        keys.append([k, (k.suite, *k.material()), orc.fips_states(1)[0], int(rng.integers(0, 2**30))])
+
+    try:
+        for _ in range(4):
+            s = int(rng.choice([1, 2, 3]))
+            add(ctx.key(s, _secret(rng, s)))
+        refused = 0
+        for step in range(70):
+            op = rng.choice(["seal", "update", "free", "new", "knob"], p=[0.6, 0.12, 0.08, 0.1, 0.1])
+            if op == "seal" and keys:
+                pick = rng.choice(len(keys), int(rng.integers(1, len(keys) + 1)), replace=False)
+                chosen = [keys[i] for i in pick]
+                n = int(rng.integers(1, 300))
+                descs = np.zeros(n, dtype=qpp.PKT_DTYPE)
+                pn_len = rng.integers(1, 5, n)
+                aad = pn_len + rng.integers(0, 30, n)
+                pt = rng.integers(4, 600, n)
+                size = aad + pt + 16
+                descs["off"] = np.concatenate([[0], np.cumsum(size + 3)[:-1]])
+                descs["aad_len"], descs["pt_len"], descs["pn_len"] = aad, pt, pn_len
+                which = rng.integers(0, len(chosen), n)
+                for i in range(n):
+                    c = chosen[int(which[i])]
+                    r = rng.random()
+                    c[3] = c[3] + 1 if r < 0.8 else c[3] if r < 0.9 else max(0, c[3] - int(rng.integers(1, 5)))
+                    descs[i]["pn"] = c[3]
+                descs["key_idx"] = np.array([c[0].slot for c in chosen], dtype=np.uint32)[which]
+                arena = rng.integers(0, 256, int(descs["off"][-1] + size[-1]) + 64, dtype=np.uint8)
+                odescs = descs.copy()
+                odescs["key_idx"] = which
+                states = orc.fips_states(len(chosen))
+                for j, c in enumerate(chosen):
+                    states[j] = c[2]
+                want = arena.copy()
+                flags = qpp.HP_MASK_OUT | qpp.HP_APPLY
+                want_masks, want_st = orc.seal_batch_fips(orc.make_keys([c[1] for c in chosen]),
+                                                          [bool(c[0].fips) for c in chosen], states, odescs, want,
+                                                          flags)
+                for j, c in enumerate(chosen):
+                    c[2] = states[j]
+                d_desc, d_arena, d_mask, d_st = ctx.alloc(descs.nbytes), ctx.alloc(arena.nbytes), ctx.alloc(5 * n), \
+                    ctx.alloc(n)
+                d_desc.upload(descs)
+                d_arena.upload(arena)
+                d_st.upload(np.full(n, 0x55, dtype=np.uint8))
+                ctx.seal_batch(d_desc, n, d_arena, d_mask, d_st, flags)
+                ctx.sync()
+                st = d_st.download(dtype=np.int8)
+                assert list(st) == want_st, f"step {step}: FIPS statuses"
+                assert (d_arena.download() == want).all(), f"step {step}: arena"
+                ok = np.array(want_st) == 0
+                m = d_mask.download().reshape(-1, 5)[ok]
+                assert (m == np.frombuffer(want_masks, dtype=np.uint8).reshape(-1, 5)[ok]).all()
+                refused += int((~ok).sum())
+                for b in (d_desc, d_arena, d_mask, d_st):
+                    b.free()
+            elif op == "update" and keys:
+                pick = sorted(rng.choice(len(keys), int(rng.integers(1, len(keys) + 1)), replace=False))
+                nxt = ctx.update_keys([keys[i][0] for i in pick])
+                for i, k in zip(pick, nxt):
+                    keys[i][0].free()
+                    pn = keys[i][3]
+                    keys[i] = [k, (k.suite, *k.material()), orc.fips_states(1)[0], pn]  # a new key: a fresh state
+            elif op == "free" and len(keys) > 1:
+                keys.pop(int(rng.integers(0, len(keys))))[0].free()
+            elif op == "new" and len(keys) < 8:
+                s = int(rng.choice([1, 2, 3]))
+                add(ctx.key(s, _secret(rng, s)))
+            elif op == "knob":
+                ctx.set_burst_max(int(rng.choice([0, 64, 16384])))
+                ctx.set_aes_kernel(int(rng.choice([qpp.AES_KERNEL_AUTO, qpp.AES_KERNEL_LANE, qpp.AES_KERNEL_WAVE])))
+        assert refused > 20
+    finally:
+        for k in keys:
+            k[0].free()
+        ctx.close()

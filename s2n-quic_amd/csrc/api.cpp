@@ -102,6 +102,12 @@ struct qpp_ctx {
     uint32_t live_slot_xor = 0;                  // XOR of the live packet keys' slots: THE slot when only one is live
     bool fips = false;                           // qpp_ctx_set_fips: AES packet keys created now seal in FIPS mode
     uint32_t fips_live = 0;                      // live FIPS keys: seal batches run the nonce-order gate
+    // The nonce-order state lives in the device key records and the gate reads and advances it without atomics, so
+    // the gates of all streams run one after another in submission order: each gate's stream waits for this event
+    // (recorded behind the previous gate, on whatever stream that ran) -- two txq flushes in flight on different
+    // streams could otherwise both pass a repeated packet number, or a later flush refuse an earlier one's packets.
+    hipEvent_t fips_order = nullptr;
+    bool fips_order_used = false;
     uint32_t next_slot = 0;
     // per-stream state (plan scratch, last-batch event); [0] is the context stream
     std::vector<StreamState *> streams;
@@ -242,9 +248,12 @@ int grow_keys(qpp_ctx *ctx, uint32_t need) {
     uint8_t *np = ctx->pow.base;
     if (pcap > ctx->pow.cap) {  // the precomputed tables of the slots so far move along
         HIP_TRY(ctx, hipMalloc(&np, (size_t)pcap * kPowBytes));
-        if (ctx->pow.cap)
+        if (ctx->pow.cap) {
             HIP_TRY(ctx, hipMemcpyAsync(np, ctx->pow.base, (size_t)ctx->pow.cap * kPowBytes, hipMemcpyDeviceToDevice,
                                         ctx->kstream));
+            // powers of each key's H: zeroized before the old buffer goes back to the allocator, like the records
+            HIP_TRY(ctx, hipMemsetAsync(ctx->pow.base, 0, (size_t)ctx->pow.cap * kPowBytes, ctx->kstream));
+        }
     }
     HIP_TRY(ctx, hipStreamSynchronize(ctx->kstream));
     if (ctx->d_keys) HIP_TRY(ctx, hipFree(ctx->d_keys));
@@ -357,9 +366,13 @@ int ensure_fips(qpp_ctx *ctx, StreamState *st, uint32_t n) {
 int fips_gate(qpp_ctx *ctx, StreamState *st, const qpp_pkt *&descs, uint32_t n, int8_t *status, uint32_t *refused) {
     if (!ctx->fips_live || !n) return QPP_OK;
     RC_TRY(ensure_fips(ctx, st, n));
+    if (!ctx->fips_order) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->fips_order, hipEventDisableTiming));
+    if (ctx->fips_order_used) HIP_TRY(ctx, hipStreamWaitEvent(st->stream, ctx->fips_order, 0));
     qpp_pkt *gated = nullptr;
     HIP_TRY(ctx, launch_fips_gate(ctx->d_keys, ctx->key_cap, descs, n, st->fips_buf, st->fips_bytes, &gated, status,
                                   refused, st->stream));
+    HIP_TRY(ctx, hipEventRecord(ctx->fips_order, st->stream));
+    ctx->fips_order_used = true;
     descs = gated;
     return QPP_OK;
 }
@@ -679,11 +692,13 @@ int mask_one(qpp_ctx *ctx, uint32_t slot, const uint8_t *sample, uint8_t mask[5]
     return QPP_OK;
 }
 
+int derive_batch_device(qpp_ctx *ctx, int suite, const uint8_t *secrets, const uint8_t *hp_in, size_t n,
+                        uint32_t updates, const std::vector<uint32_t> &slots, qpp_key **out);
+
 // n secrets (n * hash_len, host) [+ header keys hp_in, n * key_len, host] -> n device-derived keys in fresh or
 // recycled slots.  updates x "quic ku" on each; material copied back for the host handles.
 int derive_batch(qpp_ctx *ctx, int suite, const uint8_t *secrets, const uint8_t *hp_in, size_t n, uint32_t updates,
                  qpp_key **out) {
-    const size_t hl = suite_hash_len(suite), kl = suite_key_len(suite), mb = key_material_bytes();
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     RC_TRY(flush_keys(ctx));  // pending host records first
     // The pinned key stage is reused below: the records that flush just queued are copied from it asynchronously, so
@@ -692,8 +707,26 @@ int derive_batch(qpp_ctx *ctx, int suite, const uint8_t *secrets, const uint8_t 
     HIP_TRY(ctx, hipStreamSynchronize(ctx->kstream));
     if (ctx->kstage_pending) secure_zero(ctx->h_kstage, ctx->kstage_pending);
     ctx->kstage_pending = 0;
-    std::vector<uint32_t> slots(n);
-    for (size_t i = 0; i < n; i++) RC_TRY(alloc_slot(ctx, &slots[i]));
+    std::vector<uint32_t> slots;
+    slots.reserve(n);
+    // a failure after slots were taken gives them back through retirement (the device may have written their records)
+    auto give_back = [&](int rc) {
+        for (uint32_t s : slots) retire_slot(ctx, s);
+        return rc;
+    };
+    for (size_t i = 0; i < n; i++) {
+        uint32_t s = 0;
+        if (int rc = alloc_slot(ctx, &s)) return give_back(rc);
+        slots.push_back(s);
+    }
+    if (int rc = derive_batch_device(ctx, suite, secrets, hp_in, n, updates, slots, out)) return give_back(rc);
+    return QPP_OK;
+}
+
+// derive_batch after the slots are taken: stage, derive on the device, copy the material back, make the handles
+int derive_batch_device(qpp_ctx *ctx, int suite, const uint8_t *secrets, const uint8_t *hp_in, size_t n,
+                        uint32_t updates, const std::vector<uint32_t> &slots, qpp_key **out) {
+    const size_t hl = suite_hash_len(suite), kl = suite_key_len(suite), mb = key_material_bytes();
     // key stage: secrets | hp_in | slots | material
     const size_t o_hp = n * hl, o_slot = o_hp + (hp_in ? n * kl : 0), o_mat = (o_slot + 4 * n + 15) & ~size_t(15);
     const size_t total = o_mat + n * mb;
@@ -881,6 +914,7 @@ void qpp_ctx_destroy(qpp_ctx *ctx) {
     if (ctx->kstream) hipStreamDestroy(ctx->kstream);
     if (ctx->rstream) hipStreamDestroy(ctx->rstream);
     if (ctx->keys_ready) hipEventDestroy(ctx->keys_ready);
+    if (ctx->fips_order) hipEventDestroy(ctx->fips_order);
     delete ctx;
 }
 
@@ -944,6 +978,7 @@ int qpp_key_update_batch(qpp_key *const *keys, size_t n, qpp_key **out) {
     if (!out || (n && !keys)) return QPP_INTERNAL_ERROR;
     if (!n) return QPP_OK;
     if (n > (1u << 24)) return QPP_INTERNAL_ERROR;
+    for (size_t i = 0; i < n; i++) out[i] = nullptr;  // the caller's array may be uninitialised
     qpp_ctx *ctx = keys[0] ? keys[0]->ctx : nullptr;
     if (!ctx) return QPP_INTERNAL_ERROR;
     for (size_t i = 0; i < n; i++)
@@ -1256,6 +1291,9 @@ int qpp_seal_batch(qpp_ctx *ctx, const qpp_pkt *descs, size_t n, uint8_t *arena,
     if ((flags & QPP_HP_MASK_OUT) && !masks) return QPP_INTERNAL_ERROR;
     if (n > UINT32_MAX) return QPP_INTERNAL_ERROR;
     if (!n) return QPP_OK;
+    // FIPS mode refuses out-of-order nonces per packet (the packet stays plaintext): without a status array the call
+    // could not say which, so it is refused (the reference fails such an encrypt call: aead/fips.rs)
+    if (ctx->fips_live && !status && !(flags & QPP_ONLY_CHACHA)) return QPP_INTERNAL_ERROR;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     RC_TRY(flush_keys(ctx));
     StreamState *st = nullptr;
@@ -1370,6 +1408,8 @@ int qpp_host_batch_submit(qpp_ctx *ctx, const qpp_pkt *descs, size_t n, uint8_t 
     if (!(ops & (QPP_OP_SEAL | QPP_OP_OPEN)) || (ops & ~(QPP_OP_SEAL | QPP_OP_OPEN))) return QPP_INTERNAL_ERROR;
     if ((flags & QPP_HP_MASK_OUT) && !(masks && (ops & QPP_OP_SEAL))) return QPP_INTERNAL_ERROR;
     if ((ops & QPP_OP_OPEN) && n && !status) return QPP_INTERNAL_ERROR;
+    if ((ops & QPP_OP_SEAL) && n && !status && ctx->fips_live && !(flags & QPP_ONLY_CHACHA))
+        return QPP_INTERNAL_ERROR;  // FIPS refusals are reported per packet (qpp_seal_batch)
     if ((ops & QPP_OP_SEAL) && (ops & QPP_OP_OPEN) && (flags & QPP_HP_APPLY)) return QPP_INTERNAL_ERROR;
     *ticket = 0;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
@@ -1567,7 +1607,6 @@ struct TxqSlot {
     uint64_t first = 0, last = 0;  // tickets (bursts) of the flush that last used this slot (0: never)
     uint32_t *h_refused = nullptr;  // pinned: packets of the flush the FIPS nonce-order gate refused
     bool busy = false;    // `done` recorded and not yet seen complete
-    size_t lo = 0, hi = 0;  // ring span of that flush (DMA path)
 };
 
 struct qpp_txq {
@@ -1589,6 +1628,7 @@ struct qpp_txq {
     // plan directly over PCIe (no DMA copies, no plan launches)
     uint32_t zc_max = 0;
     std::vector<uint32_t> order;
+    std::vector<std::pair<size_t, size_t>> runs;  // DMA path: the flush's contiguous packet byte ranges
 };
 
 extern "C" {
@@ -1796,14 +1836,33 @@ static int txq_submit(qpp_txq *q) {
         RC_TRY(txq_enqueue_zero_copy(q, sl, st, n));
     } else {
         hipStream_t s = sl.stream;
-        const size_t span = q->hi - q->lo;
-        HIP_TRY(ctx, hipMemcpyAsync(q->d_ring + q->lo, q->h_ring + q->lo, span, hipMemcpyHostToDevice, s));
+        // Only this flush's own packet bytes travel, as runs of adjacent packets: the ring between and around them
+        // belongs to the transport or to other flushes in flight (a copy of the whole [lo, hi) span would write stale
+        // device bytes over them on the way back)
+        std::vector<std::pair<size_t, size_t>> &runs = q->runs;
+        runs.clear();
+        for (uint32_t i = 0; i < n; i++) {
+            const qpp_pkt &d = sl.h_desc[i];
+            runs.emplace_back((size_t)d.off, (size_t)d.off + d.aad_len + d.pt_len + 16);
+        }
+        std::sort(runs.begin(), runs.end());
+        size_t w = 0;
+        for (size_t i = 1; i < runs.size(); i++) {
+            if (runs[i].first <= runs[w].second) runs[w].second = std::max(runs[w].second, runs[i].second);
+            else runs[++w] = runs[i];
+        }
+        runs.resize(w + 1);
+        for (const auto &r : runs)
+            HIP_TRY(ctx, hipMemcpyAsync(q->d_ring + r.first, q->h_ring + r.first, r.second - r.first,
+                                        hipMemcpyHostToDevice, s));
         HIP_TRY(ctx, hipMemcpyAsync(sl.d_desc, sl.h_desc, sizeof(qpp_pkt) * n, hipMemcpyHostToDevice, s));
         uint32_t flags = QPP_HP_APPLY;
         if (!(q->suites & ~kAesSuites)) flags |= QPP_ONLY_AES;
         else if (!(q->suites & kAesSuites)) flags |= QPP_ONLY_CHACHA;
         RC_TRY(enqueue_seal(ctx, st, sl.d_desc, n, q->d_ring, nullptr, nullptr, flags, st->fips_refused));
-        HIP_TRY(ctx, hipMemcpyAsync(q->h_ring + q->lo, q->d_ring + q->lo, span, hipMemcpyDeviceToHost, s));
+        for (const auto &r : runs)
+            HIP_TRY(ctx, hipMemcpyAsync(q->h_ring + r.first, q->d_ring + r.first, r.second - r.first,
+                                        hipMemcpyDeviceToHost, s));
     }
     if (gate) HIP_TRY(ctx, hipMemcpyAsync(sl.h_refused, st->fips_refused, 4, hipMemcpyDeviceToHost, sl.stream));
     RC_TRY(note_work(ctx, st));  // key retirement orders behind this flush
@@ -1811,8 +1870,6 @@ static int txq_submit(qpp_txq *q) {
     sl.busy = true;
     sl.first = q->pend_first;
     sl.last = q->pend_last;
-    sl.lo = q->lo;
-    sl.hi = q->hi;
     q->pend_first = q->pend_last = 0;
     q->pend_bursts = 0;
     q->count = q->count_at_ticket = 0;

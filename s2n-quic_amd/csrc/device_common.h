@@ -215,17 +215,18 @@ __device__ __forceinline__ void static_for(F &&f) {
     static_for_impl(f, std::make_integer_sequence<int, N>{});
 }
 
-template <int NR, int NB>
+// STRIDE: the NB blocks are counters c0, c0 + STRIDE, ... (the quad layout's lane takes every 4th counter block)
+template <int NR, int NB, int STRIDE = 1>
 __device__ __forceinline__ void ctr_keystream_pipe(const AesLds &a, const CtrPage &pg, const uint32_t *__restrict__ rk,
                                                    uint32_t c0, uint4 (&ks)[NB]) {
-    static_assert(NB >= 2 && NB <= 4, "pipeline depth NB - 1 lookups groups of 4 within the 15-read counter");
+    static_assert(NB >= 1 && NB <= 4, "pipeline depth NB - 1 lookups groups of 4 within the 15-read counter");
     constexpr int D = NB - 1;
     constexpr int U = (NR - 2) * 4 * NB;  // units of rounds 3..NR
     // round states by parity; the final round writes into the parity buffer of round NR - 2, dead by then
     uint32_t st[2][NB][4];
     uint32_t ld[D + 1][4];  // lookups of the units in flight (ring)
 #pragma unroll
-    for (int j = 0; j < NB; j++) pg.two_rounds(a, c0 + j, st[0][j]);  // round-2 state (round 2 is even)
+    for (int j = 0; j < NB; j++) pg.two_rounds(a, c0 + STRIDE * j, st[0][j]);  // round-2 state (round 2 is even)
     auto issue = [&](auto uc) {
         constexpr int u = decltype(uc)::value;
         constexpr int r = 3 + u / (4 * NB), c = (u / NB) & 3, j = u % NB;

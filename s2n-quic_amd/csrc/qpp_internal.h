@@ -156,6 +156,10 @@ hipError_t launch_aes_gcm(bool seal, const DevKey *keys, const qpp_pkt *descs, c
 hipError_t launch_aes_gcm_single(bool seal, const DevKey *keys, const qpp_pkt *descs, uint32_t slot, uint32_t nr,
                                  uint32_t n, uint32_t n_cu, uint8_t *arena, uint8_t *masks, int8_t *status,
                                  uint32_t flags, hipStream_t s);
+// quad.hip: the quad-layout (4 lanes per packet, 1024-thread workgroups) throughput kernel behind the two above
+hipError_t launch_aes_gcm_quad(bool seal, uint32_t nr, dim3 grid, hipStream_t s, const DevKey *keys,
+                               const qpp_pkt *descs, const PlanBuffers &pb, uint8_t *arena, uint8_t *masks,
+                               int8_t *status, uint32_t flags, uint32_t single, uint32_t n_single);
 // many keys: work items of <= kWavePacketsPerItem packets (plan with per = kWavePacketsPerItem), one wave each
 hipError_t launch_aes_gcm_wave(bool seal, const DevKey *keys, const qpp_pkt *descs, const PlanBuffers &pb, uint32_t n,
                                uint32_t key_cap, uint32_t n_cu, uint8_t *arena, uint8_t *masks, int8_t *status,

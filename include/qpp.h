@@ -300,6 +300,14 @@ uint8_t *qpp_txq_ring(qpp_txq *q);
  * context. */
 int qpp_txq_push(qpp_txq *q, const qpp_key *key, uint64_t pn, size_t off, size_t header_len, size_t pn_len,
                  size_t payload_len);
+/* qpp_txq_push for a scatter::Buffer with an `extra` tail (common/s2n-codec/src/encoder/scatter.rs:6-68;
+ * encoding.rs:245-270 re-wraps the inline bytes + extra before crypto::encrypt): the packet's inline plaintext
+ * (inline_len bytes after header || PN) is already in the ring; the extra bytes are copied into the ring right after
+ * it (what scatter::Buffer::flatten does, since the engine seals contiguous bytes), then the packet is pushed with
+ * payload_len = inline_len + extra_len.  extra may be NULL when extra_len is 0.  Same errors as qpp_txq_push; nothing
+ * is copied unless the push is accepted. */
+int qpp_txq_push_scatter(qpp_txq *q, const qpp_key *key, uint64_t pn, size_t off, size_t header_len, size_t pn_len,
+                         size_t inline_len, const uint8_t *extra, size_t extra_len);
 /* n pushes at once from ready descriptors (key_idx = qpp_key_slot of a live key of this context, off into the ring,
  * aad_len = header_len + pn_len, flags 0): for bindings whose per-call cost dominates a GSO burst (Python), same
  * checks as qpp_txq_push; nothing is queued unless every descriptor passes. */

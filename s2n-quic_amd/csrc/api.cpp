@@ -1742,6 +1742,19 @@ int qpp_txq_push(qpp_txq *q, const qpp_key *key, uint64_t pn, size_t off, size_t
     return QPP_OK;
 }
 
+int qpp_txq_push_scatter(qpp_txq *q, const qpp_key *key, uint64_t pn, size_t off, size_t header_len, size_t pn_len,
+                         size_t inline_len, const uint8_t *extra, size_t extra_len) {
+    if (!q || (extra_len && !extra)) return QPP_INTERNAL_ERROR;
+    const size_t payload_len = inline_len + extra_len;
+    if (payload_len < inline_len || off > q->ring_bytes || header_len + pn_len > q->ring_bytes - off ||
+        inline_len > q->ring_bytes - off - header_len - pn_len)
+        return QPP_INTERNAL_ERROR;
+    const size_t at = off + header_len + pn_len + inline_len;
+    RC_TRY(qpp_txq_push(q, key, pn, off, header_len, pn_len, payload_len));  // every range / capacity check
+    if (extra_len) memcpy(q->h_ring + at, extra, extra_len);  // the ring holds it through end + 16 (checked above)
+    return QPP_OK;
+}
+
 int qpp_txq_push_descs(qpp_txq *q, const qpp_pkt *descs, size_t n) {
     if (!q || (n && !descs)) return QPP_INTERNAL_ERROR;
     if (n > q->max_packets - q->count) return QPP_INTERNAL_ERROR;  // flush first

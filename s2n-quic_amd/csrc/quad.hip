@@ -33,7 +33,10 @@ using namespace dev;
 
 constexpr uint32_t kQLdsPow = 131072;  // 4-bit tables of H^1..H^4
 constexpr uint32_t kQLdsVe = 65536;    // V_e during the build
-constexpr int kQuadWG = 1024;
+#ifndef QPP_QUAD_WG
+#define QPP_QUAD_WG 768  // 3 waves per SIMD (<= 168 VGPRs: no spills); 1024 (4 waves, <= 128) spilled: 8 % slower (profiles/r03g_wg)
+#endif
+constexpr int kQuadWG = QPP_QUAD_WG;
 constexpr uint32_t kQuadPkts = kQuadWG / 4;  // packets per workgroup pass
 
 // X * H through the 8-bit tables of H at [0, 64K) (T_j[x] at 256 x + 16 j): the setup's products
@@ -102,101 +105,168 @@ constexpr int kQuadSwap2 = 0x4e;   // [2, 3, 0, 1]
 constexpr int kQuadBcast1 = 0x55;  // [1, 1, 1, 1]
 constexpr int kQuadBcast2 = 0xaa;  // [2, 2, 2, 2]
 
+// AES of one block over the 4 lanes of a quad, column s of the state in lane s: per round each lane takes bytes 1, 2, 3
+// of its right-hand neighbours' columns through DPP (3 moves) and does its column's 4 lookups, so a once-per-packet
+// block (the header-protection mask; E_K(J0) when opening) costs the wave a quarter of what one lane doing the whole
+// block costs.  rk_g: a key schedule in the key record (lane s reads word s of each round).  Returns column s of E(in).
+constexpr int kQuadRot1 = 0x39;  // [1, 2, 3, 0]
+constexpr int kQuadRot3 = 0x93;  // [3, 0, 1, 2]
+template <int NR>
+__device__ __forceinline__ uint32_t aes_quad(const AesLds &a, const uint32_t *__restrict__ rk_g, uint32_t col, uint32_t s) {
+    uint32_t rk[NR + 1];
+#pragma unroll
+    for (int r = 0; r <= NR; r++) rk[r] = rk_g[4 * r + s];
+    uint32_t x = col ^ rk[0];
+#pragma unroll
+    for (int r = 1; r <= NR; r++) {
+        const uint32_t b = qperm<kQuadRot1>(x), c = qperm<kQuadSwap2>(x), d = qperm<kQuadRot3>(x);
+        if (r < NR) {
+            x = a.col(x, b, c, d, rk[r]);
+        } else {
+            x = a.last(x, b, c, d, rk[r]);
+        }
+    }
+    return x;
+}
+
+// The descriptor again at the packet's tail (through a laundered pointer, so that the compiler reloads it instead of
+// keeping its fields in VGPRs across the group loop: the loop needs only the payload offset, length and nonce)
+__device__ __forceinline__ qpp_pkt reload_desc(const qpp_pkt *p) {
+    uint64_t a = (uint64_t)p;
+    asm volatile("" : "+v"(a));
+    return *(const qpp_pkt *)a;
+}
+
 // One packet per quad; s = lane % 4.  has = false: the quad has no packet (its lanes only keep the wave's loop shape).
+// Addresses are 32-bit offsets into the arena (SGPR base + VGPR offset).
 template <int NR, bool SEAL>
 __device__ __forceinline__ void quad_packet(const AesLds &aes, const GhashT<true> &gh, const DevKey *__restrict__ key,
-                                            const uint32_t *__restrict__ rk, bool has, const qpp_pkt &d,
-                                            uint32_t pkt_index, uint8_t *arena, uint8_t *masks, int8_t *status,
+                                            bool has, const qpp_pkt &d,
+                                            const qpp_pkt *__restrict__ dptr, uint32_t pkt_index,
+                                            uint8_t *__restrict__ arena, uint8_t *masks, int8_t *status,
                                             uint32_t flags, uint32_t s) {
-    constexpr int NB = 4;
-    PacketView p = load_packet(d, key, arena);
-    if (!has) p.len = 0;
-    uint8_t *pay = p.base + p.aad_len;
-    const int len = (int)p.len, nfull = len >> 4, rem = len & 15, m = nfull + (rem ? 1 : 0);
-    const int a = has ? (int)((p.aad_len + 15) >> 4) : 0;
+    // loop state
+    const uint32_t aad_len = d.aad_len, len = has ? d.pt_len : 0u, pay = d.off + aad_len;
+    const uint32_t n0 = key->iv[0], n1 = key->iv[1] ^ bswap32((uint32_t)(d.pn >> 32)),  // Iv::nonce (iv.rs:27-39)
+                   n2 = key->iv[2] ^ bswap32((uint32_t)d.pn);
+    const int nfull = (int)(len >> 4), rem = (int)(len & 15), m = nfull + (rem ? 1 : 0);
+    const int a = has ? (int)((aad_len + 15) >> 4) : 0;
+    auto at = [&](uint32_t off) { return arena + off; };
 
     // AAD blocks of this lane: virtual slots t = 1 - a .. 0, t = s (mod 4).  The chain starts at w = 0: its first step
     // multiplies zero (one product more per lane that has no AAD block, in exchange for no started-flag control flow)
     uint4 w = make_uint4(0, 0, 0, 0);
     for (int t = (1 - a) + (((int)s - (1 - a)) & 3); t <= 0; t += 4) {
         const uint32_t i = (uint32_t)(t + a - 1);
-        uint4 x = ld16(p.base + 16 * i);
-        const uint32_t r = p.aad_len - 16 * i;
+        uint4 x = ld16(at(d.off + 16 * i));
+        const uint32_t r = aad_len - 16 * i;
         if (r < 16) x = keep_bytes(x, r);
         w = gh.mulx(w, x);
     }
 
+    // Round keys: scalar loads where they are used (the key record stays in the scalar cache) instead of 44 / 60 SGPRs
+    // held for the whole kernel, which pushed other uniform values into VGPR lanes (a v_readlane per use in the loop)
+    auto round_keys = [&](uint32_t (&k)[4 * (NR + 1)]) {
+        uint64_t a = (uint64_t)key->rk;
+        asm volatile("" : "+s"(a));  // reloaded here, not hoisted into SGPRs for the whole loop
+        const uint4 *p = (const uint4 *)a;
+#pragma unroll
+        for (int r = 0; r <= NR; r++) {
+            const uint4 v = p[r];
+            k[4 * r] = v.x; k[4 * r + 1] = v.y; k[4 * r + 2] = v.z; k[4 * r + 3] = v.w;
+        }
+    };
     CtrPage pg;
-    pg.build(aes, rk, p.n0, p.n1, p.n2, 0);
+    {
+        uint32_t rk[4 * (NR + 1)];
+        round_keys(rk);
+        pg.build(aes, rk, n0, n1, n2, 0);
+    }
     const int ngroups = has ? (m + 1 + 15) >> 4 : 0;  // counter slots 0 (J0) .. m
     const int G = (int)wave_max((uint32_t)ngroups);
     const int min_full = (int)__builtin_amdgcn_readfirstlane(wave_min(has ? (uint32_t)nfull : 0u));
     auto interior = [&](int g) { return g >= 1 && 16 * g + 15 <= min_full; };  // every slot a whole payload block
+    // counter blocks per lane the last group needs (uniform): the longest packet's slots past 16 (G - 1)
+    const int tail_slots = (int)wave_max(has ? (uint32_t)max(0, m + 1 - 16 * (G - 1)) : 0u);
+    // length block: be64(aad bits) || be64(payload bits)
+    auto lenblk = [&]() { return make_uint4(0, bswap32(aad_len * 8), 0, bswap32(len * 8)); };
+    bool len_done = !has;
 
-    uint4 ek0 = make_uint4(0, 0, 0, 0), smp = make_uint4(0, 0, 0, 0);
-    for (int g = 0; g < G; g++) {
-        const bool inner = interior(g);  // uniform
-        const int t0 = 16 * g + (int)s;  // slot of k = 0; slot t holds counter t + 1 and ciphertext block t - 1
-        uint4 ks[NB];
+    // one group: slots t = 16 g + 4 k + s, k < NBG; slot t holds counter t + 1 and ciphertext block t - 1
+    auto group = [&](auto nbc, int g) {
+        constexpr int NBG = decltype(nbc)::value;
+        const bool inner = NBG == 4 && interior(g);  // uniform
+        uint32_t rk[4 * (NR + 1)];
+        round_keys(rk);
+        const int t0 = 16 * g + (int)s;
+        uint4 ks[NBG];
         const uint32_t c0 = (uint32_t)t0 + 1u;
-        if ((g & 15) != 15) {  // uniform: no lane's 4 counters straddle a 256-block page
-            if ((c0 >> 8) != pg.page) pg.build(aes, rk, p.n0, p.n1, p.n2, c0 >> 8);
-            ctr_keystream_pipe<NR, NB, 4>(aes, pg, rk, c0, ks);
+        // The nonce words are laundered where the loop uses them (a new page; the straddling group): left alone, the
+        // compiler hoisted the page build's first-round lookups addresses out of the loop as loop invariants and
+        // spilled them (16 scratch accesses per group in the open kernel).
+        uint32_t m0 = n0, m1 = n1, m2 = n2;
+        if ((g & 15) != 15) {  // uniform: no lane's counters straddle a 256-block page
+            if ((c0 >> 8) != pg.page) {
+                asm volatile("" : "+v"(m0), "+v"(m1), "+v"(m2));
+                pg.build(aes, rk, m0, m1, m2, c0 >> 8);
+            }
+            ctr_keystream_pipe<NR, NBG, 4>(aes, pg, rk, c0, ks);
         } else {
-            static_for<NB>([&](auto kc) {
+            asm volatile("" : "+v"(m0), "+v"(m1), "+v"(m2));
+            static_for<NBG>([&](auto kc) {
                 constexpr int k = decltype(kc)::value;
-                ks[k] = aes.encrypt<NR>(make_uint4(p.n0, p.n1, p.n2, bswap32(c0 + 4 * k)), rk);
+                ks[k] = aes.encrypt<NR>(make_uint4(m0, m1, m2, bswap32(c0 + 4 * k)), rk);
             });
         }
         // payload loads after the keystream: held across the AES pipeline they cost 16 VGPRs at its peak (spills at
         // 128); the other 3 waves of the SIMD cover their latency
-        uint4 in[NB];
+        uint4 in[NBG];
         if (inner) {
-            const uint8_t *b = pay + 16 * (t0 - 1);
+            const uint32_t b = pay + 16 * (uint32_t)(t0 - 1);
 #pragma unroll
-            for (int k = 0; k < NB; k++) in[k] = ld16(b + 64 * k);
+            for (int k = 0; k < NBG; k++) in[k] = ld16(at(b + 64 * k));
         } else {
 #pragma unroll
-            for (int k = 0; k < NB; k++) {
+            for (int k = 0; k < NBG; k++) {
                 const int j = t0 + 4 * k - 1;
-                in[k] = ld16(pay + (j >= 0 && 16 * j <= len ? 16 * j : 0));
+                in[k] = ld16(at(pay + (j >= 0 && 16 * j <= (int)len ? 16 * (uint32_t)j : 0u)));
             }
         }
-        uint4 out[NB];
+        uint4 out[NBG];
 #pragma unroll
-        for (int k = 0; k < NB; k++) out[k] = in[k] ^ ks[k];
-        if (g == 0) {  // uniform
-            ek0 = ks[0];  // lane 0: slot 0 = J0
-            if constexpr (SEAL) {
-                // header-protection sample = ciphertext bytes [4 - pn_len, 20 - pn_len) (payload.rs:151-169): blocks 0 and
-                // 1 are slots 1 and 2, i.e. lanes 1 and 2 at k = 0; lane 0 takes them (packets whose sample reaches into
-                // the tag re-read it at the end)
-                const uint4 o1 = qperm<kQuadBcast1>(out[0]), o2 = qperm<kQuadBcast2>(out[0]);
-                const uint32_t sh = (4u - p.pn_len) & 3u;
-                smp = make_uint4(__builtin_amdgcn_alignbyte(o1.y, o1.x, sh), __builtin_amdgcn_alignbyte(o1.z, o1.y, sh),
-                                 __builtin_amdgcn_alignbyte(o1.w, o1.z, sh), __builtin_amdgcn_alignbyte(o2.x, o1.w, sh));
-            }
+        for (int k = 0; k < NBG; k++) out[k] = in[k] ^ ks[k];
+        if constexpr (SEAL) {
+            // E_K(J0) (slot 0, lane 0) waits in the tag's place until the tag is known (4 VGPRs fewer across the loop;
+            // opening needs the received tag there and recomputes E_K(J0) on the quad at the end instead)
+            if (g == 0 && has && s == 0) st16(at(pay + len), ks[0]);
         }
         if (inner) {
-            uint8_t *b = pay + 16 * (t0 - 1);
+            const uint32_t b = pay + 16 * (uint32_t)(t0 - 1);
 #pragma unroll
-            for (int k = 0; k < NB; k++) st16_nt(b + 64 * k, out[k]);
+            for (int k = 0; k < NBG; k++) st16_nt(at(b + 64 * k), out[k]);
 #pragma unroll
-            for (int k = 0; k < NB; k++) w = gh.mulx(w, SEAL ? out[k] : in[k]);
+            for (int k = 0; k < NBG; k++) w = gh.mulx(w, SEAL ? out[k] : in[k]);
         } else {
 #pragma unroll
-            for (int k = 0; k < NB; k++) {
+            for (int k = 0; k < NBG; k++) {
                 const int t = t0 + 4 * k, j = t - 1;
-                const bool full = t >= 1 && j < nfull, part = rem && j == nfull;
-                if (full) st16_nt(pay + 16 * j, out[k]);
-                if (part) st_bytes(pay + 16 * j, keep_bytes(out[k], (uint32_t)rem), (uint32_t)rem);
-                const uint4 x = SEAL ? out[k] : in[k];
-                if (full || part) w = gh.mulx(w, part ? keep_bytes(x, (uint32_t)rem) : x);
+                const bool full = t >= 1 && j < nfull, part = rem && j == nfull, lenslot = has && t == m + 1;
+                if (full) st16_nt(at(pay + 16 * (uint32_t)j), out[k]);
+                if (part) st_bytes(at(pay + 16 * (uint32_t)j), keep_bytes(out[k], (uint32_t)rem), (uint32_t)rem);
+                // the length block rides in the slot after the payload when the group reaches it
+                const uint4 x = lenslot ? lenblk() : part ? keep_bytes(SEAL ? out[k] : in[k], (uint32_t)rem)
+                                                        : (SEAL ? out[k] : in[k]);
+                if (full || part || lenslot) w = gh.mulx(w, x);
+                len_done = len_done || lenslot;
             }
         }
+    };
+    for (int g = 0; g + 1 < G; g++) group(std::integral_constant<int, 4>{}, g);
+    if (G > 0) {  // the last group with as few counter blocks per lane as its longest packet needs
+        if (tail_slots <= 12) group(std::integral_constant<int, 3>{}, G - 1);
+        else group(std::integral_constant<int, 4>{}, G - 1);
     }
-    // length block (slot m + 1): be64(aad bits) || be64(payload bits)
-    if (has && (((m + 1) & 3) == (int)s)) w = gh.mulx(w, make_uint4(0, bswap32(p.aad_len * 8), 0, bswap32(p.len * 8)));
+    if (!len_done && (((m + 1) & 3) == (int)s)) w = gh.mulx(w, lenblk());
     // this lane's chain times H^e, e = (m + 2) - its last slot; then the quad's sum
     const int t_last = (m + 1) - (((m + 1) - (int)s) & 3);
     const uint32_t e = (uint32_t)(m + 2 - t_last);  // 1..4 (a lane with no block has w = 0 and any e)
@@ -212,41 +282,57 @@ __device__ __forceinline__ void quad_packet(const AesLds &aes, const GhashT<true
     uint4 y = fin.prod(w, make_uint4(0, 0, 0, 0));
     y = y ^ qperm<kQuadSwap1>(y);
     y = y ^ qperm<kQuadSwap2>(y);
-    if (s != 0 || !has) return;
 
-    const uint4 tag = y ^ ek0;
     if constexpr (SEAL) {
+        if (has && s == 0) st16(at(pay + len), y ^ ld16(at(pay + len)));  // tag = GHASH ^ E_K(J0) (stashed at group 0)
         constexpr int HNR = NR == 10 ? 10 : 14;
-        const bool hp = (flags & (QPP_HP_MASK_OUT | QPP_HP_APPLY)) && p.pn_len >= 1 && p.pn_len <= 4 &&
-                        p.len >= 4 - p.pn_len;
-        st16(pay + p.len, tag);
-        int8_t st = QPP_OK;
-        if (flags & (QPP_HP_MASK_OUT | QPP_HP_APPLY)) {
-            if (!hp) {
-                st = QPP_DECODE_ERROR;
-            } else {
-                const uint32_t hdr_len = p.aad_len - p.pn_len;
-                HpPrefetch<HNR> hpk;
-                hpk.load(key->hp_rk, p.base, hdr_len, flags);
-                if (p.len < 20 - p.pn_len) {
-                    // the sample reaches into the tag: read ciphertext||tag back (other lanes of this wave stored the
-                    // blocks, this lane the tag: a wavefront fence orders them first)
-                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-                    smp = ld16(pay + 4 - p.pn_len);
+        const bool want_hp = (flags & (QPP_HP_MASK_OUT | QPP_HP_APPLY)) != 0;
+        const qpp_pkt dt = reload_desc(dptr);
+        const uint32_t pn_len = dt.pn_len;
+        const bool hp = want_hp && has && pn_len >= 1 && pn_len <= 4 && len >= 4 - pn_len;  // quad-uniform
+        if (hp) {
+            // header-protection sample = ciphertext||tag bytes [4 - pn_len, 20 - pn_len) (payload.rs:151-169), column s
+            // read back (the quad's lanes stored the blocks and lane 0 the tag: a wavefront fence orders them first;
+            // read back rather than kept in registers across the loop); the mask AES on the quad (aes_quad)
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            uint32_t col;
+            __builtin_memcpy(&col, at(pay + 4 - pn_len + 4 * s), 4);
+            const uint32_t m0 = aes_quad<HNR>(aes, key->hp_rk, col, s);
+            const uint32_t m1 = qperm<kQuadBcast1>(m0);  // column 1 (mask byte 4 is its byte 0)
+            if (s == 0) {
+                if (flags & QPP_HP_MASK_OUT) {
+                    uint8_t *mo = masks + 5 * (size_t)pkt_index;
+                    mo[0] = (uint8_t)m0; mo[1] = (uint8_t)(m0 >> 8); mo[2] = (uint8_t)(m0 >> 16);
+                    mo[3] = (uint8_t)(m0 >> 24); mo[4] = (uint8_t)m1;
                 }
-                hpk.finish(aes, smp, p.base, hdr_len, p.pn_len, masks + 5 * (size_t)pkt_index, flags);
+                const uint32_t hdr_len = aad_len - pn_len;
+                if (flags & QPP_HP_APPLY) hdr_apply(at(dt.off), hdr_len, pn_len, hdr_load(at(dt.off), hdr_len), m0, m1);
             }
         }
-        if (status) status[pkt_index] = st;
+        if (!has || s != 0) return;
+        if (status) status[pkt_index] = want_hp && !hp ? QPP_DECODE_ERROR : QPP_OK;
     } else {
-        const uint4 want = ld16(pay + p.len);
-        const uint4 diff = tag ^ want;
-        const bool ok = (diff.x | diff.y | diff.z | diff.w) == 0;  // all 16 bytes compared, no early exit
+        // E_K(J0) on the quad (column s in lane s; J0 = nonce || be32(1)), compared column by column with the received
+        // tag, the verdict OR-ed over the quad: all 16 bytes compared, no early exit
+        const qpp_pkt dt = reload_desc(dptr);
+        const uint32_t j0 = s == 0 ? key->iv[0]
+                          : s == 1 ? key->iv[1] ^ bswap32((uint32_t)(dt.pn >> 32))
+                          : s == 2 ? key->iv[2] ^ bswap32((uint32_t)dt.pn)
+                                   : bswap32(1u);
+        const uint32_t ek0 = aes_quad<NR>(aes, key->rk, j0, s);
+        uint32_t want;
+        __builtin_memcpy(&want, at(pay + len + 4 * s), 4);
+        const uint32_t ys = s == 0 ? y.x : s == 1 ? y.y : s == 2 ? y.z : y.w;
+        uint32_t diff = ys ^ ek0 ^ want;
+        diff |= qperm<kQuadSwap1>(diff);
+        diff |= qperm<kQuadSwap2>(diff);
+        if (!has || s != 0) return;
+        const bool ok = diff == 0;
         if (!ok) {
             // never release unauthenticated plaintext (the quad's other lanes stored it: order these stores after theirs)
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            for (int b = 0; b < nfull; b++) st16(pay + 16 * b, make_uint4(0, 0, 0, 0));
-            if (rem) st_bytes(pay + 16 * nfull, make_uint4(0, 0, 0, 0), (uint32_t)rem);
+            for (int b = 0; b < nfull; b++) st16(at(pay + 16 * b), make_uint4(0, 0, 0, 0));
+            if (rem) st_bytes(at(pay + 16 * nfull), make_uint4(0, 0, 0, 0), (uint32_t)rem);
         }
         status[pkt_index] = ok ? QPP_OK : QPP_DECRYPT_ERROR;
     }
@@ -290,9 +376,6 @@ __global__ __launch_bounds__(kQuadWG) void aes_gcm_quad_kernel(const DevKey *__r
         const DevKey *__restrict__ key = keys + w.key;
         __syncthreads();  // every wave is done with the previous segment's tables
         quad_tables(key);
-        uint32_t rk[4 * (NR + 1)];
-#pragma unroll
-        for (int r = 0; r < 4 * (NR + 1); r++) rk[r] = __builtin_amdgcn_readfirstlane(key->rk[r]);
         for (uint32_t t0 = lo; t0 < end; t0 += kQuadPkts) {
             const uint32_t t = t0 + q;
             const bool real = t < end;
@@ -303,7 +386,7 @@ __global__ __launch_bounds__(kQuadWG) void aes_gcm_quad_kernel(const DevKey *__r
                 if (status && s == 0) status[pi] = QPP_INTERNAL_ERROR;
                 has = false;
             }
-            quad_packet<NR, SEAL>(aes, gh, key, rk, has, d, pi, arena, masks, status, flags, s);
+            quad_packet<NR, SEAL>(aes, gh, key, has, d, descs + pi, pi, arena, masks, status, flags, s);
         }
         lo = end;
     }

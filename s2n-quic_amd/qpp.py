@@ -53,7 +53,7 @@ EXPORTS = [
     "qpp_stream_destroy", "qpp_stream_synchronize", "qpp_event_create", "qpp_event_destroy", "qpp_event_record",
     "qpp_event_elapsed_ms", "qpp_stream_wait_event", "qpp_unprotect_open_batch", "qpp_pn_truncate", "qpp_pn_expand",
     "qpp_key_new_batch", "qpp_txq_create", "qpp_txq_destroy", "qpp_txq_ring", "qpp_txq_push", "qpp_txq_flush",
-    "qpp_txq_create_async", "qpp_txq_flush_async", "qpp_txq_poll", "qpp_txq_wait", "qpp_txq_push_descs", "qpp_txq_set_coalesce",
+    "qpp_txq_create_async", "qpp_txq_flush_async", "qpp_txq_poll", "qpp_txq_wait", "qpp_txq_push_descs", "qpp_txq_set_coalesce", "qpp_txq_push_scatter",
     "qpp_txq_pending", "qpp_memcpy_d2d", "qpp_ctx_set_burst_max", "qpp_dc_key_new", "qpp_dc_seal", "qpp_dc_open",
     "qpp_dc_open_in_place", "qpp_ctx_key_slots", "qpp_key_new_pair", "qpp_key_update_batch", "qpp_initial_keys_pair",
     "qpp_header_key_new", "qpp_header_key_new_raw", "qpp_header_key_free", "qpp_header_key_slot",
@@ -145,6 +145,7 @@ def lib():
             "qpp_txq_poll": (ctypes.c_int, [vp, u64, ctypes.POINTER(ctypes.c_int)]),
             "qpp_txq_wait": (ctypes.c_int, [vp, u64]),
             "qpp_txq_push_descs": (ctypes.c_int, [vp, vp, sz]),
+            "qpp_txq_push_scatter": (ctypes.c_int, [vp, vp, u64, sz, sz, sz, sz, vp, sz]),
             "qpp_txq_set_coalesce": (ctypes.c_int, [vp, sz]),
             "qpp_txq_pending": (sz, [vp]),
             "qpp_memcpy_d2d": (ctypes.c_int, [vp, vp, vp, sz, vp]),
@@ -666,6 +667,14 @@ class TxQueue:
         rc = lib().qpp_txq_flush(self.handle)
         if rc != OK:
             raise QppError(rc, "qpp_txq_flush")
+
+    def push_scatter(self, key, pn, off, header_len, pn_len, inline_len, extra=b""):
+        """qpp_txq_push_scatter: the inline plaintext is in the ring; `extra` (scatter::Buffer's tail) is copied after it"""
+        buf = (ctypes.c_uint8 * max(1, len(extra))).from_buffer_copy(bytes(extra) or b"\0")
+        rc = lib().qpp_txq_push_scatter(self.handle, key.handle, pn, off, header_len, pn_len, inline_len,
+                                        ctypes.cast(buf, vp) if extra else None, len(extra))
+        if rc != OK:
+            raise QppError(rc, "qpp_txq_push_scatter")
 
     def push_descs(self, descs):
         """qpp_txq_push_descs: a PKT_DTYPE array of ready descriptors in one call"""

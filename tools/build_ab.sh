@@ -7,7 +7,7 @@ src=$root/s2n-quic_amd/csrc
 out=$root/ab; tmp=$(mktemp -d)
 mkdir -p $out
 pids=()
-for f in aes_gcm.hip burst.hip chacha.hip plan.hip keysched.hip fips.hip api.cpp kdf.cpp; do
+for f in aes_gcm.hip quad.hip burst.hip chacha.hip plan.hip keysched.hip fips.hip api.cpp kdf.cpp; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -Wno-unused-value --offload-arch=gfx950 -munsafe-fp-atomics "$@" -c $src/$f -o $tmp/${f%.*}.o &
   pids+=($!)
 done

@@ -238,6 +238,8 @@ typedef struct qpp_pkt {
 #define QPP_HP_APPLY 0x2u      /* apply the mask to the header in place (header_crypto.rs:80-95) */
 #define QPP_ONLY_AES 0x10u     /* hint: every key in the batch is an AES-GCM key */
 #define QPP_ONLY_CHACHA 0x20u  /* hint: every key in the batch is ChaCha20-Poly1305 */
+#define QPP_KEY_BY_CONN 0x40u  /* host batches: qpp_pkt.key_idx is a connection index into the table of
+                                  qpp_ctx_set_conn_keys, resolved to the connection's current key on the device */
 
 /* Seal n packets: all pointers are device pointers (descs, arena, masks, status); masks may be NULL
  * unless QPP_HP_MASK_OUT; status may be NULL (per-packet QPP_OK / QPP_DECODE_ERROR when the HP sample
@@ -275,6 +277,12 @@ int qpp_host_batch_wait(qpp_ctx *ctx, uint64_t ticket);
  * them, and each batch cut into ~16 chunks of 64 Ki-256 Ki packets (at least 64 per live AES key); setting a geometry
  * fixes the chunk size.  Waits for the device. */
 int qpp_ctx_set_host_pipe(qpp_ctx *ctx, size_t chunk_packets, size_t chunk_bytes, size_t slots);
+/* The connection -> key slot table of QPP_KEY_BY_CONN host batches (the transport's KeySets,
+ * crypto/application/keyset.rs: a key update replaces the key behind a connection's entry, not the packets queued
+ * for it).  slots[c] = qpp_key_slot of connection c's current packet key.  Stream-ordered on the host pipeline:
+ * batches submitted before the call resolve through the previous table, later ones through this one; the caller's
+ * array may be reused on return. */
+int qpp_ctx_set_conn_keys(qpp_ctx *ctx, const uint32_t *slots, size_t n);
 
 /* ------------------------------------------------------------------ deferred transmit queue */
 
@@ -291,6 +299,23 @@ int qpp_txq_create(qpp_ctx *ctx, size_t ring_bytes, size_t max_packets, qpp_txq 
  * packet belong to the engine until its ticket completes (the transport encodes the next bursts elsewhere in the
  * ring).  qpp_txq_create(..) = in_flight 1. */
 int qpp_txq_create_async(qpp_ctx *ctx, size_t ring_bytes, size_t max_packets, size_t in_flight, qpp_txq **out);
+/* The same queue (one flush in flight) served by a PERSISTENT kernel: the transport's queue.flush() posts the
+ * flush through a doorbell word in pinned host memory instead of launching kernels, and qpp_txq_wait spins on a
+ * completion word the kernel writes back into the same page (no launch, no runtime call, no interrupt per flush).
+ * The server keeps the AES tables and the last key's GHASH tables in LDS between flushes; it occupies a few CUs
+ * (QPP_TXQ_SERVER_WGS, default 16; full-chip batch kernels of the context size their grids around them).  A flush
+ * after a quarter of QPP_TXQ_SERVER_IDLE_MS (default 200) without one restarts it first (one launch); the kernel itself
+ * leaves after the whole idle time (a host that went away).  Flushes with a
+ * ChaCha20-Poly1305 packet, or while a FIPS key is live, take the launched path of qpp_txq_create (same results).
+ * Replaces the per-flush launch behind quic/s2n-quic-platform/src/socket/io/tx.rs:204-268. */
+int qpp_txq_create_persistent(qpp_ctx *ctx, size_t ring_bytes, size_t max_packets, qpp_txq **out);
+/* Flushes sealed by the persistent server / by launched kernels, and server launches so far (any queue). */
+int qpp_txq_info(const qpp_txq *q, uint64_t *server_flushes, uint64_t *launched_flushes, uint64_t *server_starts);
+/* Persistent queue: microseconds from the server seeing the last posted flush's doorbell to its completion word. */
+int qpp_txq_server_time(const qpp_txq *q, double *us);
+/* Diagnostics: the server's clock (100 MHz) at the last flush's doorbell, workgroup 0's phase stamps (a build with
+ * QPP_TXS_TRACE, else 0) and its completion word. */
+int qpp_txq_server_stamps(const qpp_txq *q, uint64_t out[6]);
 void qpp_txq_destroy(qpp_txq *q);
 /* Host pointer to the ring (ring_bytes, pinned). */
 uint8_t *qpp_txq_ring(qpp_txq *q);

@@ -136,11 +136,7 @@ __device__ __forceinline__ void process_packet(const AesLds &aes, const GH &gh, 
         const uint32_t c = (uint32_t)(NB * g + 1);  // counter of slot 0 (wave-uniform)
         if (((c + NB - 1) >> 8) == (c >> 8)) {
             if ((c >> 8) != pg.page) pg.build(aes, rk, p.n0, p.n1, p.n2, c >> 8);
-#ifdef QPP_AES_NOPIPE
-            ctr_keystream<NR, NB>(aes, pg, rk, c, ks);
-#else
             ctr_keystream_pipe<NR, NB>(aes, pg, rk, c, ks);  // +3-4 % over the scheduler's own order
-#endif
         } else {  // straddles a page boundary: plain rounds (unrolled: a runtime index into ks[] would make the
                   // compiler move the array to LDS, on top of the 160 KiB the launch reserves)
             static_for<NB>([&](auto jc) {
@@ -239,118 +235,10 @@ __device__ __forceinline__ void process_packet(const AesLds &aes, const GH &gh, 
     }
 }
 
-// One workgroup per CU (grid = CUs), each with an equal slice of the key-sorted packet list (perm): the slice may
-// cross key boundaries, and the workgroup rebuilds its tables per key segment.  Fixed per-key work items instead made
-// every key's remainder a workgroup of its own: 64 keys x ~16 Ki packets were 1088 items of <= 1024 on 256 CUs, and
-// the last quarter round ran alone.  meta (plan_scan): {items, AES-128 items, AES-128 packets, AES-256 packets};
-// work[] holds one item per key (begin = its first perm index), AES-128 keys first.
-template <bool SEAL, int NB, int WG, int NR>
-// single: a context with one live AES key (its slot; meta, perm and work unused): descs[0, n_single) in slices
-// without a plan, packets of any other slot refused.
-__global__ __launch_bounds__(WG) void aes_gcm_kernel(const DevKey *__restrict__ keys, const qpp_pkt *__restrict__ descs,
-                                                    const uint32_t *__restrict__ perm, const WorkItem *__restrict__ work,
-                                                    const uint32_t *__restrict__ meta, uint8_t *__restrict__ arena,
-                                                    uint8_t *masks, int8_t *status, uint32_t flags, uint32_t single,
-                                                    uint32_t n_single) {
-    // dynamic LDS (tables + this variant's staging, reserved by the launch), addressed by offset (lds_ld32 / lds_ld128)
-    const bool one = single != 0xffffffffu;  // uniform
-    uint32_t i_lo = 0, i_hi = 1, p0 = 0, n = n_single;
-    if (!one) {
-        const uint32_t items = meta[0], i10 = meta[1], n10 = meta[2], n14 = meta[3];
-        i_lo = NR == 10 ? 0 : i10;
-        i_hi = NR == 10 ? i10 : items;
-        p0 = NR == 10 ? 0 : n10;
-        n = NR == 10 ? n10 : n14;
-    }
-    const uint32_t P = ((n + gridDim.x - 1) / gridDim.x + 63u) & ~63u;  // whole waves per slice
-    uint32_t lo = p0 + min(n, blockIdx.x * P);
-    const uint32_t hi = p0 + min(n, (blockIdx.x + 1) * P);
-    if (lo >= hi) return;  // uniform
-    uint32_t i = i_lo, j = i_hi;  // the item holding lo: largest i with work[i].begin <= lo
-    while (!one && j - i > 1) {
-        const uint32_t m = (i + j) >> 1;
-        if (work[m].begin <= lo) i = m; else j = m;
-    }
-    const AesLds aes = make_aes(kLdsAes);
-    const GhashT<true> gh = GhashT<true>::make();
-    Stage<NB> st;
-    st.lane = threadIdx.x & 63u;
-    st.base = kLdsStage + (threadIdx.x >> 6) * (64u * 16u * NB);
-    for (; lo < hi; i++) {  // key segments of the slice
-        const WorkItem w = one ? WorkItem{single, 0u, n, (uint32_t)NR} : work[i];
-        const uint32_t end = min(hi, w.begin + w.count);
-        const DevKey *__restrict__ key = keys + w.key;
-        __syncthreads();  // every wave is done with the previous segment's tables
-        build_tables(key);
-        // packet round keys in SGPRs for the whole segment (uniform: one key per workgroup)
-        uint32_t rk[4 * (NR + 1)];
-#pragma unroll
-        for (int r = 0; r < 4 * (NR + 1); r++) rk[r] = __builtin_amdgcn_readfirstlane(key->rk[r]);
-        for (uint32_t t0 = lo; t0 < end; t0 += WG) {
-            const uint32_t t = t0 + threadIdx.x;
-            const bool real = t < end;
-            const uint32_t pi = one ? (real ? t : lo) : perm[real ? t : lo];
-            const qpp_pkt d = descs[pi];  // (any valid descriptor for helper lanes)
-            bool has = real && !(d.flags & QPP_PKT_SKIP);
-            if (one && has && d.key_idx != single) {  // not the live key: refused, untouched
-                if (status) status[pi] = QPP_INTERNAL_ERROR;
-                has = false;
-            }
-            process_packet<NR, NB, SEAL>(aes, gh, st, key, rk, has, d, pi, arena, masks, status, flags);
-        }
-        lo = end;
-    }
-}
-
-// Fused receive path (unprotect -> PN expand -> open in ONE launch) for a context whose only live
-// packet key is the AES key `single` (one connection, or a server process per key; the plan-free case of
-// aes_gcm_kernel): each lane removes its packet's header protection, expands the PN and picks the key by the phase bit
-// (rx_unprotect_one, as unprotect_kernel does), writes the qpp_pkt the two-launch path would have written, and opens
-// the packet with the workgroup's tables.  Packets whose chosen key is not `single` are refused (INTERNAL_ERROR) as
-// the plan-free open refuses them.  Saves the separate unprotect launch (its own AES table build per 1024 packets) and
-// the re-read of the descriptors.  Outputs (arena, descs_out, status) equal the two-launch path's bit for bit
-// (tests/test_gpu_rx_fused.py).
-template <int NB, int WG, int NR>
-__global__ __launch_bounds__(WG) void aes_gcm_rx_kernel(const DevKey *__restrict__ keys, uint32_t key_cap,
-                                                       const qpp_rx_pkt *__restrict__ rx, uint32_t n, uint32_t single,
-                                                       uint8_t *__restrict__ arena, qpp_pkt *__restrict__ descs_out,
-                                                       int8_t *status) {
-    const uint32_t P = ((n + gridDim.x - 1) / gridDim.x + 63u) & ~63u;  // whole waves per slice
-    const uint32_t lo = min(n, blockIdx.x * P), hi = min(n, (blockIdx.x + 1) * P);
-    if (lo >= hi) return;  // uniform
-    const AesLds aes = make_aes(kLdsAes);
-    const GhashT<true> gh = GhashT<true>::make();
-    Stage<NB> st;
-    st.lane = threadIdx.x & 63u;
-    st.base = kLdsStage + (threadIdx.x >> 6) * (64u * 16u * NB);
-    const DevKey *__restrict__ key = keys + single;
-    build_tables(key);
-    uint32_t rk[4 * (NR + 1)];
-#pragma unroll
-    for (int r = 0; r < 4 * (NR + 1); r++) rk[r] = __builtin_amdgcn_readfirstlane(key->rk[r]);
-    for (uint32_t t0 = lo; t0 < hi; t0 += WG) {
-        const uint32_t t = t0 + threadIdx.x;
-        const bool real = t < hi;
-        const uint32_t pi = real ? t : lo;
-        qpp_pkt d{};  // helper lanes: an empty packet at offset 0 (only its pointer arithmetic is used)
-        bool has = false;
-        if (real) {
-            d = rx_unprotect_one(aes, keys, key_cap, rx[pi], arena, status, pi);
-            descs_out[pi] = d;
-            has = !(d.flags & QPP_PKT_SKIP);
-            if (has && d.key_idx != single) {  // the phase's key is not the live one: refused, payload untouched
-                status[pi] = QPP_INTERNAL_ERROR;
-                has = false;
-            }
-        }
-        process_packet<NR, NB, false>(aes, gh, st, key, rk, has, d, pi, arena, nullptr, status, 0u);
-    }
-}
-
 // Many keys, few packets per key (key churn, a chunk of a host batch): work items of <= 64 packets of one key (a
 // wave), each wave with its own key's Ghash4 tables and round keys, the AES T-tables shared by the workgroup.  A
 // workgroup loops over items (grid-stride over waves), so every lane has a packet whenever its key has >= 64 packets
-// in the batch (aes_gcm_kernel needs 1024 per workgroup).
+// in the batch (aes_gcm_quad_kernel wants ~1024 per workgroup: its tables are rebuilt per key segment).
 template <bool SEAL, int NB, int NR>
 __global__ __launch_bounds__(512) void aes_gcm_wave_kernel(const DevKey *__restrict__ keys,
                                                            const qpp_pkt *__restrict__ descs,
@@ -452,93 +340,14 @@ hipError_t launch_key_install(DevKey *keys, const uint32_t *slots, const DevKey 
     return launch_pow_setup(keys, slots, count, pow, s);
 }
 
-namespace {
-// (blocks per lane-iteration NB, workgroup size WG) variants; QPP_AES_VARIANT=<index> selects one (tuning knob,
-// DESIGN.md §4).  One workgroup per CU (tables + staging fill the 160 KiB LDS), so WG = waves per CU x 64.
-struct Variant {
-    int nb, wg;
-};
-constexpr Variant kVariants[] = {{4, 512}, {2, 1024}, {2, 512}, {4, 256}, {2, 768}};
-constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
-constexpr uint32_t lds_bytes(int nb, int wg) {
-    return kLdsStage + (uint32_t)(wg / 64) * 1024u * (uint32_t)nb;
-}
-
-template <bool SEAL, int NR>
-void launch_variant(int v, dim3 grid, hipStream_t s, const DevKey *keys, const qpp_pkt *descs, const PlanBuffers &pb,
-                    uint8_t *arena, uint8_t *masks, int8_t *status, uint32_t flags, uint32_t single = 0xffffffffu,
-                    uint32_t n_single = 0) {
-#define QPP_AES_LAUNCH(NB, WG)                                                                                    \
-    static_assert(lds_bytes(NB, WG) <= kLdsMax, "LDS budget");                                                 \
-    hipLaunchKernelGGL((aes_gcm_kernel<SEAL, NB, WG, NR>), grid, dim3(WG), lds_bytes(NB, WG), s, keys, descs,   \
-                       pb.perm, pb.work, pb.n_work, arena, masks, status, flags, single, n_single)
-    switch (v) {
-        case 1: { QPP_AES_LAUNCH(2, 1024); break; }
-        case 2: { QPP_AES_LAUNCH(2, 512); break; }
-        case 3: { QPP_AES_LAUNCH(4, 256); break; }
-        case 4: { QPP_AES_LAUNCH(2, 768); break; }
-        default: { QPP_AES_LAUNCH(4, 512); break; }
-    }
-#undef QPP_AES_LAUNCH
-}
-
-// QPP_AES_LAYOUT=lane: the lane-per-packet kernel instead of the quad layout (quad.hip) for the throughput path
-bool aes_layout_quad() {
-    static const bool q = [] {
-        const char *e = getenv("QPP_AES_LAYOUT");
-        return !(e && !strcmp(e, "lane"));
-    }();
-    return q;
-}
-
-int aes_variant() {
-    static int v = [] {
-        const char *e = getenv("QPP_AES_VARIANT");
-        int x = e ? atoi(e) : kDefaultAesVariant;
-        return (x >= 0 && x < kNumVariants) ? x : kDefaultAesVariant;
-    }();
-    return v;
-}
-}  // namespace
-
 hipError_t launch_aes_gcm_single(bool seal, const DevKey *keys, const qpp_pkt *descs, uint32_t slot, uint32_t nr,
                                  uint32_t n, uint32_t n_cu, uint8_t *arena, uint8_t *masks, int8_t *status,
                                  uint32_t flags, hipStream_t s) {
     if (!n) return hipSuccess;
     const PlanBuffers none{};
-    if (aes_layout_quad()) {
-        const uint32_t quads_waves = (n + 15) / 16;
-        return launch_aes_gcm_quad(seal, nr, dim3(quads_waves < n_cu ? quads_waves : n_cu), s, keys, descs, none, arena,
-                                   masks, status, flags, slot, n);
-    }
-    const uint32_t waves = (n + 63) / 64;
-    const dim3 grid(waves < n_cu ? waves : n_cu);
-    const int v = aes_variant();
-    if (nr == 10) {
-        if (seal) launch_variant<true, 10>(v, grid, s, keys, descs, none, arena, masks, status, flags, slot, n);
-        else launch_variant<false, 10>(v, grid, s, keys, descs, none, arena, masks, status, flags, slot, n);
-    } else {
-        if (seal) launch_variant<true, 14>(v, grid, s, keys, descs, none, arena, masks, status, flags, slot, n);
-        else launch_variant<false, 14>(v, grid, s, keys, descs, none, arena, masks, status, flags, slot, n);
-    }
-    return hipGetLastError();
-}
-
-hipError_t launch_aes_gcm_rx(const DevKey *keys, uint32_t key_cap, const qpp_rx_pkt *rx, uint32_t n, uint32_t slot,
-                             uint32_t nr, uint32_t n_cu, uint8_t *arena, qpp_pkt *descs_out, int8_t *status,
-                             hipStream_t s) {
-    if (!n) return hipSuccess;
-    const uint32_t waves = (n + 63) / 64;
-    const dim3 grid(waves < n_cu ? waves : n_cu);
-    constexpr uint32_t lds = lds_bytes(4, 512);
-    static_assert(lds <= kLdsMax, "LDS budget");
-    if (nr == 10)
-        hipLaunchKernelGGL((aes_gcm_rx_kernel<4, 512, 10>), grid, dim3(512), lds, s, keys, key_cap, rx, n, slot, arena,
-                           descs_out, status);
-    else
-        hipLaunchKernelGGL((aes_gcm_rx_kernel<4, 512, 14>), grid, dim3(512), lds, s, keys, key_cap, rx, n, slot, arena,
-                           descs_out, status);
-    return hipGetLastError();
+    const uint32_t waves = (n + 15) / 16;  // quad layout: 16 packets per wave
+    return launch_aes_gcm_quad(seal, nr, dim3(waves < n_cu ? waves : n_cu), s, keys, descs, none, arena, masks, status,
+                               flags, slot, n);
 }
 
 hipError_t launch_aes_gcm_wave(bool seal, const DevKey *keys, const qpp_pkt *descs, const PlanBuffers &pb, uint32_t n,
@@ -570,27 +379,13 @@ hipError_t launch_aes_gcm(bool seal, const DevKey *keys, const qpp_pkt *descs, c
                           uint32_t n_cu, uint8_t *arena, uint8_t *masks, int8_t *status, uint32_t flags,
                           uint32_t suites, hipStream_t s) {
     if (!n) return hipSuccess;
-    if (aes_layout_quad()) {
-        const uint32_t waves = (n + 15) / 16;
-        const dim3 grid(waves < n_cu ? waves : n_cu);
-        if (suites & (1u << QPP_SUITE_TLS_AES_128_GCM_SHA256))
-            launch_aes_gcm_quad(seal, 10, grid, s, keys, descs, pb, arena, masks, status, flags, 0xffffffffu, 0);
-        if (suites & (1u << QPP_SUITE_TLS_AES_256_GCM_SHA384))
-            launch_aes_gcm_quad(seal, 14, grid, s, keys, descs, pb, arena, masks, status, flags, 0xffffffffu, 0);
-        return hipGetLastError();
-    }
-    // one slice per CU; a batch smaller than a wave per CU takes fewer workgroups
-    const uint32_t waves = (n + 63) / 64;
+    // one slice per CU (quad.hip); a batch smaller than a wave per CU takes fewer workgroups
+    const uint32_t waves = (n + 15) / 16;
     const dim3 grid(waves < n_cu ? waves : n_cu);
-    const int v = aes_variant();
-    if (suites & (1u << QPP_SUITE_TLS_AES_128_GCM_SHA256)) {
-        if (seal) launch_variant<true, 10>(v, grid, s, keys, descs, pb, arena, masks, status, flags);
-        else launch_variant<false, 10>(v, grid, s, keys, descs, pb, arena, masks, status, flags);
-    }
-    if (suites & (1u << QPP_SUITE_TLS_AES_256_GCM_SHA384)) {
-        if (seal) launch_variant<true, 14>(v, grid, s, keys, descs, pb, arena, masks, status, flags);
-        else launch_variant<false, 14>(v, grid, s, keys, descs, pb, arena, masks, status, flags);
-    }
+    if (suites & (1u << QPP_SUITE_TLS_AES_128_GCM_SHA256))
+        launch_aes_gcm_quad(seal, 10, grid, s, keys, descs, pb, arena, masks, status, flags, 0xffffffffu, 0);
+    if (suites & (1u << QPP_SUITE_TLS_AES_256_GCM_SHA384))
+        launch_aes_gcm_quad(seal, 14, grid, s, keys, descs, pb, arena, masks, status, flags, 0xffffffffu, 0);
     return hipGetLastError();
 }
 

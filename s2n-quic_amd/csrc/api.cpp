@@ -19,6 +19,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <deque>
 #include <map>
 #include <string>
@@ -42,6 +43,16 @@ struct StreamState {
     size_t fips_bytes = 0;
     uint32_t fips_n_cap = 0;
     uint32_t *fips_refused = nullptr;  // device word: packets the gate refused (txq flushes report it)
+    uint32_t *rx_scratch = nullptr;    // fused receive kernel (quad.hip): barrier, per-key counts / cursors, work items
+    uint32_t rx_scratch_keys = 0;      // the key_cap it is sized for
+};
+
+struct KStage {
+    uint8_t *h = nullptr, *d = nullptr;
+    size_t cap = 0;
+    size_t pending = 0;          // bytes of key records / secrets in h, zeroized once the job's copy is done
+    hipEvent_t free_ev = nullptr;  // recorded on the key stream after the last job that reads this stage
+    bool used = false;
 };
 
 struct Retired {
@@ -116,9 +127,14 @@ struct qpp_ctx {
     uint8_t *d_stage = nullptr, *h_stage = nullptr;
     uint8_t *v_stage = nullptr;  // device view of the pinned h_stage (zero-copy per-packet calls)
     size_t stage_cap = 0;
-    uint8_t *h_kstage = nullptr, *d_kstage = nullptr;
-    size_t kstage_cap = 0, kstage_pending = 0;
+    // two pinned key stages (+ device twins), used alternately by the key-stream jobs (installs, derivations): a
+    // job waits only for the previous job of ITS stage (an event), never for the key stream as a whole
+    KStage kstage[2];
+    int kstage_next = 0;
     HostPipe *pipe = nullptr;
+    std::vector<qpp_txq *> servers;  // transmit queues with a persistent server kernel (qpp_txq_create_persistent)
+    uint32_t *d_connmap = nullptr;    // qpp_ctx_set_conn_keys: connection -> key slot (device)
+    size_t connmap_cap = 0, connmap_n = 0;
     std::string last_error;
 };
 
@@ -159,6 +175,18 @@ bool fail(qpp_ctx *ctx, hipError_t e, const char *what) {
         if (rc_) return rc_;  \
     } while (0)
 
+// Persistent transmit-queue servers (defined with qpp_txq below).  A server kernel never ends on its own while
+// flushes keep coming, so every device-wide wait first stops them (servers_stop), and key retirement first waits
+// for their flushes in flight (servers_quiesce).
+int servers_stop(qpp_ctx *ctx);
+int servers_quiesce(qpp_ctx *ctx);
+uint32_t servers_cu(const qpp_ctx *ctx);
+// CUs a full-chip kernel (one workgroup per CU) should size its grid for: those of running servers are taken
+uint32_t cu_avail(const qpp_ctx *ctx) {
+    const uint32_t r = servers_cu(ctx);
+    return ctx->n_cu > r ? ctx->n_cu - r : 1u;
+}
+
 bool valid_suite(int s) {
     return s == QPP_SUITE_TLS_AES_128_GCM_SHA256 || s == QPP_SUITE_TLS_AES_256_GCM_SHA384 ||
            s == QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256;
@@ -188,6 +216,7 @@ void free_stream_state(StreamState *st) {
     free_plan(st->plan);
     hipFree(st->fips_buf);
     hipFree(st->fips_refused);
+    hipFree(st->rx_scratch);
     if (st->last) hipEventDestroy(st->last);
     delete st;
 }
@@ -234,6 +263,7 @@ int grow_keys(qpp_ctx *ctx, uint32_t need) {
     uint32_t cap = std::max<uint32_t>(64, ctx->key_cap);
     while (cap < need) cap *= 2;
     DevKey *nk = nullptr;
+    RC_TRY(servers_stop(ctx));  // they hold the old table's address
     HIP_TRY(ctx, hipDeviceSynchronize());  // no batch may still read the old table
     HIP_TRY(ctx, hipMalloc(&nk, sizeof(DevKey) * cap));
     // Stream-ordered and waited for: a plain hipMemset runs on the null stream, which does not order against the
@@ -268,19 +298,37 @@ int grow_keys(qpp_ctx *ctx, uint32_t need) {
     return QPP_OK;
 }
 
-int ensure_kstage(qpp_ctx *ctx, size_t bytes) {
-    if (bytes <= ctx->kstage_cap) return QPP_OK;
-    size_t cap = std::max<size_t>(1 << 16, ctx->kstage_cap);
-    while (cap < bytes) cap *= 2;
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->kstream));
-    if (ctx->d_kstage) hipFree(ctx->d_kstage);
-    if (ctx->h_kstage) { secure_zero(ctx->h_kstage, ctx->kstage_cap); hipHostFree(ctx->h_kstage); }
-    ctx->d_kstage = nullptr;
-    ctx->h_kstage = nullptr;
-    ctx->kstage_cap = 0;
-    HIP_TRY(ctx, hipMalloc(&ctx->d_kstage, cap));
-    HIP_TRY(ctx, hipHostMalloc(&ctx->h_kstage, cap, hipHostMallocDefault));
-    ctx->kstage_cap = cap;
+// The key stage for the next key-stream job, with room for `bytes`: the stage the previous job did not use, once
+// ITS previous job has read it (host wait on that job's event only -- the other stage's job, e.g. the install that
+// flush_keys just queued, keeps running).  The caller records release_kstage after enqueueing its copies.
+int take_kstage(qpp_ctx *ctx, size_t bytes, KStage **out) {
+    KStage &k = ctx->kstage[ctx->kstage_next];
+    ctx->kstage_next ^= 1;
+    if (k.used) HIP_TRY(ctx, hipEventSynchronize(k.free_ev));
+    k.used = false;
+    if (k.pending) secure_zero(k.h, k.pending);
+    k.pending = 0;
+    if (!k.free_ev) HIP_TRY(ctx, hipEventCreateWithFlags(&k.free_ev, hipEventDisableTiming));
+    if (bytes > k.cap) {
+        size_t cap = std::max<size_t>(1 << 16, k.cap);
+        while (cap < bytes) cap *= 2;
+        if (k.d) hipFree(k.d);
+        if (k.h) { secure_zero(k.h, k.cap); hipHostFree(k.h); }
+        k.d = nullptr;
+        k.h = nullptr;
+        k.cap = 0;
+        HIP_TRY(ctx, hipMalloc(&k.d, cap));
+        HIP_TRY(ctx, hipHostMalloc(&k.h, cap, hipHostMallocDefault));
+        k.cap = cap;
+    }
+    *out = &k;
+    return QPP_OK;
+}
+// after the job's last read of the stage was enqueued on the key stream; `pending` bytes of h are zeroized later
+int release_kstage(qpp_ctx *ctx, KStage *k, size_t pending) {
+    HIP_TRY(ctx, hipEventRecord(k->free_ev, ctx->kstream));
+    k->used = true;
+    k->pending = pending;
     return QPP_OK;
 }
 
@@ -293,25 +341,22 @@ int flush_keys(qpp_ctx *ctx) {
     if (ctx->dirty.empty()) return QPP_OK;
     const uint32_t n = (uint32_t)ctx->dirty.size();
     const size_t rec = sizeof(DevKey) * n, slots = 4 * (size_t)n;
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->kstream));  // the pinned key stage of the previous flush is free again
-    if (ctx->kstage_pending) secure_zero(ctx->h_kstage, ctx->kstage_pending);
-    ctx->kstage_pending = 0;
-    RC_TRY(ensure_kstage(ctx, rec + slots));
+    KStage *k = nullptr;
+    RC_TRY(take_kstage(ctx, rec + slots, &k));
     for (uint32_t i = 0; i < n; i++) {
-        memcpy(ctx->h_kstage + sizeof(DevKey) * i, &ctx->h_keys[ctx->dirty[i]], sizeof(DevKey));
+        memcpy(k->h + sizeof(DevKey) * i, &ctx->h_keys[ctx->dirty[i]], sizeof(DevKey));
         ctx->dirty_flag[ctx->dirty[i]] = 0;
     }
-    memcpy(ctx->h_kstage + rec, ctx->dirty.data(), slots);
+    memcpy(k->h + rec, ctx->dirty.data(), slots);
     hipStream_t s = ctx->kstream;
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->d_kstage, ctx->h_kstage, rec + slots, hipMemcpyHostToDevice, s));
-    HIP_TRY(ctx, launch_key_install(ctx->d_keys, (const uint32_t *)(ctx->d_kstage + rec),
-                                    (const DevKey *)ctx->d_kstage, n, ctx->pow, s));
-    HIP_TRY(ctx, hipMemsetAsync(ctx->d_kstage, 0, rec, s));
+    HIP_TRY(ctx, hipMemcpyAsync(k->d, k->h, rec + slots, hipMemcpyHostToDevice, s));
+    HIP_TRY(ctx, launch_key_install(ctx->d_keys, (const uint32_t *)(k->d + rec), (const DevKey *)k->d, n, ctx->pow, s));
+    HIP_TRY(ctx, hipMemsetAsync(k->d, 0, rec, s));
     HIP_TRY(ctx, hipEventRecord(ctx->keys_ready, s));
     ctx->key_gen++;
     ctx->dirty.clear();
-    ctx->kstage_pending = rec;  // the pinned copy of the records is zeroized once the copy is done (next key call)
-    return QPP_OK;
+    // the pinned copy of the records is zeroized when the stage is next taken (its copy is done by then)
+    return release_kstage(ctx, k, rec);
 }
 
 void mark_dirty(qpp_ctx *ctx, uint32_t slot) {
@@ -425,6 +470,7 @@ int alloc_slot(qpp_ctx *ctx, uint32_t *out) {
 int flush_retire(qpp_ctx *ctx) {
     if (ctx->retire_pending.empty()) return QPP_OK;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
+    RC_TRY(servers_quiesce(ctx));  // a server flush in flight may still read the freed records
     for (StreamState *st : ctx->streams)
         if (st->used) HIP_TRY(ctx, hipStreamWaitEvent(ctx->rstream, st->last, 0));
     HIP_TRY(ctx, hipStreamWaitEvent(ctx->rstream, ctx->keys_ready, 0));  // behind the slots' own installs
@@ -541,10 +587,10 @@ hipError_t launch_aes(const qpp_ctx *ctx, AesPath p, bool seal, const qpp_pkt *d
             return launch_aes_gcm_burst(seal, ctx->d_keys, descs, pb, n, ctx->key_cap, per, arena, masks, status, flags,
                                         suite_mask(ctx), ctx->pow, s);
         case AesPath::wave:
-            return launch_aes_gcm_wave(seal, ctx->d_keys, descs, pb, n, ctx->key_cap, ctx->n_cu, arena, masks, status,
+            return launch_aes_gcm_wave(seal, ctx->d_keys, descs, pb, n, ctx->key_cap, cu_avail(ctx), arena, masks, status,
                                        flags, suite_mask(ctx), s);
         default:
-            return launch_aes_gcm(seal, ctx->d_keys, descs, pb, n, ctx->n_cu, arena, masks, status, flags,
+            return launch_aes_gcm(seal, ctx->d_keys, descs, pb, n, cu_avail(ctx), arena, masks, status, flags,
                                   suite_mask(ctx), s);
     }
 }
@@ -568,7 +614,7 @@ int enqueue_seal(qpp_ctx *ctx, StreamState *st, const qpp_pkt *descs, uint32_t n
         const AesPath path = aes_path(ctx, n);
         const uint32_t one = path == AesPath::lane ? single_aes_slot(ctx) : UINT32_MAX;
         if (one != UINT32_MAX) {
-            HIP_TRY(ctx, launch_aes_gcm_single(true, ctx->d_keys, descs, one, ctx->h_keys[one].nr, n, ctx->n_cu, arena,
+            HIP_TRY(ctx, launch_aes_gcm_single(true, ctx->d_keys, descs, one, ctx->h_keys[one].nr, n, cu_avail(ctx), arena,
                                                masks, status, flags, s));
         } else {
             RC_TRY(ensure_plan(ctx, st, n));
@@ -589,7 +635,7 @@ int enqueue_open(qpp_ctx *ctx, StreamState *st, const qpp_pkt *descs, uint32_t n
         const AesPath path = aes_path(ctx, n);
         const uint32_t one = path == AesPath::lane ? single_aes_slot(ctx) : UINT32_MAX;
         if (one != UINT32_MAX) {
-            HIP_TRY(ctx, launch_aes_gcm_single(false, ctx->d_keys, descs, one, ctx->h_keys[one].nr, n, ctx->n_cu, arena,
+            HIP_TRY(ctx, launch_aes_gcm_single(false, ctx->d_keys, descs, one, ctx->h_keys[one].nr, n, cu_avail(ctx), arena,
                                                nullptr, status, 0, s));
         } else {
             RC_TRY(ensure_plan(ctx, st, n));
@@ -701,12 +747,10 @@ int derive_batch(qpp_ctx *ctx, int suite, const uint8_t *secrets, const uint8_t 
                  qpp_key **out) {
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     RC_TRY(flush_keys(ctx));  // pending host records first
-    // The pinned key stage is reused below: the records that flush just queued are copied from it asynchronously, so
-    // wait for that copy before overwriting the stage (found by tests/test_gpu_fuzz.py: a key created just before a
-    // batched update was installed from the secrets written over its record -- a non-live slot, INTERNAL_ERROR).
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->kstream));
-    if (ctx->kstage_pending) secure_zero(ctx->h_kstage, ctx->kstage_pending);
-    ctx->kstage_pending = 0;
+    // (The records that flush just queued are copied from its key stage asynchronously; the derivation takes the
+    // OTHER stage -- take_kstage -- so it neither waits for that copy nor overwrites the records: overwriting them was
+    // found by tests/test_gpu_fuzz.py, a key created just before a batched update installed from the secrets written
+    // over its record.)
     std::vector<uint32_t> slots;
     slots.reserve(n);
     // a failure after slots were taken gives them back through retirement (the device may have written their records)
@@ -730,8 +774,9 @@ int derive_batch_device(qpp_ctx *ctx, int suite, const uint8_t *secrets, const u
     // key stage: secrets | hp_in | slots | material
     const size_t o_hp = n * hl, o_slot = o_hp + (hp_in ? n * kl : 0), o_mat = (o_slot + 4 * n + 15) & ~size_t(15);
     const size_t total = o_mat + n * mb;
-    RC_TRY(ensure_kstage(ctx, total));
-    uint8_t *h = ctx->h_kstage, *d = ctx->d_kstage;
+    KStage *ks = nullptr;
+    RC_TRY(take_kstage(ctx, total, &ks));
+    uint8_t *h = ks->h, *d = ks->d;
     memcpy(h, secrets, n * hl);
     if (hp_in) memcpy(h + o_hp, hp_in, n * kl);
     memcpy(h + o_slot, slots.data(), 4 * n);
@@ -743,6 +788,7 @@ int derive_batch_device(qpp_ctx *ctx, int suite, const uint8_t *secrets, const u
     HIP_TRY(ctx, hipMemsetAsync(d, 0, total, s));
     HIP_TRY(ctx, hipEventRecord(ctx->keys_ready, s));
     ctx->key_gen++;
+    RC_TRY(release_kstage(ctx, ks, 0));
     HIP_TRY(ctx, hipStreamSynchronize(s));  // the material comes back to the host handles
     const uint32_t nr = suite == QPP_SUITE_TLS_AES_128_GCM_SHA256 ? 10 : suite == QPP_SUITE_TLS_AES_256_GCM_SHA384 ? 14 : 0;
     for (size_t i = 0; i < n; i++) {
@@ -883,6 +929,7 @@ void qpp_ctx_destroy(qpp_ctx *ctx) {
     if (!ctx) return;
     hipSetDevice(ctx->device);
     if (ctx->d_keys) flush_retire(ctx);  // pending zeroizations, while the table and the stream states still exist
+    servers_stop(ctx);
     hipDeviceSynchronize();
     if (ctx->d_keys) {
         hipMemsetAsync(ctx->d_keys, 0, sizeof(DevKey) * ctx->key_cap, ctx->stream);
@@ -907,9 +954,13 @@ void qpp_ctx_destroy(qpp_ctx *ctx) {
         delete ctx->pipe;
     }
     hipFree(ctx->d_stage);
+    hipFree(ctx->d_connmap);
     if (ctx->h_stage) hipHostFree(ctx->h_stage);
-    hipFree(ctx->d_kstage);
-    if (ctx->h_kstage) { secure_zero(ctx->h_kstage, ctx->kstage_cap); hipHostFree(ctx->h_kstage); }
+    for (KStage &k : ctx->kstage) {
+        hipFree(k.d);
+        if (k.h) { secure_zero(k.h, k.cap); hipHostFree(k.h); }
+        if (k.free_ev) hipEventDestroy(k.free_ev);
+    }
     if (ctx->stream) hipStreamDestroy(ctx->stream);
     if (ctx->kstream) hipStreamDestroy(ctx->kstream);
     if (ctx->rstream) hipStreamDestroy(ctx->rstream);
@@ -923,6 +974,7 @@ void *qpp_ctx_stream(qpp_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr;
 int qpp_ctx_synchronize(qpp_ctx *ctx) {
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     RC_TRY(flush_retire(ctx));
+    RC_TRY(servers_stop(ctx));  // (restarted by the next flush of their queue)
     HIP_TRY(ctx, hipDeviceSynchronize());
     return QPP_OK;
 }
@@ -1324,16 +1376,28 @@ int qpp_unprotect_open_batch(qpp_ctx *ctx, const qpp_rx_pkt *rx, size_t n, uint8
     RC_TRY(flush_keys(ctx));
     StreamState *st = nullptr;
     RC_TRY(batch_stream(ctx, stream, &st));
-    // One live AES packet key and a lane-kernel batch: ONE fused launch (unprotect -> PN expand -> open; the same
-    // outputs).  QPP_RX_FUSED=0 forces the two-launch path (A/B, tests).
+    // Live packet keys all of ONE AES size (any number of them, any header-key suite) and a batch of the throughput
+    // kernel's size: ONE fused cooperative launch -- unprotect, group by the chosen key, open (quad.hip; the same
+    // outputs as the launches below).  QPP_RX_FUSED=0 forces the multi-launch path (A/B, tests).
     const char *fz = getenv("QPP_RX_FUSED");
-    const uint32_t one = !(flags & QPP_ONLY_CHACHA) && !(fz && fz[0] == '0') &&
-                                 aes_path(ctx, (uint32_t)n) == AesPath::lane
-                             ? single_aes_slot(ctx)
-                             : UINT32_MAX;
-    if (one != UINT32_MAX) {
-        HIP_TRY(ctx, launch_aes_gcm_rx(ctx->d_keys, ctx->key_cap, rx, (uint32_t)n, one, ctx->h_keys[one].nr, ctx->n_cu,
-                                       arena, descs_out, status, st->stream));
+    const uint32_t a128 = ctx->live_by_suite[QPP_SUITE_TLS_AES_128_GCM_SHA256],
+                   a256 = ctx->live_by_suite[QPP_SUITE_TLS_AES_256_GCM_SHA384];
+    if (!(flags & QPP_ONLY_CHACHA) && !(fz && fz[0] == '0') && !ctx->live_by_suite[QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256] &&
+        (a128 > 0) != (a256 > 0) && aes_path(ctx, (uint32_t)n) == AesPath::lane && ctx->key_cap <= quad_rx_max_keys()) {
+        RC_TRY(ensure_plan(ctx, st, (uint32_t)n));  // perm
+        const uint32_t kc = ctx->key_cap;
+        if (st->rx_scratch_keys < kc) {
+            HIP_TRY(ctx, hipStreamSynchronize(st->stream));  // the old scratch is no longer read
+            hipFree(st->rx_scratch);
+            st->rx_scratch = nullptr;
+            st->rx_scratch_keys = 0;
+            HIP_TRY(ctx, hipMalloc(&st->rx_scratch, 4 * (16 + 2 * (size_t)kc + 4 + 4 * ((size_t)kc + 1))));
+            st->rx_scratch_keys = kc;
+        }
+        HIP_TRY(ctx, hipMemsetAsync(st->rx_scratch, 0, 4 * (16 + 2 * (size_t)kc), st->stream));
+        const uint32_t grid = std::min<uint32_t>(cu_avail(ctx), std::max<uint32_t>(1, (uint32_t)((n + 191) / 192)));
+        HIP_TRY(ctx, launch_aes_gcm_quad_rx(a128 ? 10 : 14, grid, st->stream, ctx->d_keys, kc, rx, (uint32_t)n, arena,
+                                            descs_out, status, st->rx_scratch, st->plan.perm));
         return note_work(ctx, st);
     }
     // No AES record live at all (packet or header keys): every header and packet key a packet can name is ChaCha20,
@@ -1392,6 +1456,7 @@ int qpp_ctx_set_host_pipe(qpp_ctx *ctx, size_t chunk_packets, size_t chunk_bytes
     if (!ctx || !chunk_packets || chunk_packets > UINT32_MAX || chunk_bytes < 4096 || slots < 2 || slots > 16)
         return QPP_INTERNAL_ERROR;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
+    RC_TRY(servers_stop(ctx));
     HIP_TRY(ctx, hipDeviceSynchronize());
     if (!ctx->pipe) ctx->pipe = new HostPipe();
     pipe_release(ctx);
@@ -1411,6 +1476,9 @@ int qpp_host_batch_submit(qpp_ctx *ctx, const qpp_pkt *descs, size_t n, uint8_t 
     if ((ops & QPP_OP_SEAL) && n && !status && ctx->fips_live && !(flags & QPP_ONLY_CHACHA))
         return QPP_INTERNAL_ERROR;  // FIPS refusals are reported per packet (qpp_seal_batch)
     if ((ops & QPP_OP_SEAL) && (ops & QPP_OP_OPEN) && (flags & QPP_HP_APPLY)) return QPP_INTERNAL_ERROR;
+    const bool by_conn = (flags & QPP_KEY_BY_CONN) != 0;
+    if (by_conn && !ctx->connmap_n) return QPP_INTERNAL_ERROR;  // no connection table
+    flags &= ~QPP_KEY_BY_CONN;
     *ticket = 0;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     if (!ctx->pipe) ctx->pipe = new HostPipe();
@@ -1454,6 +1522,8 @@ int qpp_host_batch_submit(qpp_ctx *ctx, const qpp_pkt *descs, size_t n, uint8_t 
         HIP_TRY(ctx, hipMemcpyAsync(sl.descs, descs + first, sizeof(qpp_pkt) * cn, hipMemcpyHostToDevice, p->h2d));
         HIP_TRY(ctx, hipEventRecord(sl.h2d, p->h2d));
         HIP_TRY(ctx, hipStreamWaitEvent(p->comp, sl.h2d, 0));
+        if (by_conn)
+            HIP_TRY(ctx, launch_conn_remap(sl.descs, cn, ctx->d_connmap, (uint32_t)ctx->connmap_n, p->comp));
         uint8_t *base = sl.arena - lo;  // descriptor offsets stay absolute: the kernels address base + off
         if (ops & QPP_OP_SEAL)
             RC_TRY(enqueue_seal(ctx, st, sl.descs, cn, base, sl.masks, (ops & QPP_OP_OPEN) ? nullptr : sl.status,
@@ -1475,6 +1545,27 @@ int qpp_host_batch_submit(qpp_ctx *ctx, const qpp_pkt *descs, size_t n, uint8_t 
     HIP_TRY(ctx, hipEventRecord(done, p->d2h));
     *ticket = p->next_ticket++;
     p->tickets[*ticket] = done;
+    return QPP_OK;
+}
+
+int qpp_ctx_set_conn_keys(qpp_ctx *ctx, const uint32_t *slots, size_t n) {
+    if (!ctx || !n || !slots || n > UINT32_MAX) return QPP_INTERNAL_ERROR;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    if (!ctx->pipe) ctx->pipe = new HostPipe();
+    RC_TRY(pipe_init(ctx));
+    hipStream_t s = ctx->pipe->comp;  // the remap launches' stream: earlier batches read the old table first
+    if (n > ctx->connmap_cap) {
+        HIP_TRY(ctx, hipStreamSynchronize(s));
+        hipFree(ctx->d_connmap);
+        ctx->d_connmap = nullptr;
+        ctx->connmap_cap = ctx->connmap_n = 0;
+        const size_t cap = std::max<size_t>(n, 1024);
+        HIP_TRY(ctx, hipMalloc(&ctx->d_connmap, 4 * cap));
+        ctx->connmap_cap = cap;
+    }
+    // (a pageable source: the runtime has consumed it when the call returns)
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->d_connmap, slots, 4 * n, hipMemcpyHostToDevice, s));
+    ctx->connmap_n = n;
     return QPP_OK;
 }
 
@@ -1629,7 +1720,107 @@ struct qpp_txq {
     uint32_t zc_max = 0;
     std::vector<uint32_t> order;
     std::vector<std::pair<size_t, size_t>> runs;  // DMA path: the flush's contiguous packet byte ranges
+    // Persistent server (qpp_txq_create_persistent; burst.hip txq_server_kernel): flushes of AES packets are posted
+    // through a doorbell in pinned memory instead of launched.  One posted flush at a time: its plan (work items and
+    // key-sorted descriptors, pinned) is rewritten only once `done` shows the previous one sealed.
+    bool persistent = false;
+    TxsMail *h_mail = nullptr, *v_mail = nullptr;
+    TxsSync *d_sync = nullptr;
+    WorkItem *h_items = nullptr, *v_items = nullptr;
+    qpp_pkt *h_sdesc = nullptr, *v_sdesc = nullptr;
+    hipStream_t srv_stream = nullptr;
+    bool srv_running = false;           // launched and not yet seen to have ended
+    const DevKey *srv_keys = nullptr;   // the key table the running server reads
+    uint32_t srv_seq = 0;               // seq of the last doorbell word written (flush or stop)
+    uint32_t srv_posted = 0;            // seq of the last flush posted (0: none)
+    uint64_t srv_first = 0, srv_last = 0;  // its tickets
+    uint32_t srv_epoch = 0;             // key epoch of the doorbell (8 bits)
+    uint64_t srv_key_gen = ~0ull;       // ctx->key_gen the server's epoch stands for
+    uint32_t srv_wgs = 16, srv_idle_ticks = 0;
+    std::chrono::steady_clock::time_point srv_last_post{};  // the server may leave idle_ticks after it
+    std::chrono::microseconds srv_host_idle{0};             // a quarter of that: past it, restart before posting
+    uint64_t n_server = 0, n_launch = 0, n_starts = 0;  // flushes posted / launched; server launches
 };
+
+namespace {
+
+uint32_t srv_next(uint32_t s) { return s + 1u ? s + 1u : 1u; }  // 0 is never a flush's seq
+
+bool srv_alive(qpp_txq *q) {
+    if (!q->srv_running) return false;
+    if (hipStreamQuery(q->srv_stream) == hipErrorNotReady) return true;
+    q->srv_running = false;  // it ended on its own (idle timeout), or failed (the next launch reports that)
+    return false;
+}
+
+// Launches the server unless it runs.  A flush posted but not done (posted while the last server was leaving on its
+// idle timeout) is picked up by the new one: it starts with seq0 != the posted seq.
+int srv_start(qpp_txq *q) {
+    // (no stream query while the server is believed running: a server that left on its idle timeout is found by
+    // srv_wait's slow path, which relaunches it behind the posted flush)
+    if (q->srv_running) return QPP_OK;
+    qpp_ctx *ctx = q->ctx;
+    const bool pending = q->srv_posted && __atomic_load_n(&q->h_mail->done, __ATOMIC_ACQUIRE) != q->srv_posted;
+    const uint32_t seq0 = pending ? q->srv_posted - 1u : q->srv_seq;
+    HIP_TRY(ctx, hipMemsetAsync(q->d_sync, 0, sizeof(TxsSync), q->srv_stream));
+    HIP_TRY(ctx, launch_txq_server(ctx->d_keys, ctx->pow, q->v_mail, q->d_sync, q->v_items, q->v_sdesc, q->v_ring,
+                                   seq0, q->srv_idle_ticks, q->srv_wgs, q->srv_stream));
+    q->srv_running = true;
+    q->srv_keys = ctx->d_keys;
+    q->n_starts++;
+    return QPP_OK;
+}
+
+// Host wait for the flush with this seq (spinning on the pinned `done` word: no interrupt, no runtime call).
+int srv_wait(qpp_txq *q, uint32_t seq) {
+    if (!seq) return QPP_OK;
+    const volatile uint32_t *done = &q->h_mail->done;
+    std::chrono::steady_clock::time_point t0{};
+    for (uint64_t spin = 0;; spin++) {
+        if (*done == seq) {
+            __atomic_thread_fence(__ATOMIC_ACQUIRE);
+            return QPP_OK;
+        }
+        if ((spin & 4095u) == 4095u) {
+            if (!srv_alive(q)) RC_TRY(srv_start(q));  // it left (idle) before this flush was seen: a new one takes it
+            const auto now = std::chrono::steady_clock::now();
+            if (spin == 4095u) t0 = now;
+            else if (now - t0 > std::chrono::seconds(10)) {
+                q->ctx->last_error = "txq server: flush not completed within 10 s";
+                return QPP_DEVICE_ERROR;
+            }
+        }
+        __builtin_ia32_pause();
+    }
+}
+
+int srv_stop(qpp_txq *q) {
+    if (!q->srv_running) return QPP_OK;
+    RC_TRY(srv_wait(q, q->srv_posted));
+    if (!srv_alive(q)) return QPP_OK;
+    q->srv_seq = srv_next(q->srv_seq);
+    __atomic_store_n(&q->h_mail->doorbell, ((uint64_t)q->srv_seq << 32) | kTxsStop, __ATOMIC_RELEASE);
+    HIP_TRY(q->ctx, hipStreamSynchronize(q->srv_stream));
+    q->srv_running = false;
+    return QPP_OK;
+}
+
+int servers_stop(qpp_ctx *ctx) {
+    for (qpp_txq *q : ctx->servers) RC_TRY(srv_stop(q));
+    return QPP_OK;
+}
+int servers_quiesce(qpp_ctx *ctx) {
+    for (qpp_txq *q : ctx->servers) RC_TRY(srv_wait(q, q->srv_posted));
+    return QPP_OK;
+}
+uint32_t servers_cu(const qpp_ctx *ctx) {
+    uint32_t r = 0;
+    for (qpp_txq *q : ctx->servers)
+        if (srv_alive(q)) r += q->srv_wgs;
+    return r;
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -1696,6 +1887,16 @@ int qpp_txq_create_async(qpp_ctx *ctx, size_t ring_bytes, size_t max_packets, si
 void qpp_txq_destroy(qpp_txq *q) {
     if (!q) return;
     hipSetDevice(q->ctx->device);
+    if (q->persistent) {
+        srv_stop(q);
+        std::vector<qpp_txq *> &v = q->ctx->servers;
+        v.erase(std::remove(v.begin(), v.end(), q), v.end());
+        if (q->srv_stream) { hipStreamSynchronize(q->srv_stream); hipStreamDestroy(q->srv_stream); }
+        if (q->h_mail) hipHostFree(q->h_mail);
+        if (q->d_sync) hipFree(q->d_sync);
+        if (q->h_items) hipHostFree(q->h_items);
+        if (q->h_sdesc) { secure_zero(q->h_sdesc, sizeof(qpp_pkt) * q->max_packets * txq_server_waves()); hipHostFree(q->h_sdesc); }
+    }
     for (hipStream_t st : q->streams) hipStreamSynchronize(st);
     if (q->h_ring) { secure_zero(q->h_ring, q->ring_bytes); hipHostFree(q->h_ring); }
     if (q->d_ring) {
@@ -1830,12 +2031,81 @@ static int txq_refused(TxqSlot &sl) {
     return QPP_INTERNAL_ERROR;
 }
 
+// The pushed batch is handed over: the next pushes start a new one
+static void txq_reset_batch(qpp_txq *q) {
+    q->pend_first = q->pend_last = 0;
+    q->pend_bursts = 0;
+    q->count = q->count_at_ticket = 0;
+    q->lo = SIZE_MAX;
+    q->hi = 0;
+    q->suites = 0;
+}
+
+// Persistent queue: posts slots[cur]'s packets (all AES, no FIPS key live) to the server.  The descriptors are copied
+// into the server's plan (key-sorted, items of <= one packet per wave), so the slot is free for the next pushes at
+// once; the previous posted flush must be done first (its plan is being rewritten).
+static int srv_submit(qpp_txq *q) {
+    qpp_ctx *ctx = q->ctx;
+    TxqSlot &sl = q->slots[q->cur];
+    const uint32_t n = (uint32_t)q->count;
+    RC_TRY(srv_wait(q, q->srv_posted));
+    if (ctx->key_gen != q->srv_key_gen) {
+        // records installed since the last post are in HBM before the server reads them (host wait, only after key
+        // changes), and the new epoch drops every workgroup's cached GHASH tables (a slot may hold a new key now)
+        HIP_TRY(ctx, hipEventSynchronize(ctx->keys_ready));
+        q->srv_key_gen = ctx->key_gen;
+        q->srv_epoch = (q->srv_epoch + 1u) & 0xffu;
+    }
+    if (q->srv_running && q->srv_keys != ctx->d_keys) RC_TRY(srv_stop(q));  // (grow_keys stops servers already)
+    // a server idle for long may be leaving on its own timeout: never post to it (part of it could miss the flush)
+    const auto now = std::chrono::steady_clock::now();
+    if (q->srv_running && now - q->srv_last_post > q->srv_host_idle) RC_TRY(srv_stop(q));
+    const uint32_t W = txq_server_waves();
+    std::vector<uint32_t> &ord = q->order;
+    ord.resize(n);
+    for (uint32_t i = 0; i < n; i++) ord[i] = i;
+    std::stable_sort(ord.begin(), ord.end(),
+                     [&sl](uint32_t a, uint32_t b) { return sl.h_desc[a].key_idx < sl.h_desc[b].key_idx; });
+    // packets per item: spread the flush over the server's workgroups, at most one packet per wave
+    const uint32_t per = std::max(1u, std::min(W, (n + q->srv_wgs - 1) / q->srv_wgs));
+    uint32_t items = 0;
+    for (uint32_t i = 0; i < n;) {
+        const uint32_t slot = sl.h_desc[ord[i]].key_idx;
+        uint32_t j = i;
+        while (j < n && sl.h_desc[ord[j]].key_idx == slot) j++;
+        for (uint32_t b = i; b < j; b += per) {
+            const uint32_t cnt = std::min(per, j - b);
+            q->h_items[items] = WorkItem{slot, items * W, cnt, ctx->h_keys[slot].nr};
+            for (uint32_t k = 0; k < cnt; k++) q->h_sdesc[(size_t)items * W + k] = sl.h_desc[ord[b + k]];
+            items++;
+        }
+        i = j;
+    }
+    RC_TRY(srv_start(q));
+    q->srv_seq = srv_next(q->srv_seq);
+    const uint64_t word = ((uint64_t)q->srv_seq << 32) | ((uint64_t)q->srv_epoch << 24) | items;
+    __atomic_store_n(&q->h_mail->doorbell, word, __ATOMIC_RELEASE);  // the plan and the ring bytes are written
+    q->srv_last_post = now;
+    q->srv_posted = q->srv_seq;
+    q->srv_first = q->pend_first;
+    q->srv_last = q->pend_last;
+    q->n_server++;
+    txq_reset_batch(q);
+    return QPP_OK;
+}
+
 // Sends slots[cur] (every burst flushed into it) and moves on to the next slot, once that one's last flush is over.
 static int txq_submit(qpp_txq *q) {
     if (!q->pend_bursts) return QPP_OK;
     qpp_ctx *ctx = q->ctx;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     RC_TRY(flush_keys(ctx));
+    if (q->persistent) {
+        if (!ctx->fips_live && !(q->suites & ~kAesSuites)) return srv_submit(q);
+        // FIPS gating and ChaCha20-Poly1305 packets take the launched path, behind the posted flush
+        RC_TRY(srv_wait(q, q->srv_posted));
+    }
+    q->n_launch++;
     TxqSlot &sl = q->slots[q->cur];
     const uint32_t n = (uint32_t)q->count;
     StreamState *st = nullptr;
@@ -1883,12 +2153,7 @@ static int txq_submit(qpp_txq *q) {
     sl.busy = true;
     sl.first = q->pend_first;
     sl.last = q->pend_last;
-    q->pend_first = q->pend_last = 0;
-    q->pend_bursts = 0;
-    q->count = q->count_at_ticket = 0;
-    q->lo = SIZE_MAX;
-    q->hi = 0;
-    q->suites = 0;
+    txq_reset_batch(q);
     // the next batch fills the next slot, once that slot's previous flush is over (back-pressure)
     q->cur = (q->cur + 1) % q->slots.size();
     RC_TRY(txq_slot_drain(q, q->slots[q->cur]));
@@ -1926,11 +2191,21 @@ static int txq_slot_of(qpp_txq *q, uint64_t ticket, TxqSlot **out) {
     return QPP_OK;
 }
 
+// a ticket of the flush last posted to the server (earlier posted ones are done: one is posted at a time)
+static bool srv_ticket(const qpp_txq *q, uint64_t ticket) {
+    return q->persistent && q->srv_first && ticket >= q->srv_first && ticket <= q->srv_last;
+}
+
 int qpp_txq_poll(qpp_txq *q, uint64_t ticket, int *done) {
     if (!q || !done) return QPP_INTERNAL_ERROR;
     if (ticket >= q->next_ticket) return QPP_INTERNAL_ERROR;
     TxqSlot *sl = nullptr;
     RC_TRY(txq_slot_of(q, ticket, &sl));
+    if (srv_ticket(q, ticket)) {
+        *done = __atomic_load_n(&q->h_mail->done, __ATOMIC_ACQUIRE) == q->srv_posted;
+        if (!*done && !srv_alive(q)) RC_TRY(srv_start(q));
+        return QPP_OK;
+    }
     if (!sl) { *done = 1; return QPP_OK; }
     if (!sl->busy) { *done = 1; return txq_refused(*sl); }
     const hipError_t e = hipEventQuery(sl->done);
@@ -1946,9 +2221,83 @@ int qpp_txq_wait(qpp_txq *q, uint64_t ticket) {
     if (ticket >= q->next_ticket) return QPP_INTERNAL_ERROR;
     TxqSlot *sl = nullptr;
     RC_TRY(txq_slot_of(q, ticket, &sl));
+    if (srv_ticket(q, ticket)) return srv_wait(q, q->srv_posted);
     if (!sl) return QPP_OK;
     RC_TRY(txq_slot_drain(q, *sl));
     return txq_refused(*sl);
+}
+
+int qpp_txq_create_persistent(qpp_ctx *ctx, size_t ring_bytes, size_t max_packets, qpp_txq **out) {
+    if (!ctx || !out || max_packets >= kTxsItemsMask) return QPP_INTERNAL_ERROR;
+    RC_TRY(qpp_txq_create_async(ctx, ring_bytes, max_packets, 1, out));
+    qpp_txq *q = *out;
+    auto bad = [&](hipError_t e, const char *what) {
+        if (!fail(ctx, e, what)) return false;
+        qpp_txq_destroy(q);
+        *out = nullptr;
+        return true;
+    };
+    q->persistent = true;
+    ctx->servers.push_back(q);
+    const size_t W = txq_server_waves();
+    // fine-grained (coherent) pinned memory: polled by the server over PCIe while the host writes it, and read and
+    // written by a kernel that does not end between flushes (no cached copy may outlive a flush) -- the ring too
+    const unsigned fl = hipHostMallocCoherent | hipHostMallocMapped;
+    void *v = nullptr;
+    hipHostFree(q->h_ring);
+    q->h_ring = nullptr;
+    if (bad(hipHostMalloc(&q->h_ring, ring_bytes, fl), "txq server ring") ||
+        bad(hipHostGetDevicePointer(&v, q->h_ring, 0), "ring view"))
+        return QPP_DEVICE_ERROR;
+    q->v_ring = (uint8_t *)v;
+    memset(q->h_ring, 0, ring_bytes);
+    if (bad(hipHostMalloc(&q->h_mail, sizeof(TxsMail), fl), "txq server mailbox") ||
+        bad(hipHostGetDevicePointer(&v, q->h_mail, 0), "mailbox view"))
+        return QPP_DEVICE_ERROR;
+    q->v_mail = (TxsMail *)v;
+    memset(q->h_mail, 0, sizeof(TxsMail));
+    if (bad(hipHostMalloc(&q->h_items, sizeof(WorkItem) * max_packets, fl), "txq server items") ||
+        bad(hipHostGetDevicePointer(&v, q->h_items, 0), "items view"))
+        return QPP_DEVICE_ERROR;
+    q->v_items = (WorkItem *)v;
+    if (bad(hipHostMalloc(&q->h_sdesc, sizeof(qpp_pkt) * max_packets * W, fl), "txq server descs") ||
+        bad(hipHostGetDevicePointer(&v, q->h_sdesc, 0), "descs view"))
+        return QPP_DEVICE_ERROR;
+    q->v_sdesc = (qpp_pkt *)v;
+    memset(q->h_sdesc, 0, sizeof(qpp_pkt) * max_packets * W);
+    if (bad(hipMalloc(&q->d_sync, sizeof(TxsSync)), "txq server sync") ||
+        bad(hipStreamCreateWithFlags(&q->srv_stream, hipStreamNonBlocking), "txq server stream"))
+        return QPP_DEVICE_ERROR;
+    uint32_t wgs = 16, idle_ms = 200;
+    if (const char *e = getenv("QPP_TXQ_SERVER_WGS")) wgs = (uint32_t)strtoul(e, nullptr, 10);
+    if (const char *e = getenv("QPP_TXQ_SERVER_IDLE_MS")) idle_ms = (uint32_t)strtoul(e, nullptr, 10);
+    q->srv_wgs = std::max(1u, std::min(wgs, ctx->n_cu));
+    idle_ms = std::min<uint32_t>(std::max(4u, idle_ms), 40000u);
+    q->srv_idle_ticks = idle_ms * 100000u;  // s_memrealtime: 100 MHz
+    q->srv_host_idle = std::chrono::microseconds(250u * idle_ms);
+    return QPP_OK;
+}
+
+int qpp_txq_server_time(const qpp_txq *q, double *us) {
+    if (!q || !us || !q->persistent) return QPP_INTERNAL_ERROR;
+    *us = (double)(q->h_mail->t_done - q->h_mail->t_seen) / 100.0;
+    return QPP_OK;
+}
+
+int qpp_txq_server_stamps(const qpp_txq *q, uint64_t out[6]) {
+    if (!q || !out || !q->persistent) return QPP_INTERNAL_ERROR;
+    const TxsMail &m = *q->h_mail;
+    const uint64_t v[6] = {m.t_seen, m.pad0[0], m.pad0[1], m.pad0[2], m.pad0[3], m.t_done};
+    memcpy(out, v, sizeof v);
+    return QPP_OK;
+}
+
+int qpp_txq_info(const qpp_txq *q, uint64_t *server_flushes, uint64_t *launched_flushes, uint64_t *server_starts) {
+    if (!q) return QPP_INTERNAL_ERROR;
+    if (server_flushes) *server_flushes = q->n_server;
+    if (launched_flushes) *launched_flushes = q->n_launch;
+    if (server_starts) *server_starts = q->n_starts;
+    return QPP_OK;
 }
 
 int qpp_txq_flush(qpp_txq *q) {

@@ -114,22 +114,52 @@ __device__ __forceinline__ uint32_t byte_of(uint4 v, uint32_t i) {  // byte i (<
     return (w >> (8 * (i & 3))) & 0xffu;
 }
 
-// One packet on one wave (all 64 lanes; d is wave-uniform).
-template <int NR, bool SEAL>
+// The persistent txq server's per-workgroup copy of its cached key's iv | rk | hp_rk (LDS, after the tables and
+// the control words): no device-memory round trip per packet for them.
+constexpr uint32_t kTxsKey = kBurstLds + 64;
+constexpr uint32_t kTxsLds = kTxsKey + 512;
+
+// One packet on one wave (all 64 lanes; d is wave-uniform).  LDSKEY: the key's iv and header-protection round keys
+// come from the server's LDS copy (kTxsKey) instead of the key record.
+template <int NR, bool SEAL, bool LDSKEY = false>
 __device__ __forceinline__ void burst_packet(const AesLds &aes, const DevKey *__restrict__ key,
                                              const uint32_t *__restrict__ rk, const qpp_pkt &d, uint32_t pi,
                                              uint8_t *arena, uint8_t *masks, int8_t *status, uint32_t flags) {
     const uint32_t lane = threadIdx.x & 63u;
-    const PacketView p = load_packet(d, key, arena);
+    PacketView p;
+    if constexpr (LDSKEY) {
+        p.base = arena + d.off;
+        p.aad_len = d.aad_len;
+        p.len = d.pt_len;
+        p.pn_len = d.pn_len;
+        p.n0 = lds_ld32(kTxsKey);  // Iv::nonce (src/iv.rs:27-39)
+        p.n1 = lds_ld32(kTxsKey + 4) ^ bswap32((uint32_t)(d.pn >> 32));
+        p.n2 = lds_ld32(kTxsKey + 8) ^ bswap32((uint32_t)d.pn);
+    } else {
+        p = load_packet(d, key, arena);
+    }
     uint8_t *pay = p.base + p.aad_len;
+    const uint32_t a = (p.aad_len + 15u) >> 4, c = (p.len + 15u) >> 4, m = a + c + 1;
+    const uint32_t K = (m + 63u) >> 6, pad = 64u * K - m;
+    // Each lane reads at most one 16-byte block per pass (a payload block or an AAD block).  Pass k + 1's read is
+    // issued before pass k's AES, so a packet pays one memory round trip, not one per pass (over PCIe, from the
+    // pinned ring of a txq flush, a round trip is ~1.5 us: most of a 64-packet flush once did nothing else).
+    auto block = [&](uint32_t k) {
+        const int i = (int)(lane + 64u * k) - (int)pad;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (i >= (int)a && i < (int)(a + c)) v = ld16(pay + 16u * (uint32_t)(i - (int)a));
+        else if (i >= 0 && i < (int)a) v = ld16(p.base + 16u * (uint32_t)i);
+        return v;
+    };
+    uint4 next = block(0);
     // header-protection round keys and header bytes: issued now, used after the GHASH tree (one memory round trip
     // off the end of the chain)
     constexpr int HNR = NR == 10 ? 10 : 14;
     HpPrefetch<HNR> hpk;
-    if (SEAL && (flags & (QPP_HP_MASK_OUT | QPP_HP_APPLY)) && lane == 0 && p.pn_len >= 1 && p.pn_len <= 4)
-        hpk.load(key->hp_rk, p.base, p.aad_len - p.pn_len, flags);
-    const uint32_t a = (p.aad_len + 15u) >> 4, c = (p.len + 15u) >> 4, m = a + c + 1;
-    const uint32_t K = (m + 63u) >> 6, pad = 64u * K - m;
+    if (SEAL && (flags & (QPP_HP_MASK_OUT | QPP_HP_APPLY)) && lane == 0 && p.pn_len >= 1 && p.pn_len <= 4) {
+        if constexpr (LDSKEY) hpk.load_hdr(p.base, p.aad_len - p.pn_len, flags);
+        else hpk.load(key->hp_rk, p.base, p.aad_len - p.pn_len, flags);
+    }
     uint4 acc = make_uint4(0, 0, 0, 0), ct0 = acc, ct1 = acc;  // ct0/ct1: ciphertext blocks 0/1 where owned
     uint4 ek = acc;  // E_K(J0), computed in pass 0 by the idle lane pad - 1 inside the data lanes' AES stream
     for (uint32_t k = 0; k < K; k++) {
@@ -137,16 +167,15 @@ __device__ __forceinline__ void burst_packet(const AesLds &aes, const DevKey *__
         const bool data = i >= (int)a && i < (int)(a + c);
         const bool j0 = k == 0 && i == -1;
         const uint32_t b = (uint32_t)i - a;  // data block b uses counter b + 2
-        uint4 in = make_uint4(0, 0, 0, 0), ks = in;
-        if (data || j0) {
-            if (data) in = ld16(pay + 16u * b);
-            ks = aes.encrypt<NR>(make_uint4(p.n0, p.n1, p.n2, bswap32(data ? b + 2u : 1u)), rk);
-        }
+        const uint4 raw = next;
+        if (k + 1 < K) next = block(k + 1);
+        uint4 in = data ? raw : make_uint4(0, 0, 0, 0), ks = make_uint4(0, 0, 0, 0);
+        if (data || j0) ks = aes.encrypt<NR>(make_uint4(p.n0, p.n1, p.n2, bswap32(data ? b + 2u : 1u)), rk);
         uint4 x = make_uint4(0, 0, 0, 0);
         if (j0) ek = ks;
         if (i >= 0 && i < (int)a) {
             const uint32_t off = 16u * (uint32_t)i;
-            x = ld16(p.base + off);
+            x = raw;
             if (p.aad_len - off < 16u) x = keep_bytes(x, p.aad_len - off);
         } else if (data) {
             const uint32_t r = p.len - 16u * b;
@@ -199,7 +228,13 @@ __device__ __forceinline__ void burst_packet(const AesLds &aes, const DevKey *__
                     }
                     smp = make_uint4(w[0], w[1], w[2], w[3]);
                 }
-                if (lane == 0) hpk.finish(aes, smp, p.base, p.aad_len - p.pn_len, p.pn_len, masks + 5 * (size_t)pi, flags);
+                if (lane == 0) {
+                    if constexpr (LDSKEY)
+                        hpk.finish_lds(aes, kTxsKey + 16 + 240, smp, p.base, p.aad_len - p.pn_len, p.pn_len,
+                                       masks + 5 * (size_t)pi, flags);
+                    else
+                        hpk.finish(aes, smp, p.base, p.aad_len - p.pn_len, p.pn_len, masks + 5 * (size_t)pi, flags);
+                }
             }
         }
         if (status && lane == 0) status[pi] = st;
@@ -259,6 +294,149 @@ __global__ __launch_bounds__(kBurstWG) void aes_gcm_burst_kernel(const DevKey *_
     }
 }
 
+// ---------------------------------------------------------------- persistent transmit-queue server
+// qpp_txq_create_persistent: the seal of a GSO burst without a kernel launch per flush.  The transport's queue.flush()
+// (endpoint/mod.rs:158 -> socket/io/tx.rs:204-268) posts a flush by writing one 64-bit doorbell word into pinned
+// host memory; the workgroups below are already resident, with the AES tables built and the last key's GHASH tables
+// in LDS, and write `done` back into the same pinned page when the burst is sealed.
+//
+// Protocol (one flush in flight; the host posts the next only after `done`):
+//   doorbell = seq << 32 | epoch << 24 | items   (items = kTxsStop: exit)
+// * every workgroup polls the doorbell itself (QPP_TXS_DIRECT; else workgroup 0 polls and forwards the word through
+//   device memory, one hop more).  A workgroup leaves on the stop word, or after idle_ticks without a new doorbell --
+//   the host never posts to a server that may be leaving on its own: after a quarter of that idle time without a
+//   post it stops the server and starts a new one first (api.cpp srv_submit), so a flush is seen by every workgroup
+//   or by none (the idle exit is for a host that went away);
+// * item i (one key, <= kBurstWaves packets, host-built) goes to workgroup i % grid, packet q of it to wave q; the
+//   descriptors sit at sdesc[i * kBurstWaves + q], so a wave reads its item and its descriptor in one round trip;
+// * a workgroup keeps the GHASH tables of the key it used last until a doorbell carries a new key epoch (the host
+//   bumps it whenever key records were installed since its previous post: a slot can have been reused); only then
+//   does it invalidate its caches (the plan and the ring are fine-grained host memory, never cached);
+// * completion: every storing wave drains its stores, the workgroup releases at system scope and counts itself in
+//   sync->arrive; the last one resets the count and writes done = seq (system scope).
+#ifndef QPP_TXS_DIRECT
+#define QPP_TXS_DIRECT 1
+#endif
+#ifndef QPP_TXS_TRACE
+#define QPP_TXS_TRACE 0  // 1: workgroup 0 stamps its phases into the mailbox (tools/diag/server_trace.py)
+#endif
+constexpr uint32_t kTxsCtl = kBurstLds;  // LDS: the doorbell word and the stop flag broadcast to the workgroup
+static_assert(kTxsKey >= kTxsCtl + 16 && kTxsLds <= kLdsMax, "server LDS");
+
+template <int NR>
+__device__ __forceinline__ void txs_item(const AesLds &aes, const DevKey *key, const qpp_pkt &d,
+                                         uint32_t wave, uint32_t count, uint8_t *ring) {
+    uint32_t rk[4 * (NR + 1)];
+#pragma unroll
+    for (int i = 0; i < 4 * (NR + 1); i++) rk[i] = __builtin_amdgcn_readfirstlane(lds_ld32(kTxsKey + 16 + 4 * i));
+    if (wave < count && !(d.flags & QPP_PKT_SKIP))
+        burst_packet<NR, true, true>(aes, key, rk, d, 0, ring, nullptr, nullptr, QPP_HP_APPLY);
+}
+
+__global__ __launch_bounds__(kBurstWG) void txq_server_kernel(const DevKey *keys, const PowTables pow, TxsMail *mail,
+                                                              TxsSync *sync, const WorkItem *items,
+                                                              const qpp_pkt *sdesc, uint8_t *ring, uint32_t seq0,
+                                                              uint32_t idle_ticks) {
+    build_aes_tables(kBurstAes);
+    __syncthreads();
+    const AesLds aes = make_aes(kBurstAes);
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint32_t seen = seq0, cached = 0xffffffffu, epoch = 0xffffffffu;
+    for (;;) {
+        if (threadIdx.x == 0) {
+            uint64_t word = 0;
+            uint32_t stop = 0;
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            if (QPP_TXS_DIRECT || blockIdx.x == 0) {
+                for (;;) {
+                    word = __hip_atomic_load(&mail->doorbell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    if ((uint32_t)(word >> 32) != seen) break;
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) { stop = 1; break; }
+                    __builtin_amdgcn_s_sleep(2);
+                }
+                if ((uint32_t)(word & kTxsItemsMask) == kTxsStop) stop = 1;
+                if (!stop && blockIdx.x == 0)
+                    __hip_atomic_store(&mail->t_seen, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_SYSTEM);
+                if (!QPP_TXS_DIRECT) {
+                    if (stop) __hip_atomic_store(&sync->stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    else __hip_atomic_store(&sync->go, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            } else {
+                for (;;) {
+                    if (__hip_atomic_load(&sync->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) { stop = 1; break; }
+                    word = __hip_atomic_load(&sync->go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const uint32_t sq = (uint32_t)(word >> 32);
+                    if (sq != seen && sq != 0) break;
+                    __builtin_amdgcn_s_sleep(2);
+                }
+            }
+            // key records installed since this workgroup's caches last looked: visible from here on
+            if (!stop && ((uint32_t)word >> 24) != epoch) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+            lds_st64(kTxsCtl, make_uint2((uint32_t)word, (uint32_t)(word >> 32)));
+            lds_st32(kTxsCtl + 8, stop);
+        }
+        __syncthreads();
+        const uint2 w2 = lds_ld64(kTxsCtl);
+        const uint32_t stop = lds_ld32(kTxsCtl + 8);
+        __syncthreads();  // (the next doorbell's broadcast does not overwrite these before every wave read them)
+        if (stop) break;  // uniform
+        seen = w2.y;
+        const uint32_t n_items = w2.x & kTxsItemsMask, ep = w2.x >> 24;
+        // The plan and the key records change between flushes, so they are read with VECTOR loads, through the
+        // caches the acquire above invalidated: left alone, the compiler read the wave-uniform work item, descriptor
+        // and round keys with scalar loads, whose cache the fence does not cover, and every flush after the first
+        // sealed the first flush's descriptors again.  The pointers are re-laundered into VGPRs once per flush.
+        const WorkItem *items_v = items;
+        const qpp_pkt *sdesc_v = sdesc;
+        const DevKey *keys_v = keys;
+        asm volatile("" : "+v"(items_v), "+v"(sdesc_v), "+v"(keys_v));
+        if (ep != epoch) {
+            epoch = ep;
+            cached = 0xffffffffu;
+        }
+        uint64_t tr[4] = {0, 0, 0, 0};
+        if (QPP_TXS_TRACE && threadIdx.x == 0) tr[0] = __builtin_amdgcn_s_memrealtime();
+        for (uint32_t it = blockIdx.x; it < n_items; it += gridDim.x) {
+            const WorkItem w = items_v[it];
+            const qpp_pkt d = sdesc_v[it * kBurstWaves + wave];
+            if (QPP_TXS_TRACE && threadIdx.x == 0 && !tr[1]) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                tr[1] = __builtin_amdgcn_s_memrealtime();
+            }
+            const DevKey *key = keys_v + w.key;
+            if (w.key != cached) {  // uniform
+                __syncthreads();  // every wave is done with the previous key's tables
+                // iv | rk | hp_rk: 124 consecutive words of the record (DevKey: iv at word 4)
+                if (threadIdx.x < 124) lds_st32(kTxsKey + 4 * threadIdx.x, ((const uint32_t *)key)[4 + threadIdx.x]);
+                burst_tables(key, w.key, pow);  // (ends with a barrier)
+                cached = w.key;
+            }
+            if (w.nr == 10) txs_item<10>(aes, key, d, wave, w.count, ring);
+            else txs_item<14>(aes, key, d, wave, w.count, ring);
+        }
+        // completion: this workgroup's ring stores reach the host before it counts itself
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (QPP_TXS_TRACE && threadIdx.x == 0) tr[2] = __builtin_amdgcn_s_memrealtime();
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            const uint32_t prev = __hip_atomic_fetch_add(&sync->arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+            if (QPP_TXS_TRACE && blockIdx.x == 0) {
+                tr[3] = __builtin_amdgcn_s_memrealtime();
+                for (int j = 0; j < 4; j++)
+                    __hip_atomic_store(&mail->pad0[j], tr[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            if (prev == gridDim.x - 1) {
+                __hip_atomic_store(&sync->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&mail->t_done, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(&mail->done, seen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
+    }
+}
+
 template <bool SEAL, int NR>
 void launch_burst(dim3 grid, hipStream_t s, const DevKey *keys, const qpp_pkt *descs, const PlanBuffers &pb,
                   uint8_t *arena, uint8_t *masks, int8_t *status, uint32_t flags, const PowTables &pow) {
@@ -290,6 +468,16 @@ hipError_t launch_aes_gcm_burst(bool seal, const DevKey *keys, const qpp_pkt *de
         if (seal) launch_burst<true, 14>(grid, s, keys, descs, pb, arena, masks, status, flags, pow);
         else launch_burst<false, 14>(grid, s, keys, descs, pb, arena, masks, status, flags, pow);
     }
+    return hipGetLastError();
+}
+
+uint32_t txq_server_waves() { return (uint32_t)kBurstWaves; }
+
+hipError_t launch_txq_server(const DevKey *keys, const PowTables &pow, TxsMail *mail, TxsSync *sync,
+                             const WorkItem *items, const qpp_pkt *sdesc, uint8_t *ring, uint32_t seq0,
+                             uint32_t idle_ticks, uint32_t wgs, hipStream_t s) {
+    hipLaunchKernelGGL(txq_server_kernel, dim3(wgs), dim3(kBurstWG), kTxsLds, s, keys, pow, mail, sync, items,
+                       sdesc, ring, seq0, idle_ticks);
     return hipGetLastError();
 }
 

@@ -131,7 +131,7 @@ __global__ __launch_bounds__(256, 3) void chacha_kernel(const DevKey *__restrict
     if (refused && pi < n && status && !(d.flags & QPP_PKT_SKIP)) status[pi] = QPP_INTERNAL_ERROR;
     const bool has = pi < n && !refused && key->suite == QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256 &&
                      !(d.flags & QPP_PKT_SKIP);
-    if (!__any(has)) return;  // wave-uniform: AES packets go to aes_gcm_kernel
+    if (!__any(has)) return;  // wave-uniform: AES packets go to the AES kernels
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t stage = (threadIdx.x >> 6) * kChachaWaveLds, tab = stage + kChachaStage;
     uint32_t k[8];

@@ -27,6 +27,10 @@ __device__ __forceinline__ uint4 lds_ld128(uint32_t a) {
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 __device__ __forceinline__ void lds_st32(uint32_t a, uint32_t v) { *(lds_u32 *)(size_t)a = v; }
+// ds_add_rtn_u32: the old value (workgroup scope)
+__device__ __forceinline__ uint32_t lds_add32(uint32_t a, uint32_t v) {
+    return __hip_atomic_fetch_add((lds_u32 *)(size_t)a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) u32x2 lds_u64;
 __device__ __forceinline__ uint2 lds_ld64(uint32_t a) {
@@ -262,6 +266,60 @@ __device__ __forceinline__ void ctr_keystream_pipe(const AesLds &a, const CtrPag
     for (int j = 0; j < NB; j++) ks[j] = make_uint4(st[NR & 1][j][0], st[NR & 1][j][1], st[NR & 1][j][2], st[NR & 1][j][3]);
 }
 
+// The same pipeline with the units in block-major order (round r, block j, column c) and each block's state updated
+// in place: a block's 4 new columns wait in `nw` until its 4th unit has issued its lookups (D <= 3 units ahead), so
+// the state is NB x 4 words instead of the parity pair's 2 x NB x 4 -- 12 VGPRs fewer at NB = 4, what lets the quad
+// kernel (quad.hip) run more waves per SIMD without spilling.  Same lookups, same combines, same results.
+template <int NR, int NB, int STRIDE = 1>
+__device__ __forceinline__ void ctr_keystream_inplace(const AesLds &a, const CtrPage &pg, const uint32_t *__restrict__ rk,
+                                                      uint32_t c0, uint4 (&ks)[NB]) {
+    static_assert(NB >= 1 && NB <= 4, "pipeline depth NB - 1 lookups groups of 4 within the 15-read counter");
+    constexpr int D = NB - 1;
+    constexpr int U = (NR - 2) * 4 * NB;  // units of rounds 3..NR
+    uint32_t st[NB][4];
+    uint32_t nw[4];
+    uint32_t ld[D + 1][4];  // lookups of the units in flight (ring)
+#pragma unroll
+    for (int j = 0; j < NB; j++) pg.two_rounds(a, c0 + STRIDE * j, st[j]);
+    auto issue = [&](auto uc) {
+        constexpr int u = decltype(uc)::value;
+        constexpr int j = (u / 4) % NB, c = u % 4;
+        const uint32_t *s = st[j];
+        uint32_t *l = ld[u % (D + 1)];
+        l[0] = a.t0<0>(s[c]);
+        l[1] = a.t1<1>(s[(c + 1) & 3]);
+        l[2] = a.t0<2>(s[(c + 2) & 3]);
+        l[3] = a.t1<3>(s[(c + 3) & 3]);
+    };
+    auto combine = [&](auto uc) {
+        constexpr int u = decltype(uc)::value;
+        constexpr int r = 3 + u / (4 * NB), j = (u / 4) % NB, c = u % 4;
+        const uint32_t *l = ld[u % (D + 1)];
+        const uint32_t k = rk[4 * r + c];
+        if constexpr (r < NR) {
+            nw[c] = xor3(l[0], l[1], k) ^ rotl16(l[2] ^ l[3]);
+        } else {  // final round: S-box bytes only (AesLds::last)
+            const uint32_t lo = __builtin_amdgcn_perm(l[1], l[0], 0x0c0c0601u);
+            const uint32_t hi = __builtin_amdgcn_perm(l[3], l[2], 0x07020c0cu);
+            nw[c] = xor3(lo, hi, k);
+        }
+        if constexpr (c == 3) {  // the block's 4 units have all issued (D <= 3): its new state replaces the old
+#pragma unroll
+            for (int i = 0; i < 4; i++) st[j][i] = nw[i];
+        }
+    };
+    static_for<D>([&](auto uc) { issue(uc); });
+    static_for<U>([&](auto uc) {
+        constexpr int u = decltype(uc)::value;
+        if constexpr (u + D < U) issue(std::integral_constant<int, u + D>{});
+        __builtin_amdgcn_sched_barrier(0);
+        combine(uc);
+        __builtin_amdgcn_sched_barrier(0);
+    });
+#pragma unroll
+    for (int j = 0; j < NB; j++) ks[j] = make_uint4(st[j][0], st[j][1], st[j][2], st[j][3]);
+}
+
 // AES T0/T1 bank-replicated tables for the AesLds view: row x = 256 B, dword slot 0..31 = T0[x], 32..63 =
 // T1[x] = rotl8 T0[x].  Thread t owns S-box value x = t % 256 (one S-box load) and writes its row's slots in an
 // order rotated by x, so a wave's 64 stores of one step go to 32 distinct banks per 32-lane group.  Needs
@@ -348,6 +406,16 @@ struct HpPrefetch {
             rk[4 * i] = v.x; rk[4 * i + 1] = v.y; rk[4 * i + 2] = v.z; rk[4 * i + 3] = v.w;
         }
         h = (flags & QPP_HP_APPLY) ? hdr_load(base, hdr_len) : HdrBytes{0, 0};
+    }
+    // round keys in LDS (finish_lds reads them there when needed): only the header bytes are prefetched
+    __device__ __forceinline__ void load_hdr(const uint8_t *base, uint32_t hdr_len, uint32_t flags) {
+        h = (flags & QPP_HP_APPLY) ? hdr_load(base, hdr_len) : HdrBytes{0, 0};
+    }
+    __device__ __forceinline__ void finish_lds(const AesLds &aes, uint32_t lds_rk, uint4 sample, uint8_t *base,
+                                               uint32_t hdr_len, uint32_t pn_len, uint8_t *mask_out, uint32_t flags) {
+#pragma unroll
+        for (int i = 0; i < 4 * (HNR + 1); i++) rk[i] = lds_ld32(lds_rk + 4 * i);
+        finish(aes, sample, base, hdr_len, pn_len, mask_out, flags);
     }
     __device__ __forceinline__ void finish(const AesLds &aes, uint4 sample, uint8_t *base, uint32_t hdr_len,
                                            uint32_t pn_len, uint8_t *mask_out, uint32_t flags) const {

@@ -293,4 +293,21 @@ hipError_t launch_plan(const DevKey *keys, uint32_t key_cap, const qpp_pkt *desc
     return hipGetLastError();
 }
 
+// Connection-indexed descriptors (QPP_KEY_BY_CONN): key_idx names a connection's entry in the device table `map`
+// (the transport's KeySet, crypto/application/keyset.rs: a key update swaps the key behind the entry, the packets
+// queued for the connection do not change); the slot it holds replaces key_idx in the batch's device copy.  An index
+// past the table becomes 0xffffffff, a slot outside every key table (the packet is refused, INTERNAL_ERROR).
+__global__ void conn_remap_kernel(qpp_pkt *descs, uint32_t n, const uint32_t *__restrict__ map, uint32_t map_n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t c = descs[i].key_idx;
+    descs[i].key_idx = c < map_n ? map[c] : 0xffffffffu;
+}
+
+hipError_t launch_conn_remap(qpp_pkt *descs, uint32_t n, const uint32_t *map, uint32_t map_n, hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(conn_remap_kernel, dim3((n + 255) / 256), dim3(256), 0, s, descs, n, map, map_n);
+    return hipGetLastError();
+}
+
 }  // namespace qpp

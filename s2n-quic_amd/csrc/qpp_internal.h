@@ -95,13 +95,12 @@ struct WorkItem {
 constexpr int kMinPacketsPerItem = 4;
 constexpr uint32_t kWavePacketsPerItem = 64;  // aes_gcm_wave_kernel: one wave, one key, <= 64 packets per work item
 constexpr uint32_t kWaveKernelPacketsPerKey = 1024;  // batches with fewer packets per live AES key take the wave kernel
-constexpr uint32_t kLanePerItem = 0x7fffffffu;  // aes_gcm_kernel: one work item per key (workgroups take equal slices)
+constexpr uint32_t kLanePerItem = 0x7fffffffu;  // aes_gcm_quad_kernel: one work item per key (workgroups take equal slices)
 constexpr uint32_t kBurstMaxDefault = 16384;  // AES batches up to this many packets run one wave per packet
 constexpr uint32_t kChachaBurstShift = 2;     // ChaCha20-Poly1305 batches up to burst_max >> 2 do (its lane kernel
                                               // fills the chip with fewer packets: crossover ~6 Ki vs ~20 Ki)
 constexpr uint32_t kTxqZeroCopyMax = 1024;    // txq flushes up to this many packets run on the pinned ring in place
                                               // (coalesced bursts: 512-packet launches were 36 % faster in place)
-constexpr int kDefaultAesVariant = 0;  // see aes_gcm.hip launch_variant
 constexpr int kMaxPlanKeys = 8192;      // keys binned in LDS by the plan kernels (larger tables: global bins)
 
 // Per-key GHASH power tables of the burst kernel (burst.hip): T_t = 4-bit tables of H^(2^t), t = 1..6, 48 KiB per
@@ -138,11 +137,36 @@ uint32_t key_material_bytes();
 hipError_t launch_plan(const DevKey *keys, uint32_t key_cap, const qpp_pkt *descs, uint32_t n, PlanBuffers pb,
                        uint32_t per, hipStream_t s);
 uint32_t plan_max_work(uint32_t n, uint32_t key_cap, uint32_t per);
+// QPP_KEY_BY_CONN: descs[i].key_idx = map[descs[i].key_idx] (0xffffffff past map_n), in place on the device copy
+hipError_t launch_conn_remap(qpp_pkt *descs, uint32_t n, const uint32_t *map, uint32_t map_n, hipStream_t s);
 // burst.hip: one wave per packet for small batches (GSO bursts); work items of whole waves, <= 64 packets
 uint32_t burst_packets_per_item(uint32_t n, uint32_t n_cu);
 hipError_t launch_aes_gcm_burst(bool seal, const DevKey *keys, const qpp_pkt *descs, const PlanBuffers &pb,
                                 uint32_t n, uint32_t key_cap, uint32_t per, uint8_t *arena, uint8_t *masks,
                                 int8_t *status, uint32_t flags, uint32_t suites, const PowTables &pow, hipStream_t s);
+// Persistent transmit-queue server (burst.hip txq_server_kernel; api.cpp qpp_txq_create_persistent).
+// TxsMail: pinned, coherent host memory (the host writes doorbell, the server writes done); TxsSync: device memory.
+struct alignas(64) TxsMail {
+    uint64_t doorbell;  // seq << 32 | key epoch << 24 | work items (kTxsStop: exit)
+    // server-side timestamps of the last flush (s_memrealtime, 100 MHz): the leader saw the doorbell / the last
+    // workgroup finished (written before done)
+    uint64_t t_seen, t_done;
+    uint64_t pad0[5];  // QPP_TXS_TRACE: workgroup 0's broadcast / item read / packets done / arrival stamps
+    uint32_t done;      // seq of the last flush sealed
+    uint32_t pad1[15];
+};
+struct alignas(64) TxsSync {
+    uint64_t go;      // the leader's copy of the doorbell word for the other workgroups
+    uint32_t stop;    // set by the leader when the server exits
+    uint32_t arrive;  // workgroups done with the current flush
+    uint32_t pad[12];
+};
+constexpr uint32_t kTxsItemsMask = 0xffffffu;
+constexpr uint32_t kTxsStop = 0xffffffu;
+uint32_t txq_server_waves();  // packets per work item (one per wave); sdesc holds items x this many slots
+hipError_t launch_txq_server(const DevKey *keys, const PowTables &pow, TxsMail *mail, TxsSync *sync,
+                             const WorkItem *items, const qpp_pkt *sdesc, uint8_t *ring, uint32_t seq0,
+                             uint32_t idle_ticks, uint32_t wgs, hipStream_t s);
 // the burst power tables of keys[slots[i]] (AES packet keys with slot < pow.cap), after their V[m] are in place
 hipError_t launch_pow_setup(const DevKey *keys, const uint32_t *slots, uint32_t count, const PowTables &pow,
                             hipStream_t s);
@@ -157,6 +181,13 @@ hipError_t launch_aes_gcm_single(bool seal, const DevKey *keys, const qpp_pkt *d
                                  uint32_t n, uint32_t n_cu, uint8_t *arena, uint8_t *masks, int8_t *status,
                                  uint32_t flags, hipStream_t s);
 // quad.hip: the quad-layout (4 lanes per packet, 1024-thread workgroups) throughput kernel behind the two above
+// quad.hip: fused unprotect -> PN expand -> key-phase choice -> open for any mix of live packet keys of ONE AES size
+// (nr), one cooperative launch of `grid` workgroups (<= the CUs it may use; key_cap <= quad_rx_max_keys(), even).
+// scratch: 16 + 2 key_cap + 4 + 4 (key_cap + 1) words, the first 16 + 2 key_cap zeroed before the launch; perm: n words.
+uint32_t quad_rx_max_keys();
+hipError_t launch_aes_gcm_quad_rx(uint32_t nr, uint32_t grid, hipStream_t s, const DevKey *keys, uint32_t key_cap,
+                                  const qpp_rx_pkt *rx, uint32_t n, uint8_t *arena, qpp_pkt *descs_out, int8_t *status,
+                                  uint32_t *scratch, uint32_t *perm);
 hipError_t launch_aes_gcm_quad(bool seal, uint32_t nr, dim3 grid, hipStream_t s, const DevKey *keys,
                                const qpp_pkt *descs, const PlanBuffers &pb, uint8_t *arena, uint8_t *masks,
                                int8_t *status, uint32_t flags, uint32_t single, uint32_t n_single);
@@ -169,10 +200,6 @@ hipError_t launch_aes_gcm_wave(bool seal, const DevKey *keys, const qpp_pkt *des
 hipError_t launch_chacha(bool seal, const DevKey *keys, uint32_t key_cap, const qpp_pkt *descs, uint32_t n,
                          uint8_t *arena, uint8_t *masks, int8_t *status, uint32_t flags, bool burst, hipStream_t s);
 // receive side: remove header protection, expand the PN, choose the key by key phase -> descs_out (chacha.hip)
-// fused unprotect -> PN expand -> open for a context whose only live packet key is the AES key `slot` (aes_gcm.hip)
-hipError_t launch_aes_gcm_rx(const DevKey *keys, uint32_t key_cap, const qpp_rx_pkt *rx, uint32_t n, uint32_t slot,
-                             uint32_t nr, uint32_t n_cu, uint8_t *arena, qpp_pkt *descs_out, int8_t *status,
-                             hipStream_t s);
 // fused unprotect -> PN expand -> open for a context with no live AES record (chacha.hip)
 hipError_t launch_chacha_rx(const DevKey *keys, uint32_t key_cap, const qpp_rx_pkt *rx, uint32_t n, uint8_t *arena,
                             qpp_pkt *descs_out, int8_t *status, hipStream_t s);

@@ -33,11 +33,42 @@ using namespace dev;
 
 constexpr uint32_t kQLdsPow = 131072;  // 4-bit tables of H^1..H^4
 constexpr uint32_t kQLdsVe = 65536;    // V_e during the build
-#ifndef QPP_QUAD_WG
-#define QPP_QUAD_WG 768  // 3 waves per SIMD (<= 168 VGPRs: no spills); 1024 (4 waves, <= 128) spilled: 8 % slower (profiles/r03g_wg)
+#ifndef QPP_QUAD_TOUCH
+#define QPP_QUAD_TOUCH 0
 #endif
-constexpr int kQuadWG = QPP_QUAD_WG;
-constexpr uint32_t kQuadPkts = kQuadWG / 4;  // packets per workgroup pass
+#ifndef QPP_QUAD_EARLY_LOADS
+#define QPP_QUAD_EARLY_LOADS 0
+#endif
+#ifndef QPP_QUAD_PIPE
+#define QPP_QUAD_PIPE ctr_keystream_inplace
+#endif
+#ifndef QPP_QUAD_NT
+#define QPP_QUAD_NT 1  // payload stores non-temporal
+#endif
+#ifndef QPP_QUAD_EK_REG
+#define QPP_QUAD_EK_REG 1  // seal: E_K(J0) kept in a register (else stashed in the tag slot and read back)
+#endif
+#ifndef QPP_QUAD_HP_EARLY
+#define QPP_QUAD_HP_EARLY 1  // seal: header protection right after group 0 (the sample is in its ciphertext blocks)
+#endif
+#ifndef QPP_QUAD_DEFER
+#define QPP_QUAD_DEFER 1  // interior groups: the last 64 bytes go out with the next group's first 64
+#endif
+#ifndef QPP_QUAD_WG
+#define QPP_QUAD_WG 768  // AES-128: 3 waves per SIMD (<= 168 VGPRs); 1024 (4 waves, <= 128) spilled
+#endif
+#ifndef QPP_QUAD_WG256
+#define QPP_QUAD_WG256 768  // AES-256 (60 round-key words, 14 rounds of pipeline state)
+#endif
+__device__ __forceinline__ void st_payload(uint8_t *p, uint4 v) {
+#if QPP_QUAD_NT
+    st16_nt(p, v);
+#else
+    st16(p, v);
+#endif
+}
+template <int NR>
+constexpr int kQuadWG = NR == 10 ? QPP_QUAD_WG : QPP_QUAD_WG256;
 
 // X * H through the 8-bit tables of H at [0, 64K) (T_j[x] at 256 x + 16 j): the setup's products
 __device__ __forceinline__ uint4 mul_h8(uint4 x) {
@@ -192,6 +223,38 @@ __device__ __forceinline__ void quad_packet(const AesLds &aes, const GhashT<true
     auto lenblk = [&]() { return make_uint4(0, bswap32(aad_len * 8), 0, bswap32(len * 8)); };
     bool len_done = !has;
 
+    constexpr int HNR = NR == 10 ? 10 : 14;
+    const bool want_hp = SEAL && (flags & (QPP_HP_MASK_OUT | QPP_HP_APPLY)) != 0;
+    uint4 ek0 = make_uint4(0, 0, 0, 0);  // seal: E_K(J0) (slot 0: lane 0, group 0)
+    uint4 held = make_uint4(0, 0, 0, 0);  // QPP_QUAD_DEFER: the previous interior group's blocks k = 3
+    bool held_ok = false;
+    bool hp_done = false;                // seal: header protection applied after group 0 (quad-uniform)
+    // Header protection as soon as the sample exists: the sample (ciphertext bytes [4 - pn_len, 20 - pn_len),
+    // payload.rs:151-169) lies in ciphertext blocks 0 and 1 -- slots 1 and 2, group 0, lanes 1 and 2 -- when the payload
+    // has at least 20 - pn_len bytes.  The header bytes are then written while the packet's first 64-byte segment still
+    // holds group 0's ciphertext in L2 (one memory write for both, not two), and nothing is read back.
+    auto hp_early = [&](const uint4 &ct) {
+        const qpp_pkt dt = reload_desc(dptr);
+        const uint32_t pn_len = dt.pn_len;
+        if (!(want_hp && has && pn_len >= 1 && pn_len <= 4 && len + pn_len >= 20)) return;  // quad-uniform
+        const uint4 b0 = qperm<kQuadBcast1>(ct), b1 = qperm<kQuadBcast2>(ct);  // ciphertext blocks 0 and 1
+        const uint32_t lo = s == 0 ? b0.x : s == 1 ? b0.y : s == 2 ? b0.z : b0.w;
+        const uint32_t hi = s == 0 ? b0.y : s == 1 ? b0.z : s == 2 ? b0.w : b1.x;
+        const uint32_t col = __builtin_amdgcn_alignbyte(hi, lo, 4 - pn_len);  // sample column s
+        const uint32_t m0 = aes_quad<HNR>(aes, key->hp_rk, col, s);
+        const uint32_t m1 = qperm<kQuadBcast1>(m0);  // column 1 (mask byte 4 is its byte 0)
+        if (s == 0) {
+            if (flags & QPP_HP_MASK_OUT) {
+                uint8_t *mo = masks + 5 * (size_t)pkt_index;
+                mo[0] = (uint8_t)m0; mo[1] = (uint8_t)(m0 >> 8); mo[2] = (uint8_t)(m0 >> 16);
+                mo[3] = (uint8_t)(m0 >> 24); mo[4] = (uint8_t)m1;
+            }
+            const uint32_t hdr_len = aad_len - pn_len;
+            if (flags & QPP_HP_APPLY) hdr_apply(at(dt.off), hdr_len, pn_len, hdr_load(at(dt.off), hdr_len), m0, m1);
+        }
+        hp_done = true;
+    };
+
     // one group: slots t = 16 g + 4 k + s, k < NBG; slot t holds counter t + 1 and ciphertext block t - 1
     auto group = [&](auto nbc, int g) {
         constexpr int NBG = decltype(nbc)::value;
@@ -201,6 +264,30 @@ __device__ __forceinline__ void quad_packet(const AesLds &aes, const GhashT<true
         const int t0 = 16 * g + (int)s;
         uint4 ks[NBG];
         const uint32_t c0 = (uint32_t)t0 + 1u;
+#if QPP_QUAD_TOUCH
+        // Touch the next group's 256 payload bytes (one dword per lane, 64 B apart) before this group's keystream, so
+        // that its loads -- issued after the keystream, where their latency is exposed -- find the lines in L2.  The
+        // value is folded into `touch`, which nothing reads (kept alive by the asm below).
+        uint32_t tv = 0;
+        if (g + 1 < G) {
+            const uint32_t o = 16u * (uint32_t)(16 * (g + 1) - 1) + 64u * s;
+            __builtin_memcpy(&tv, at(pay + (o + 4 <= len + 16 ? o : 0u)), 4);
+        }
+#endif
+#if QPP_QUAD_EARLY_LOADS
+        // payload loads issued before the keystream: their latency passes under the AES pipeline
+        uint4 in[NBG];
+        if (inner) {
+            const uint32_t b = pay + 16 * (uint32_t)(t0 - 1);
+#pragma unroll
+            for (int k = 0; k < NBG; k++) in[k] = ld16(at(b + 64 * k));
+        } else {
+#pragma unroll
+            for (int k = 0; k < NBG; k++) {
+                const int j = t0 + 4 * k - 1;
+                in[k] = ld16(at(pay + (j >= 0 && 16 * j <= (int)len ? 16 * (uint32_t)j : 0u)));
+            }
+        }
         // The nonce words are laundered where the loop uses them (a new page; the straddling group): left alone, the
         // compiler hoisted the page build's first-round lookups addresses out of the loop as loop invariants and
         // spilled them (16 scratch accesses per group in the open kernel).
@@ -210,7 +297,25 @@ __device__ __forceinline__ void quad_packet(const AesLds &aes, const GhashT<true
                 asm volatile("" : "+v"(m0), "+v"(m1), "+v"(m2));
                 pg.build(aes, rk, m0, m1, m2, c0 >> 8);
             }
-            ctr_keystream_pipe<NR, NBG, 4>(aes, pg, rk, c0, ks);
+            QPP_QUAD_PIPE<NR, NBG, 4>(aes, pg, rk, c0, ks);
+        } else {
+            asm volatile("" : "+v"(m0), "+v"(m1), "+v"(m2));
+            static_for<NBG>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                ks[k] = aes.encrypt<NR>(make_uint4(m0, m1, m2, bswap32(c0 + 4 * k)), rk);
+            });
+        }
+#else
+        // The nonce words are laundered where the loop uses them (a new page; the straddling group): left alone, the
+        // compiler hoisted the page build's first-round lookups addresses out of the loop as loop invariants and
+        // spilled them (16 scratch accesses per group in the open kernel).
+        uint32_t m0 = n0, m1 = n1, m2 = n2;
+        if ((g & 15) != 15) {  // uniform: no lane's counters straddle a 256-block page
+            if ((c0 >> 8) != pg.page) {
+                asm volatile("" : "+v"(m0), "+v"(m1), "+v"(m2));
+                pg.build(aes, rk, m0, m1, m2, c0 >> 8);
+            }
+            QPP_QUAD_PIPE<NR, NBG, 4>(aes, pg, rk, c0, ks);
         } else {
             asm volatile("" : "+v"(m0), "+v"(m1), "+v"(m2));
             static_for<NBG>([&](auto kc) {
@@ -232,18 +337,37 @@ __device__ __forceinline__ void quad_packet(const AesLds &aes, const GhashT<true
                 in[k] = ld16(at(pay + (j >= 0 && 16 * j <= (int)len ? 16 * (uint32_t)j : 0u)));
             }
         }
+#endif
         uint4 out[NBG];
 #pragma unroll
         for (int k = 0; k < NBG; k++) out[k] = in[k] ^ ks[k];
         if constexpr (SEAL) {
             // E_K(J0) (slot 0, lane 0) waits in the tag's place until the tag is known (4 VGPRs fewer across the loop;
             // opening needs the received tag there and recomputes E_K(J0) on the quad at the end instead)
+#if QPP_QUAD_EK_REG
+            if (g == 0) ek0 = ks[0];
+#else
             if (g == 0 && has && s == 0) st16(at(pay + len), ks[0]);
+#endif
         }
         if (inner) {
             const uint32_t b = pay + 16 * (uint32_t)(t0 - 1);
+#if QPP_QUAD_DEFER
+            // The 64-byte segment that straddles two groups' ciphertext gets its two parts from stores a whole group
+            // apart, and in between L2 had often written the first part back on its own (a second partial write of
+            // the segment).  So between interior groups the last 64 bytes (blocks k = 3) wait for the next group and
+            // go out right after its first 64.
+            st_payload(at(b), out[0]);
+            if (held_ok) st_payload(at(b - 64), held);
 #pragma unroll
-            for (int k = 0; k < NBG; k++) st16_nt(at(b + 64 * k), out[k]);
+            for (int k = 1; k < NBG - 1; k++) st_payload(at(b + 64 * k), out[k]);
+            held_ok = interior(g + 1) && (g + 1 < G - 1 || tail_slots > 12);  // uniform: the next group is interior
+            if (held_ok) held = out[NBG - 1];
+            else st_payload(at(b + 64 * (NBG - 1)), out[NBG - 1]);
+#else
+#pragma unroll
+            for (int k = 0; k < NBG; k++) st_payload(at(b + 64 * k), out[k]);
+#endif
 #pragma unroll
             for (int k = 0; k < NBG; k++) w = gh.mulx(w, SEAL ? out[k] : in[k]);
         } else {
@@ -251,7 +375,7 @@ __device__ __forceinline__ void quad_packet(const AesLds &aes, const GhashT<true
             for (int k = 0; k < NBG; k++) {
                 const int t = t0 + 4 * k, j = t - 1;
                 const bool full = t >= 1 && j < nfull, part = rem && j == nfull, lenslot = has && t == m + 1;
-                if (full) st16_nt(at(pay + 16 * (uint32_t)j), out[k]);
+                if (full) st_payload(at(pay + 16 * (uint32_t)j), out[k]);
                 if (part) st_bytes(at(pay + 16 * (uint32_t)j), keep_bytes(out[k], (uint32_t)rem), (uint32_t)rem);
                 // the length block rides in the slot after the payload when the group reaches it
                 const uint4 x = lenslot ? lenblk() : part ? keep_bytes(SEAL ? out[k] : in[k], (uint32_t)rem)
@@ -260,6 +384,12 @@ __device__ __forceinline__ void quad_packet(const AesLds &aes, const GhashT<true
                 len_done = len_done || lenslot;
             }
         }
+#if QPP_QUAD_TOUCH
+        asm volatile("" ::"v"(tv));
+#endif
+#if QPP_QUAD_HP_EARLY
+        if (SEAL && g == 0) hp_early(out[0]);
+#endif
     };
     for (int g = 0; g + 1 < G; g++) group(std::integral_constant<int, 4>{}, g);
     if (G > 0) {  // the last group with as few counter blocks per lane as its longest packet needs
@@ -284,13 +414,15 @@ __device__ __forceinline__ void quad_packet(const AesLds &aes, const GhashT<true
     y = y ^ qperm<kQuadSwap2>(y);
 
     if constexpr (SEAL) {
+#if QPP_QUAD_EK_REG
+        if (has && s == 0) st16(at(pay + len), y ^ ek0);  // tag = GHASH ^ E_K(J0)
+#else
         if (has && s == 0) st16(at(pay + len), y ^ ld16(at(pay + len)));  // tag = GHASH ^ E_K(J0) (stashed at group 0)
-        constexpr int HNR = NR == 10 ? 10 : 14;
-        const bool want_hp = (flags & (QPP_HP_MASK_OUT | QPP_HP_APPLY)) != 0;
+#endif
         const qpp_pkt dt = reload_desc(dptr);
         const uint32_t pn_len = dt.pn_len;
         const bool hp = want_hp && has && pn_len >= 1 && pn_len <= 4 && len >= 4 - pn_len;  // quad-uniform
-        if (hp) {
+        if (hp && !hp_done) {  // short payloads: the sample runs into the tag
             // header-protection sample = ciphertext||tag bytes [4 - pn_len, 20 - pn_len) (payload.rs:151-169), column s
             // read back (the quad's lanes stored the blocks and lane 0 the tag: a wavefront fence orders them first;
             // read back rather than kept in registers across the loop); the mask AES on the quad (aes_quad)
@@ -338,17 +470,14 @@ __device__ __forceinline__ void quad_packet(const AesLds &aes, const GhashT<true
     }
 }
 
-// One workgroup per CU (grid = CUs) over an equal slice of the key-sorted packets, as aes_gcm_kernel (same plan meta,
+// One workgroup per CU (grid = CUs) over an equal slice of the key-sorted packets (plan meta,
 // same single-key mode), 256 packets per pass.
 template <bool SEAL, int NR>
-__global__ __launch_bounds__(kQuadWG) void aes_gcm_quad_kernel(const DevKey *__restrict__ keys,
-                                                              const qpp_pkt *__restrict__ descs,
-                                                              const uint32_t *__restrict__ perm,
-                                                              const WorkItem *__restrict__ work,
-                                                              const uint32_t *__restrict__ meta,
-                                                              uint8_t *__restrict__ arena, uint8_t *masks,
-                                                              int8_t *status, uint32_t flags, uint32_t single,
-                                                              uint32_t n_single) {
+__device__ __forceinline__ void quad_slices(const DevKey *__restrict__ keys, const qpp_pkt *__restrict__ descs,
+                                            const uint32_t *__restrict__ perm, const WorkItem *__restrict__ work,
+                                            const uint32_t *__restrict__ meta, uint8_t *__restrict__ arena,
+                                            uint8_t *masks, int8_t *status, uint32_t flags, uint32_t single,
+                                            uint32_t n_single) {
     const bool one = single != 0xffffffffu;  // uniform
     uint32_t i_lo = 0, i_hi = 1, p0 = 0, n = n_single;
     if (!one) {
@@ -371,12 +500,16 @@ __global__ __launch_bounds__(kQuadWG) void aes_gcm_quad_kernel(const DevKey *__r
     const GhashT<true> gh = GhashT<true>::make();
     const uint32_t s = threadIdx.x & 3u, q = threadIdx.x >> 2;
     for (; lo < hi; i++) {  // key segments of the slice
-        const WorkItem w = one ? WorkItem{single, 0u, n, (uint32_t)NR} : work[i];
+        WorkItem w = one ? WorkItem{single, 0u, n, (uint32_t)NR} : work[i];
+        // (uniform; the fused receive kernel's work items are written by the same launch, so not scalar-loaded)
+        w.key = __builtin_amdgcn_readfirstlane(w.key);
+        w.begin = __builtin_amdgcn_readfirstlane(w.begin);
+        w.count = __builtin_amdgcn_readfirstlane(w.count);
         const uint32_t end = min(hi, w.begin + w.count);
         const DevKey *__restrict__ key = keys + w.key;
         __syncthreads();  // every wave is done with the previous segment's tables
         quad_tables(key);
-        for (uint32_t t0 = lo; t0 < end; t0 += kQuadPkts) {
+        for (uint32_t t0 = lo; t0 < end; t0 += kQuadWG<NR> / 4) {
             const uint32_t t = t0 + q;
             const bool real = t < end;
             const uint32_t pi = one ? (real ? t : lo) : perm[real ? t : lo];
@@ -393,12 +526,172 @@ __global__ __launch_bounds__(kQuadWG) void aes_gcm_quad_kernel(const DevKey *__r
 }
 
 template <bool SEAL, int NR>
+__global__ __launch_bounds__(kQuadWG<NR>) void aes_gcm_quad_kernel(const DevKey *__restrict__ keys,
+                                                              const qpp_pkt *__restrict__ descs,
+                                                              const uint32_t *__restrict__ perm,
+                                                              const WorkItem *__restrict__ work,
+                                                              const uint32_t *__restrict__ meta,
+                                                              uint8_t *__restrict__ arena, uint8_t *masks,
+                                                              int8_t *status, uint32_t flags, uint32_t single,
+                                                              uint32_t n_single) {
+    quad_slices<SEAL, NR>(keys, descs, perm, work, meta, arena, masks, status, flags, single, n_single);
+}
+
+// ---------------------------------------------------------------- fused receive path, any key mix, ONE launch
+// crypto::unprotect + crypto::decrypt for a GRO batch (quic/s2n-quic-core/src/crypto/packet_protection.rs; the key by
+// the key-phase bit, crypto/application/keyset.rs:113-143), whatever the connections' keys, as one cooperative
+// launch in four phases separated by grid barriers:
+//   A. each workgroup unprotects its slice of rx[] (one lane per packet: rx_unprotect_one -- HP mask, first byte and
+//      PN unmasked in place, PN expanded, key chosen), writes descs_out[], and counts its packets per chosen key in
+//      LDS (the GHASH table area is free until phase D);
+//   B. workgroup 0 turns the global counts into each key's first perm index and one work item per key;
+//   C. each workgroup reserves a block per key (one atomic per key it saw) and scatters its packets into perm[];
+//   D. the quad open over the key-sorted perm, exactly as aes_gcm_quad_kernel runs a planned batch.
+// It replaces unprotect_kernel + the three plan launches + the open launch (tests/test_gpu_rx_fused.py: bit-exact
+// against that path and the oracle).  A barrier that does not complete within a second (a workgroup that never became
+// resident) makes every workgroup leave: its packets bound for the open phase report INTERNAL_ERROR, payload untouched.
+constexpr uint32_t kRxCtl = kQLdsPow;     // LDS: barrier verdict; [kRxCtl + 64, +6 KiB) phase B scan sums
+constexpr uint32_t kRxHistMax = 16384;    // LDS bins [0, 64 KiB): keys per workgroup in phases A-C
+constexpr uint64_t kRxBarrierTicks = 100000000ull;  // 1 s of s_memrealtime (100 MHz)
+constexpr int8_t kRxOpen = 0x7f;  // status of a packet bound for the open phase (never a final status)
+
+// scratch (device, words): [0] barrier count, [1] failed | counts[key_cap] @16 | cursor[key_cap] | meta[4] | work[]
+// (the first 16 + 2 key_cap words are zeroed before each launch)
+__device__ bool rx_grid_sync(uint32_t *scratch, uint32_t target) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t ok = 1;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __hip_atomic_fetch_add(&scratch[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(&scratch[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            if (__hip_atomic_load(&scratch[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ||
+                __builtin_amdgcn_s_memrealtime() - t0 > kRxBarrierTicks) {
+                __hip_atomic_store(&scratch[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok = 0;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        lds_st32(kRxCtl, ok);
+    }
+    __syncthreads();
+    return lds_ld32(kRxCtl) != 0;
+}
+
+template <int NR>
+__global__ __launch_bounds__(kQuadWG<NR>) void aes_gcm_quad_rx_kernel(const DevKey *__restrict__ keys,
+                                                                 uint32_t key_cap, const qpp_rx_pkt *__restrict__ rx,
+                                                                 uint32_t n, uint8_t *arena, qpp_pkt *descs_out,
+                                                                 int8_t *status, uint32_t *scratch, uint32_t *perm) {
+    uint32_t *counts = scratch + 16, *cursor = counts + key_cap, *meta = cursor + key_cap;
+    WorkItem *work = (WorkItem *)(meta + 4);  // 16-byte aligned: key_cap is even
+    const uint32_t tid = threadIdx.x, nt = blockDim.x;
+    const uint32_t bins = min(key_cap, kRxHistMax);  // (the launch requires key_cap <= kRxHistMax)
+    build_aes_tables(kLdsAes);
+    for (uint32_t i = tid; i < bins; i += nt) lds_st32(4 * i, 0);
+    __syncthreads();
+    const AesLds aes = make_aes(kLdsAes);
+    // A: unprotect the slice, count per chosen key
+    const uint32_t P = (n + gridDim.x - 1) / gridDim.x;
+    const uint32_t lo = min(n, blockIdx.x * P), hi = min(n, lo + P);
+    // A packet goes to the open phase when its chosen key is a live packet key of this launch's AES size; the others
+    // get INTERNAL_ERROR (descs_out as unprotect_kernel writes it: the multi-launch path's plan refuses them
+    // likewise).  The verdict is kept in status (kRxOpen) for phase C, which must scatter exactly the packets phase A
+    // counted (a record retired meanwhile must not change it); phase D overwrites kRxOpen.
+    for (uint32_t t = lo + tid; t < hi; t += nt) {
+        const qpp_pkt d = rx_unprotect_one(aes, keys, key_cap, rx[t], arena, status, t);
+        if (!(d.flags & QPP_PKT_SKIP)) {
+            const DevKey *__restrict__ k = keys + d.key_idx;  // (< key_cap: checked by rx_unprotect_one)
+            const bool open = k->live == 1 && k->nr == (uint32_t)NR;
+            status[t] = open ? kRxOpen : (int8_t)QPP_INTERNAL_ERROR;
+            if (open) lds_add32(4 * d.key_idx, 1u);
+        }
+        descs_out[t] = d;
+    }
+    // a barrier that timed out: this workgroup's packets that were to be opened report INTERNAL_ERROR, untouched
+    auto bail = [&]() {
+        for (uint32_t t = lo + tid; t < hi; t += nt)
+            if (status[t] == kRxOpen) status[t] = QPP_INTERNAL_ERROR;
+    };
+    __syncthreads();
+    for (uint32_t k = tid; k < bins; k += nt) {
+        const uint32_t c = lds_ld32(4 * k);
+        if (c) __hip_atomic_fetch_add(&counts[k], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (!rx_grid_sync(scratch, gridDim.x)) return bail();
+    // B: workgroup 0 -- each key's first perm index (cursor) and one work item per key with packets
+    if (blockIdx.x == 0) {
+        const uint32_t chunk = (key_cap + nt - 1) / nt, k0 = min(key_cap, tid * chunk), k1 = min(key_cap, k0 + chunk);
+        uint32_t sum = 0, nz = 0;
+        for (uint32_t k = k0; k < k1; k++) {
+            const uint32_t c = counts[k];
+            sum += c;
+            nz += c != 0;
+        }
+        lds_st32(kRxCtl + 64 + 4 * tid, sum);
+        lds_st32(kRxCtl + 64 + 4 * (nt + tid), nz);
+        __syncthreads();
+        if (tid == 0) {  // exclusive scans of the per-thread sums (<= 1024 entries)
+            uint32_t a = 0, b = 0;
+            for (uint32_t i = 0; i < nt; i++) {
+                const uint32_t x = lds_ld32(kRxCtl + 64 + 4 * i), y = lds_ld32(kRxCtl + 64 + 4 * (nt + i));
+                lds_st32(kRxCtl + 64 + 4 * i, a);
+                lds_st32(kRxCtl + 64 + 4 * (nt + i), b);
+                a += x;
+                b += y;
+            }
+            meta[0] = b;                    // work items
+            meta[1] = NR == 10 ? b : 0u;    // AES-128 items (all of them, or none)
+            meta[2] = NR == 10 ? a : 0u;    // AES-128 packets
+            meta[3] = NR == 10 ? 0u : a;    // AES-256 packets
+        }
+        __syncthreads();
+        uint32_t off = lds_ld32(kRxCtl + 64 + 4 * tid), item = lds_ld32(kRxCtl + 64 + 4 * (nt + tid));
+        for (uint32_t k = k0; k < k1; k++) {
+            const uint32_t c = counts[k];
+            cursor[k] = off;
+            if (c) work[item++] = WorkItem{k, off, c, (uint32_t)NR};
+            off += c;
+        }
+    }
+    if (!rx_grid_sync(scratch, 2 * gridDim.x)) return bail();
+    // C: one block of perm per key this workgroup saw, then its packets into it
+    for (uint32_t k = tid; k < bins; k += nt) {
+        const uint32_t c = lds_ld32(4 * k);
+        if (c) lds_st32(4 * k, __hip_atomic_fetch_add(&cursor[k], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    }
+    __syncthreads();
+    for (uint32_t t = lo + tid; t < hi; t += nt)
+        if (status[t] == kRxOpen) perm[lds_add32(4 * descs_out[t].key_idx, 1u)] = t;
+    if (!rx_grid_sync(scratch, 3 * gridDim.x)) return bail();
+    // D: open, key-sorted slices (tables per key segment, as a planned batch)
+    quad_slices<false, NR>(keys, descs_out, perm, work, meta, arena, nullptr, status, 0u, 0xffffffffu, 0u);
+}
+
+template <bool SEAL, int NR>
 void launch_quad(dim3 grid, hipStream_t s, const DevKey *keys, const qpp_pkt *descs, const PlanBuffers &pb,
                  uint8_t *arena, uint8_t *masks, int8_t *status, uint32_t flags, uint32_t single, uint32_t n_single) {
-    hipLaunchKernelGGL((aes_gcm_quad_kernel<SEAL, NR>), grid, dim3(kQuadWG), kLdsMax, s, keys, descs, pb.perm, pb.work,
+    hipLaunchKernelGGL((aes_gcm_quad_kernel<SEAL, NR>), grid, dim3(kQuadWG<NR>), kLdsMax, s, keys, descs, pb.perm, pb.work,
                        pb.n_work, arena, masks, status, flags, single, n_single);
 }
 }  // namespace
+
+uint32_t quad_rx_max_keys() { return kRxHistMax; }
+
+hipError_t launch_aes_gcm_quad_rx(uint32_t nr, uint32_t grid, hipStream_t s, const DevKey *keys, uint32_t key_cap,
+                                  const qpp_rx_pkt *rx, uint32_t n, uint8_t *arena, qpp_pkt *descs_out, int8_t *status,
+                                  uint32_t *scratch, uint32_t *perm) {
+    if (key_cap > kRxHistMax || (key_cap & 1u)) return hipErrorInvalidValue;
+    void *args[] = {&keys, &key_cap, &rx, &n, &arena, &descs_out, &status, &scratch, &perm};
+    // cooperative: the grid barriers need every workgroup resident (one per CU: grid <= the CUs it may use)
+    if (nr == 10)
+        return hipLaunchCooperativeKernel(reinterpret_cast<const void *>(&aes_gcm_quad_rx_kernel<10>), dim3(grid),
+                                          dim3(kQuadWG<10>), args, kLdsMax, s);
+    return hipLaunchCooperativeKernel(reinterpret_cast<const void *>(&aes_gcm_quad_rx_kernel<14>), dim3(grid),
+                                      dim3(kQuadWG<14>), args, kLdsMax, s);
+}
 
 // The quad-layout kernels behind launch_aes_gcm / launch_aes_gcm_single (aes_gcm.hip chooses).  single = 0xffffffff:
 // planned batch (pb), else the one live AES key's slot (descs[0, n_single) in order, other slots refused).

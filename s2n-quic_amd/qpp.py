@@ -28,6 +28,7 @@ HASH_LEN = {1: 32, 2: 48, 3: 32}
 OK, DECODE_ERROR, DECRYPT_ERROR, INTERNAL_ERROR, UNSUPPORTED, DEVICE_ERROR = 0, 1, 2, 3, 4, 5
 ROTATION_NOT_SUPPORTED = 6  # dc open::Error::RotationNotSupported
 HP_MASK_OUT, HP_APPLY, ONLY_AES, ONLY_CHACHA = 0x1, 0x2, 0x10, 0x20
+KEY_BY_CONN = 0x40  # host batches: key_idx = connection index (qpp_ctx_set_conn_keys)
 AES_KERNEL_AUTO, AES_KERNEL_LANE, AES_KERNEL_WAVE = 0, 1, 2
 ENDPOINT_CLIENT, ENDPOINT_SERVER = 0, 1
 
@@ -54,6 +55,8 @@ EXPORTS = [
     "qpp_event_elapsed_ms", "qpp_stream_wait_event", "qpp_unprotect_open_batch", "qpp_pn_truncate", "qpp_pn_expand",
     "qpp_key_new_batch", "qpp_txq_create", "qpp_txq_destroy", "qpp_txq_ring", "qpp_txq_push", "qpp_txq_flush",
     "qpp_txq_create_async", "qpp_txq_flush_async", "qpp_txq_poll", "qpp_txq_wait", "qpp_txq_push_descs", "qpp_txq_set_coalesce", "qpp_txq_push_scatter",
+    "qpp_txq_create_persistent", "qpp_txq_info", "qpp_txq_server_time", "qpp_ctx_set_conn_keys",
+    "qpp_txq_server_stamps",
     "qpp_txq_pending", "qpp_memcpy_d2d", "qpp_ctx_set_burst_max", "qpp_dc_key_new", "qpp_dc_seal", "qpp_dc_open",
     "qpp_dc_open_in_place", "qpp_ctx_key_slots", "qpp_key_new_pair", "qpp_key_update_batch", "qpp_initial_keys_pair",
     "qpp_header_key_new", "qpp_header_key_new_raw", "qpp_header_key_free", "qpp_header_key_slot",
@@ -146,6 +149,11 @@ def lib():
             "qpp_txq_wait": (ctypes.c_int, [vp, u64]),
             "qpp_txq_push_descs": (ctypes.c_int, [vp, vp, sz]),
             "qpp_txq_push_scatter": (ctypes.c_int, [vp, vp, u64, sz, sz, sz, sz, vp, sz]),
+            "qpp_txq_create_persistent": (ctypes.c_int, [vp, sz, sz, ctypes.POINTER(vp)]),
+            "qpp_txq_info": (ctypes.c_int, [vp, ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u64)]),
+            "qpp_txq_server_time": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double)]),
+            "qpp_ctx_set_conn_keys": (ctypes.c_int, [vp, vp, sz]),
+            "qpp_txq_server_stamps": (ctypes.c_int, [vp, vp]),
             "qpp_txq_set_coalesce": (ctypes.c_int, [vp, sz]),
             "qpp_txq_pending": (sz, [vp]),
             "qpp_memcpy_d2d": (ctypes.c_int, [vp, vp, vp, sz, vp]),
@@ -317,6 +325,11 @@ class Context:
 
     def set_host_pipe(self, chunk_packets, chunk_bytes, slots):
         self._check(lib().qpp_ctx_set_host_pipe(self.handle, chunk_packets, chunk_bytes, slots), "set_host_pipe")
+
+    def set_conn_keys(self, slots):
+        """qpp_ctx_set_conn_keys: slots[c] = the current key slot of connection c (QPP_KEY_BY_CONN host batches)"""
+        slots = np.ascontiguousarray(slots, dtype=np.uint32)
+        self._check(lib().qpp_ctx_set_conn_keys(self.handle, slots.ctypes.data, len(slots)), "set_conn_keys")
 
     def host_submit(self, descs, arena, masks=None, status=None, flags=0, ops=OP_SEAL | OP_OPEN):
         """qpp_host_batch_submit over host numpy arrays (arena ideally from host_alloc); returns the ticket.
@@ -650,9 +663,13 @@ def pn_expand(largest_acked, truncated, pn_len):
 class TxQueue:
     """qpp_txq: deferred Key::encrypt + header protection over a pinned ring (the GSO segment buffer)."""
 
-    def __init__(self, ctx, ring_bytes, max_packets, in_flight=1):
+    def __init__(self, ctx, ring_bytes, max_packets, in_flight=1, persistent=False):
+        """persistent: qpp_txq_create_persistent (one flush in flight, posted to a resident server kernel)"""
         h = vp()
-        rc = lib().qpp_txq_create_async(ctx.handle, ring_bytes, max_packets, in_flight, ctypes.byref(h))
+        if persistent:
+            rc = lib().qpp_txq_create_persistent(ctx.handle, ring_bytes, max_packets, ctypes.byref(h))
+        else:
+            rc = lib().qpp_txq_create_async(ctx.handle, ring_bytes, max_packets, in_flight, ctypes.byref(h))
         if rc != OK:
             raise QppError(rc, "qpp_txq_create")
         self.handle, self.ctx = h.value, ctx
@@ -675,6 +692,22 @@ class TxQueue:
                                         ctypes.cast(buf, vp) if extra else None, len(extra))
         if rc != OK:
             raise QppError(rc, "qpp_txq_push_scatter")
+
+    def info(self):
+        """qpp_txq_info: (flushes sealed by the persistent server, flushes launched, server launches)"""
+        a, b, c = u64(), u64(), u64()
+        rc = lib().qpp_txq_info(self.handle, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
+        if rc != OK:
+            raise QppError(rc, "qpp_txq_info")
+        return a.value, b.value, c.value
+
+    def server_time_us(self):
+        """qpp_txq_server_time: doorbell seen -> completion of the last posted flush, on the server's clock"""
+        t = ctypes.c_double()
+        rc = lib().qpp_txq_server_time(self.handle, ctypes.byref(t))
+        if rc != OK:
+            raise QppError(rc, "qpp_txq_server_time")
+        return t.value
 
     def push_descs(self, descs):
         """qpp_txq_push_descs: a PKT_DTYPE array of ready descriptors in one call"""

@@ -1,6 +1,7 @@
-"""The fused receive kernel (aes_gcm.hip aes_gcm_rx_kernel: unprotect -> PN expand -> open in one launch, used when
-the context's only live packet key is an AES key) against the two-launch path (unprotect_kernel + the plan-free open,
-QPP_RX_FUSED=0) and against the oracle (orc_unprotect_open_batch).
+"""The fused receive kernel (quad.hip aes_gcm_quad_rx_kernel: unprotect -> PN expand -> key-phase choice -> group by
+key -> open, ONE cooperative launch, used when the live packet keys are all of one AES size, however many) against
+the multi-launch path (unprotect_kernel + plan + open, QPP_RX_FUSED=0) and against the oracle
+(orc_unprotect_open_batch).
 
 The batch is what a receiver sees during a key update (quic/s2n-quic-core/src/crypto/application/keyset.rs:113-143):
 short headers of both key phases and long headers, PNs truncated against the largest acknowledged PN, tampered tags,
@@ -115,6 +116,67 @@ def test_fused_rx_equals_two_launch_path_and_oracle(ctx, suite, monkeypatch):
         k0.free()
     finally:
         ctx.set_burst_max(16384)
+
+
+@pytest.mark.parametrize("suite", [1, 2])
+def test_fused_rx_many_keys(suite, monkeypatch):
+    """64 live packet keys (32 connections, both key phases live: a key update in progress everywhere), 4 more
+    connections whose phase-1 key is already dropped, packets of all of them interleaved at random in one GRO batch:
+    one fused launch (in-kernel group-by on the phase-chosen key) equals the multi-launch path bit for bit and the
+    oracle on every packet (refused phase-1 packets of the 4 connections: INTERNAL_ERROR, payload untouched)."""
+    rng = np.random.default_rng(90 + suite)
+    ctx = qpp.Context(0)
+    ctx.set_burst_max(0)
+    ctx.set_aes_kernel(qpp.AES_KERNEL_LANE)  # the throughput kernel's regime at test size (fused path's condition)
+    try:
+        pairs = []
+        for c in range(36):
+            k0 = ctx.key(suite, rng.integers(0, 256, qpp.HASH_LEN[suite], dtype=np.uint8).tobytes())
+            pairs.append((k0, k0.derive_next_key()))
+        mats = [(suite, *k.material()) for pair in pairs for k in pair]
+        for c in range(32, 36):
+            pairs[c][1].free()
+        n = 6000
+        chunks, rx, orx = [], [], []
+        off = 0
+        for i in range(n):
+            c = int(rng.integers(0, 36))
+            largest = int(rng.integers(0, 2**40))
+            pn = largest + int(rng.integers(0, 300))
+            _, _, pn_len = orc.truncate_pn(pn, largest)
+            phase = int(rng.integers(0, 2))
+            header = bytes([0x40 | (phase << 2) | (pn_len - 1)]) + rng.integers(0, 256, 16, dtype=np.uint8).tobytes()
+            payload = rng.integers(0, 256, int(rng.integers(1, 1400)), dtype=np.uint8).tobytes()
+            _, k, iv, hp = mats[2 * c + phase]
+            rc, pkt = orc.protect_packet(suite, k, iv, hp, pn, header, pn_len, payload)
+            pkt = bytearray(pkt)
+            if i % 19 == 4:
+                pkt[-1 - i % 16] ^= 0x01  # tampered -> DECRYPT_ERROR
+            chunks.append(bytes(pkt) + bytes(int(rng.integers(0, 5))))
+            rx.append((largest, (pairs[c][0].slot, pairs[c][1].slot if c < 32 else pairs[c][1].slot), off,
+                       len(header), len(pkt)))
+            orx.append((largest, (2 * c, 2 * c + 1), off, len(header), len(pkt)))
+            off += len(chunks[-1])
+        rx = np.array(rx, dtype=qpp.RX_DTYPE)
+        orx = np.array(orx, dtype=qpp.RX_DTYPE)
+        arena = np.frombuffer(b"".join(chunks) + bytes(64), dtype=np.uint8).copy()
+        a_f, o_f, s_f = _run(ctx, rx, arena, monkeypatch, fused=True)
+        a_2, o_2, s_2 = _run(ctx, rx, arena, monkeypatch, fused=False)
+        assert (s_f == s_2).all(), "status differs between the fused and the multi-launch path"
+        assert (a_f == a_2).all(), "arena differs between the fused and the multi-launch path"
+        assert (o_f.view(np.uint8) == o_2.view(np.uint8)).all(), "descriptors differ"
+        want_arena = arena.copy()
+        want_out, want_st = orc.unprotect_open_batch(orc.make_keys(mats), orx, want_arena)
+        want_st = np.array(want_st, dtype=np.int8)
+        dropped = np.isin(want_out["key_idx"], [2 * c + 1 for c in range(32, 36)])
+        assert dropped.sum() > 100 and (s_f[dropped] == qpp.INTERNAL_ERROR).all()
+        assert (s_f[~dropped] == want_st[~dropped]).all()
+        assert (s_f == 0).sum() > n * 3 // 4 and (s_f == qpp.DECRYPT_ERROR).any()
+        for i in np.nonzero(~dropped)[0]:
+            o, ln = int(rx[i]["off"]), int(rx[i]["len"])
+            assert (a_f[o:o + ln] == want_arena[o:o + ln]).all(), i
+    finally:
+        ctx.close()
 
 
 def test_fused_chacha_rx_many_keys(monkeypatch):

@@ -1,0 +1,185 @@
+"""Persistent transmit-queue server (qpp_txq_create_persistent; burst.hip txq_server_kernel), on the GPU.
+
+The queue's flushes are posted through a doorbell in pinned memory to a resident kernel instead of launched
+(quic/s2n-quic-platform/src/socket/io/tx.rs:204-268 flushes the GSO segments; endpoint/mod.rs:158 calls it per
+wakeup).  Every flushed packet must equal crypto::encrypt + crypto::protect of the oracle
+(quic/s2n-quic-core/src/crypto/packet_protection.rs), whatever path sealed it: the server, or the launched kernels
+that take FIPS-gated and ChaCha20-Poly1305 flushes.  The lifecycle cases cover what a resident kernel adds: the idle
+exit and restart, key installs between flushes (cached GHASH tables), a key-table growth and a context
+synchronisation while the server runs, and the queue's destruction with it running.
+"""
+import time
+
+import numpy as np
+import pytest
+
+import _oracle as orc
+import qpp
+
+pytestmark = pytest.mark.gpu
+
+STRIDE = 1280
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = qpp.Context(0)
+    yield c
+    c.close()
+
+
+def _fill(q, rng, keys, n, pn0, largest, base=0, sizes=(1, 1200)):
+    """n packets pushed into the ring at base + i * STRIDE (key i % len(keys)); returns [(off, protected)]"""
+    want = []
+    for i in range(n):
+        k = keys[i % len(keys)]
+        pn = pn0 + i
+        trunc, pn_len = qpp.pn_truncate(pn, largest)
+        header = bytes([0x40 | (pn_len - 1)]) + rng.integers(0, 256, 16, dtype=np.uint8).tobytes()
+        payload = rng.integers(0, 256, int(rng.integers(max(sizes[0], 4 - pn_len), sizes[1])), dtype=np.uint8).tobytes()
+        pkt = header + trunc.to_bytes(pn_len, "big") + payload
+        off = base + i * STRIDE
+        q.ring[off:off + len(pkt)] = np.frombuffer(pkt, dtype=np.uint8)
+        q.push(k, pn, off, len(header), pn_len, len(payload))
+        kk, iv, hp = k.material()
+        want.append((off, orc.protect_packet(k.suite, kk, iv, hp, pn, header, pn_len, payload)[1]))
+    return want
+
+
+def _check(q, want):
+    for off, p in want:
+        assert q.ring[off:off + len(p)].tobytes() == p
+
+
+def test_server_bursts_bit_exact(ctx, monkeypatch):
+    """64-packet bursts of one AES-128 key, 30 flushes: all sealed by one server launch, bit-exact"""
+    monkeypatch.setenv("QPP_TXQ_SERVER_IDLE_MS", "4000")  # (the oracle between flushes must not look like idling)
+    rng = np.random.default_rng(71)
+    k = ctx.key(1, rng.integers(0, 256, 32, dtype=np.uint8).tobytes())
+    q = qpp.TxQueue(ctx, 64 * STRIDE, 64, persistent=True)
+    largest = int(rng.integers(0, 2**40))
+    for f in range(30):
+        want = _fill(q, rng, [k], 64, largest + 1 + 64 * f, largest + 64 * f, sizes=(1000, 1200))
+        q.flush()
+        _check(q, want)
+    served, launched, starts = q.info()
+    assert (served, launched, starts) == (30, 0, 1)
+    q.close()
+    k.free()
+
+
+def test_server_many_keys_both_sizes(ctx):
+    """AES-128 and AES-256 keys interleaved, 700 packets of 1..1200 B in one flush (several items per workgroup,
+    key changes inside a workgroup), then a ChaCha20-Poly1305 packet in the next flush: launched path, same bytes"""
+    rng = np.random.default_rng(72)
+    keys = [ctx.key(s, rng.integers(0, 256, qpp.HASH_LEN[s], dtype=np.uint8).tobytes()) for s in (1, 2, 1, 2, 1)]
+    q = qpp.TxQueue(ctx, 700 * STRIDE, 700, persistent=True)
+    largest = int(rng.integers(0, 2**40))
+    want = _fill(q, rng, keys, 700, largest + 1, largest)
+    q.flush()
+    _check(q, want)
+    assert q.info()[:2] == (1, 0)
+    ck = ctx.key(3, rng.integers(0, 256, 32, dtype=np.uint8).tobytes())
+    want = _fill(q, rng, keys[:2] + [ck], 90, largest + 701, largest + 700)
+    q.flush()
+    _check(q, want)
+    assert q.info()[:2] == (1, 1)
+    q.close()
+    for k in keys + [ck]:
+        k.free()
+
+
+def test_server_key_changes_between_flushes(ctx):
+    """a key freed and a new one created between flushes (the slot is reused): the server's cached GHASH tables of
+    the slot must not survive the install (key epoch in the doorbell)"""
+    rng = np.random.default_rng(73)
+    q = qpp.TxQueue(ctx, 64 * STRIDE, 64, persistent=True)
+    largest = 1000
+    for f in range(6):
+        k = ctx.key(1 if f % 2 else 2, rng.integers(0, 256, 32 if f % 2 else 48, dtype=np.uint8).tobytes())
+        want = _fill(q, rng, [k], 64, largest + 1, largest)
+        q.flush()
+        _check(q, want)
+        k.free()
+        largest += 64
+    assert q.info()[0] == 6
+    q.close()
+
+
+def test_server_idle_exit_and_restart(ctx, monkeypatch):
+    """with a 5 ms idle timeout the server leaves between flushes 50 ms apart and the next flush starts it again"""
+    monkeypatch.setenv("QPP_TXQ_SERVER_IDLE_MS", "5")
+    rng = np.random.default_rng(74)
+    k = ctx.key(1, rng.integers(0, 256, 32, dtype=np.uint8).tobytes())
+    q = qpp.TxQueue(ctx, 64 * STRIDE, 64, persistent=True)
+    for f in range(3):
+        want = _fill(q, rng, [k], 64, 100 + 64 * f, 99 + 64 * f)
+        q.flush()
+        _check(q, want)
+        time.sleep(0.05)
+    served, launched, starts = q.info()
+    assert served == 3 and launched == 0 and starts == 3
+    q.close()
+    k.free()
+
+
+def test_server_async_tickets_and_context_sync(ctx):
+    """flush_async + poll + wait on the server path; a context synchronisation (which stops the server) and a key
+    table growth (64 -> 128+ slots, which moves the table) between flushes"""
+    rng = np.random.default_rng(75)
+    k = ctx.key(1, rng.integers(0, 256, 32, dtype=np.uint8).tobytes())
+    q = qpp.TxQueue(ctx, 128 * STRIDE, 64, persistent=True)
+    want = _fill(q, rng, [k], 64, 5000, 4999)
+    t = q.flush_async()
+    while not q.poll(t):
+        pass
+    q.wait(t)
+    _check(q, want)
+    ctx.synchronize()
+    want = _fill(q, rng, [k], 64, 5064, 5063, base=64 * STRIDE)
+    t = q.flush_async()
+    more = [ctx.key(1, rng.integers(0, 256, 32, dtype=np.uint8).tobytes()) for _ in range(140)]  # grows the table
+    q.wait(t)
+    _check(q, want)
+    want = _fill(q, rng, [more[-1], k], 64, 6000, 5999)
+    q.flush()
+    _check(q, want)
+    served, launched, starts = q.info()
+    assert served == 3 and launched == 0 and starts >= 2
+    q.close()
+    for x in more + [k]:
+        x.free()
+
+
+def test_server_fips_flush_takes_launched_path(ctx):
+    """a live FIPS key sends the flush down the launched path (its nonce-order gate), results unchanged"""
+    rng = np.random.default_rng(76)
+    ctx.set_fips(True)
+    k = ctx.key(1, rng.integers(0, 256, 32, dtype=np.uint8).tobytes())
+    ctx.set_fips(False)
+    q = qpp.TxQueue(ctx, 64 * STRIDE, 64, persistent=True)
+    # pn 256..319: given = pn ^ (first pn) runs 0..63, strictly increasing, so the gate passes every packet
+    # (aws-lc's TLS 1.3 nonce rule, quic/s2n-quic-crypto/src/aead/fips.rs:13-60; orc_fips_seal_ok agrees)
+    state = orc.fips_states(1)
+    _, iv, _ = k.material()
+    assert all(orc.lib().orc_fips_seal_ok(state, orc._buf(orc.nonce(iv, pn))) for pn in range(256, 320))
+    want = _fill(q, rng, [k], 64, 256, 255)
+    q.flush()
+    _check(q, want)
+    assert q.info()[:2] == (0, 1)
+    q.close()
+    k.free()
+
+
+def test_server_destroy_while_running(ctx):
+    """closing a queue whose server runs (just after a flush) stops it; a second queue then works"""
+    rng = np.random.default_rng(77)
+    k = ctx.key(1, rng.integers(0, 256, 32, dtype=np.uint8).tobytes())
+    for r in range(2):
+        q = qpp.TxQueue(ctx, 64 * STRIDE, 64, persistent=True)
+        want = _fill(q, rng, [k], 64, 9000 + 64 * r, 8999 + 64 * r)
+        t = q.flush_async()
+        q.wait(t)
+        _check(q, want)
+        q.close()
+    k.free()

@@ -1,0 +1,40 @@
+"""Phase stamps of the persistent txq server (build with -DQPP_TXS_TRACE=1, e.g. tools/build_ab.sh sT
+-DQPP_TXS_TRACE=1; run with QPP_LIB=ab/sT.so): median microseconds of each step of a 64 x 1200 B flush, from the
+host's doorbell write to its return from qpp_txq_flush."""
+import ctypes
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, "s2n-quic_amd")
+import qpp
+
+ctx = qpp.Context(0)
+rng = np.random.default_rng(9)
+k = ctx.key(1, rng.integers(0, 256, 32, dtype=np.uint8).tobytes())
+stride, burst = 1248, 64
+q = qpp.TxQueue(ctx, burst * stride, burst, persistent=True)
+q.ring[:] = rng.integers(0, 256, q.ring.size, dtype=np.uint8)
+proto = np.zeros(burst, dtype=qpp.PKT_DTYPE)
+proto["key_idx"] = k.slot
+proto["off"] = np.arange(burst) * stride
+proto["aad_len"], proto["pt_len"], proto["pn_len"] = 21, 1200, 4
+# the mailbox: qpp_txq is opaque; read it through qpp_txq_server_time's neighbour fields via a raw pointer walk is not
+# possible from Python, so the stamps are fetched with ctypes from the library's debug accessor
+lib = qpp.lib()
+rows = []
+for i in range(600):
+    d = proto.copy()
+    d["pn"] = (1 << 20) + i * burst + np.arange(burst, dtype=np.uint64)
+    q.push_descs(d)
+    t0 = time.perf_counter()
+    q.flush()
+    t1 = time.perf_counter()
+    st = (ctypes.c_uint64 * 6)()
+    lib.qpp_txq_server_stamps(q.handle, st)
+    if i >= 100:
+        rows.append([(t1 - t0) * 1e6] + [(st[j] - st[0]) / 100.0 for j in range(1, 6)])
+a = np.median(np.array(rows), axis=0)
+print("median us: host flush %.1f | from doorbell seen: broadcast %.2f item+desc %.2f packets %.2f arrive %.2f done %.2f"
+      % tuple(a))

@@ -51,18 +51,21 @@ LDS_PEAK_CYCLES = 256 * 2.4e9  # LDS-array cycles per second: one array per CU, 
 
 
 def aes_lds_cycles_per_packet(pt, aad, nr, hp=True):
-    """LDS-array cycles aes_gcm_kernel spends per packet (MI355X_MICROARCH.md §LDS: ds_read_b32 2, ds_read_b128 4,
-    ds_write_b128 8 cycles per wave instruction of 64 packets, so per packet 1/64 of that).  Per counter block: the
-    CTR AES with round caching (CtrPage) = 133 T-table lookups for AES-128, 197 for AES-256; counters are issued in
-    groups of NB = 4 from J0 (counter 1); each group block also crosses the staging area (2 ds_read_b128 + 2
-    ds_write_b128).  GHASH: 16 ds_read_b128 per product, one per AAD block, ciphertext block, the length block and the
-    final product.  HP: one uncached AES block.  At P = 1200 this gives 4.49e8 cycles per 1 Mi-packet launch against
-    SQ_LDS_IDX_ACTIVE 4.63e8 incl. 1.2e7 bank-conflict cycles (profiles/r02c_prof_summary.txt)."""
+    """LDS-array cycles aes_gcm_quad_kernel spends per packet (MI355X_MICROARCH.md §LDS: ds_read_b32 2 and
+    ds_read_b128 4 cycles per wave instruction; a wave instruction serves 64 lanes = 16 packets x 4 lanes, so a lane's
+    lookup costs 1/64 of it).  Counter slots: J0 + the payload blocks, in groups of 16 slots (4 per lane), the last
+    group 12 or 16 -- 133 T-table lookups per block for AES-128 (CtrPage round caching), 197 for AES-256.  GHASH: one
+    8-bit-table product (16 ds_read_b128) per AAD block, ciphertext block and the length block, plus each lane's
+    final product by H^e (4-bit tables, 32 ds_read_b128).  HP: one AES over the quad (4 lookups per lane and round)."""
     lookups = 133 if nr == 10 else 197
-    ctr_blocks = -(-((pt + 15) // 16 + 1) // 4) * 4
-    ghash = (aad + 15) // 16 + (pt + 15) // 16 + 2
-    per_wave = 2 * (ctr_blocks * lookups + (16 * nr if hp else 0)) + 4 * 16 * ghash + ctr_blocks * (2 * 4 + 2 * 8)
-    return per_wave / 64.0
+    m = (pt + 15) // 16
+    slots = m + 1  # J0 + payload blocks (the length block rides in a slot of its own only when the group has room)
+    groups = -(-(slots + 1) // 16)
+    tail = slots + 1 - 16 * (groups - 1)
+    ctr = 16 * (groups - 1) + (12 if tail <= 12 else 16)
+    ghash = (aad + 15) // 16 + m + 1
+    lane_instr_cycles = ctr * lookups * 2 + ghash * 16 * 4 + 4 * 32 * 4 + (4 * 4 * nr * 2 if hp else 0)
+    return lane_instr_cycles / 64.0
 
 
 VALU_PEAK_PER_NS = 540.0  # wave-instructions/ns chip-wide for xor/add/alignbit/bitop3/perm/mul_lo (tools/ubench/issue.hip)
@@ -271,11 +274,12 @@ def main():
     try:
         tdb = json.load(open(os.path.join(ROOT, "profiles", "traffic.json")))
         t = tdb.get(f"{args.suite}/{pt}/{args.keys}")
-        if t and n == 1 << 20:
-            traffic = {"bytes": t["traffic_bytes"], "per_alg": round(t["traffic_bytes"] / (n * seal_bytes_per_packet(pt, aad)), 3),
-                       "fetch": t["fetch_bytes"], "write": t["write_bytes"], "source": "profiles/traffic.json: " + t["source"]}
-            if t.get("note"):
-                traffic["note"] = t["note"]
+        if t and n == 1 << 20 and "read_bytes" in t:
+            traffic = {"bytes": t["traffic_bytes"],
+                       "per_alg": round(t["traffic_bytes"] / (n * seal_bytes_per_packet(pt, aad)), 3),
+                       "read": t["read_bytes"], "fetch_size_raw": t["fetch_size_raw_bytes"], "write": t["write_bytes"],
+                       "read_per_alg": t["read_per_alg"], "write_per_alg": t["write_per_alg"],
+                       "source": "profiles/traffic.json: " + t["source"]}
     except (OSError, ValueError, KeyError):
         traffic = None
     value = payload / (t_max / 1e3) / GiB
@@ -301,8 +305,10 @@ def main():
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic["bytes"] if traffic else None,
                 "traffic_detail": traffic,
-                "kernel": (("chacha" if suite == 3 else "aes_gcm") + ("_burst" if n <= burst_max else "")
-                           + "_kernel<seal>" + ("" if suite == 3 else " + plan (per seal call)")),
+                "kernel": ("chacha_burst_kernel<seal>" if suite == 3 and n <= burst_max else
+                           "chacha_kernel<seal>" if suite == 3 else
+                           "aes_gcm_burst_kernel<seal>" if n <= burst_max else
+                           "aes_gcm_quad_kernel<seal>" + (" + plan (per seal call)" if args.keys > 1 else "")),
                 "bytes_per_packet": seal_bytes_per_packet(pt, aad),
             },
             "cpu_baseline": None,
@@ -315,12 +321,13 @@ def main():
                 "model": "bench.chacha_valu_per_packet (SQ_INSTS_VALU); peak measured by tools/ubench/issue.hip",
             }
         if suite != 3 and n > burst_max:
-            # the lane kernel's own bound: the CU's LDS array (T-table + GHASH-table lookups), not HBM
+            # the quad kernel's own bound: the CU's LDS array (T-table + GHASH-table lookups), not HBM
             cyc = n * aes_lds_cycles_per_packet(pt, aad, 10 if suite == 1 else 14)
             out["kernel_roofline"] = {
                 "bound": "lds", "achieved": round(cyc / (seal_avg / 1e3) / 1e9, 1), "peak": LDS_PEAK_CYCLES / 1e9,
                 "unit": "G LDS-array cycles/s", "frac": round(cyc / (seal_avg / 1e3) / LDS_PEAK_CYCLES, 4),
-                "model": "bench.aes_lds_cycles_per_packet, checked against SQ_LDS_IDX_ACTIVE; peak = 256 CUs x 2.4 GHz",
+                "model": "bench.aes_lds_cycles_per_packet (quad layout), checked against SQ_LDS_IDX_ACTIVE; "
+                         "peak = 256 CUs x 2.4 GHz",
             }
         if world == 1 and not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(suite, pt, aad, args.cpu_seconds)

@@ -313,9 +313,11 @@ int qpp_txq_create_persistent(qpp_ctx *ctx, size_t ring_bytes, size_t max_packet
 int qpp_txq_info(const qpp_txq *q, uint64_t *server_flushes, uint64_t *launched_flushes, uint64_t *server_starts);
 /* Persistent queue: microseconds from the server seeing the last posted flush's doorbell to its completion word. */
 int qpp_txq_server_time(const qpp_txq *q, double *us);
-/* Diagnostics: the server's clock (100 MHz) at the last flush's doorbell, workgroup 0's phase stamps (a build with
- * QPP_TXS_TRACE, else 0) and its completion word. */
-int qpp_txq_server_stamps(const qpp_txq *q, uint64_t out[6]);
+/* Diagnostics: the server's clock (100 MHz) at the last flush's doorbell, workgroup 0's phase stamps and shader-clock
+ * cycles over its work (a build with QPP_TXS_TRACE, else 0) and its completion word:
+ * {seen, broadcast, item read, packets done, arrival, done, shader cycles broadcast -> arrival}, then the low words
+ * of wave 0's stamps inside its packet {start, first block in, passes done, lane tree done, HP done}. */
+int qpp_txq_server_stamps(const qpp_txq *q, uint64_t out[12]);
 void qpp_txq_destroy(qpp_txq *q);
 /* Host pointer to the ring (ring_bytes, pinned). */
 uint8_t *qpp_txq_ring(qpp_txq *q);

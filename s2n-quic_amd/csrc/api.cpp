@@ -1721,20 +1721,20 @@ struct qpp_txq {
     std::vector<uint32_t> order;
     std::vector<std::pair<size_t, size_t>> runs;  // DMA path: the flush's contiguous packet byte ranges
     // Persistent server (qpp_txq_create_persistent; burst.hip txq_server_kernel): flushes of AES packets are posted
-    // through a doorbell in pinned memory instead of launched.  One posted flush at a time: its plan (work items and
+    // through per-workgroup slots in pinned memory instead of launched.  One posted flush at a time: its plan (work items and
     // key-sorted descriptors, pinned) is rewritten only once `done` shows the previous one sealed.
     bool persistent = false;
     TxsMail *h_mail = nullptr, *v_mail = nullptr;
-    TxsSync *d_sync = nullptr;
+    TxsSlot *h_slots = nullptr, *v_slots = nullptr;  // one per server workgroup
     WorkItem *h_items = nullptr, *v_items = nullptr;
     qpp_pkt *h_sdesc = nullptr, *v_sdesc = nullptr;
     hipStream_t srv_stream = nullptr;
     bool srv_running = false;           // launched and not yet seen to have ended
     const DevKey *srv_keys = nullptr;   // the key table the running server reads
-    uint32_t srv_seq = 0;               // seq of the last doorbell word written (flush or stop)
+    uint32_t srv_seq = 0;               // seq of the last flush or stop written into the slots
     uint32_t srv_posted = 0;            // seq of the last flush posted (0: none)
     uint64_t srv_first = 0, srv_last = 0;  // its tickets
-    uint32_t srv_epoch = 0;             // key epoch of the doorbell (8 bits)
+    uint32_t srv_epoch = 0;             // key epoch posted with the flushes (8 bits)
     uint64_t srv_key_gen = ~0ull;       // ctx->key_gen the server's epoch stands for
     uint32_t srv_wgs = 16, srv_idle_ticks = 0;
     std::chrono::steady_clock::time_point srv_last_post{};  // the server may leave idle_ticks after it
@@ -1755,15 +1755,21 @@ bool srv_alive(qpp_txq *q) {
 
 // Launches the server unless it runs.  A flush posted but not done (posted while the last server was leaving on its
 // idle timeout) is picked up by the new one: it starts with seq0 != the posted seq.
+// every workgroup has sealed the flush with this seq
+bool srv_done(const qpp_txq *q, uint32_t seq) {
+    for (uint32_t b = 0; b < q->srv_wgs; b++)
+        if (__atomic_load_n(&q->h_slots[b].done, __ATOMIC_ACQUIRE) != seq) return false;
+    return true;
+}
+
 int srv_start(qpp_txq *q) {
     // (no stream query while the server is believed running: a server that left on its idle timeout is found by
     // srv_wait's slow path, which relaunches it behind the posted flush)
     if (q->srv_running) return QPP_OK;
     qpp_ctx *ctx = q->ctx;
-    const bool pending = q->srv_posted && __atomic_load_n(&q->h_mail->done, __ATOMIC_ACQUIRE) != q->srv_posted;
+    const bool pending = q->srv_posted && !srv_done(q, q->srv_posted);
     const uint32_t seq0 = pending ? q->srv_posted - 1u : q->srv_seq;
-    HIP_TRY(ctx, hipMemsetAsync(q->d_sync, 0, sizeof(TxsSync), q->srv_stream));
-    HIP_TRY(ctx, launch_txq_server(ctx->d_keys, ctx->pow, q->v_mail, q->d_sync, q->v_items, q->v_sdesc, q->v_ring,
+    HIP_TRY(ctx, launch_txq_server(ctx->d_keys, ctx->pow, q->v_mail, q->v_slots, q->v_items, q->v_sdesc, q->v_ring,
                                    seq0, q->srv_idle_ticks, q->srv_wgs, q->srv_stream));
     q->srv_running = true;
     q->srv_keys = ctx->d_keys;
@@ -1774,13 +1780,9 @@ int srv_start(qpp_txq *q) {
 // Host wait for the flush with this seq (spinning on the pinned `done` word: no interrupt, no runtime call).
 int srv_wait(qpp_txq *q, uint32_t seq) {
     if (!seq) return QPP_OK;
-    const volatile uint32_t *done = &q->h_mail->done;
     std::chrono::steady_clock::time_point t0{};
     for (uint64_t spin = 0;; spin++) {
-        if (*done == seq) {
-            __atomic_thread_fence(__ATOMIC_ACQUIRE);
-            return QPP_OK;
-        }
+        if (srv_done(q, seq)) return QPP_OK;
         if ((spin & 4095u) == 4095u) {
             if (!srv_alive(q)) RC_TRY(srv_start(q));  // it left (idle) before this flush was seen: a new one takes it
             const auto now = std::chrono::steady_clock::now();
@@ -1799,7 +1801,10 @@ int srv_stop(qpp_txq *q) {
     RC_TRY(srv_wait(q, q->srv_posted));
     if (!srv_alive(q)) return QPP_OK;
     q->srv_seq = srv_next(q->srv_seq);
-    __atomic_store_n(&q->h_mail->doorbell, ((uint64_t)q->srv_seq << 32) | kTxsStop, __ATOMIC_RELEASE);
+    for (uint32_t b = 0; b < q->srv_wgs; b++) {
+        q->h_slots[b].word = kTxsStop;
+        __atomic_store_n(&q->h_slots[b].seq, q->srv_seq, __ATOMIC_RELEASE);
+    }
     HIP_TRY(q->ctx, hipStreamSynchronize(q->srv_stream));
     q->srv_running = false;
     return QPP_OK;
@@ -1893,9 +1898,9 @@ void qpp_txq_destroy(qpp_txq *q) {
         v.erase(std::remove(v.begin(), v.end(), q), v.end());
         if (q->srv_stream) { hipStreamSynchronize(q->srv_stream); hipStreamDestroy(q->srv_stream); }
         if (q->h_mail) hipHostFree(q->h_mail);
-        if (q->d_sync) hipFree(q->d_sync);
+        if (q->h_slots) { secure_zero(q->h_slots, sizeof(TxsSlot) * q->srv_wgs); hipHostFree(q->h_slots); }
         if (q->h_items) hipHostFree(q->h_items);
-        if (q->h_sdesc) { secure_zero(q->h_sdesc, sizeof(qpp_pkt) * q->max_packets * txq_server_waves()); hipHostFree(q->h_sdesc); }
+        if (q->h_sdesc) { secure_zero(q->h_sdesc, sizeof(qpp_pkt) * q->max_packets * kTxsWaves); hipHostFree(q->h_sdesc); }
     }
     for (hipStream_t st : q->streams) hipStreamSynchronize(st);
     if (q->h_ring) { secure_zero(q->h_ring, q->ring_bytes); hipHostFree(q->h_ring); }
@@ -2060,7 +2065,7 @@ static int srv_submit(qpp_txq *q) {
     // a server idle for long may be leaving on its own timeout: never post to it (part of it could miss the flush)
     const auto now = std::chrono::steady_clock::now();
     if (q->srv_running && now - q->srv_last_post > q->srv_host_idle) RC_TRY(srv_stop(q));
-    const uint32_t W = txq_server_waves();
+    const uint32_t W = kTxsWaves;
     std::vector<uint32_t> &ord = q->order;
     ord.resize(n);
     for (uint32_t i = 0; i < n; i++) ord[i] = i;
@@ -2083,8 +2088,24 @@ static int srv_submit(qpp_txq *q) {
     }
     RC_TRY(srv_start(q));
     q->srv_seq = srv_next(q->srv_seq);
-    const uint64_t word = ((uint64_t)q->srv_seq << 32) | ((uint64_t)q->srv_epoch << 24) | items;
-    __atomic_store_n(&q->h_mail->doorbell, word, __ATOMIC_RELEASE);  // the plan and the ring bytes are written
+    const uint32_t seq = q->srv_seq, word = (q->srv_epoch << 24) | items;
+    // each workgroup's slot: its first item and that item's descriptors, all tagged, then the seq (x86 stores are
+    // seen in order; the server also checks every tag, so a read that raced these stores is repeated)
+    for (uint32_t b = 0; b < q->srv_wgs; b++) {
+        TxsSlot &sl = q->h_slots[b];
+        sl.word = word;
+        if (b < items) {
+            sl.item = q->h_items[b];
+            for (uint32_t k = 0; k < sl.item.count; k++) {
+                sl.desc[k].d = q->h_sdesc[(size_t)b * W + k];
+                sl.desc[k].tag = seq;
+            }
+        } else {
+            sl.item = WorkItem{0, 0, 0, 0};
+        }
+        sl.item_tag = seq;
+        __atomic_store_n(&sl.seq, seq, __ATOMIC_RELEASE);
+    }
     q->srv_last_post = now;
     q->srv_posted = q->srv_seq;
     q->srv_first = q->pend_first;
@@ -2202,7 +2223,7 @@ int qpp_txq_poll(qpp_txq *q, uint64_t ticket, int *done) {
     TxqSlot *sl = nullptr;
     RC_TRY(txq_slot_of(q, ticket, &sl));
     if (srv_ticket(q, ticket)) {
-        *done = __atomic_load_n(&q->h_mail->done, __ATOMIC_ACQUIRE) == q->srv_posted;
+        *done = srv_done(q, q->srv_posted);
         if (!*done && !srv_alive(q)) RC_TRY(srv_start(q));
         return QPP_OK;
     }
@@ -2239,7 +2260,7 @@ int qpp_txq_create_persistent(qpp_ctx *ctx, size_t ring_bytes, size_t max_packet
     };
     q->persistent = true;
     ctx->servers.push_back(q);
-    const size_t W = txq_server_waves();
+    const size_t W = kTxsWaves;
     // fine-grained (coherent) pinned memory: polled by the server over PCIe while the host writes it, and read and
     // written by a kernel that does not end between flushes (no cached copy may outlive a flush) -- the ring too
     const unsigned fl = hipHostMallocCoherent | hipHostMallocMapped;
@@ -2265,13 +2286,17 @@ int qpp_txq_create_persistent(qpp_ctx *ctx, size_t ring_bytes, size_t max_packet
         return QPP_DEVICE_ERROR;
     q->v_sdesc = (qpp_pkt *)v;
     memset(q->h_sdesc, 0, sizeof(qpp_pkt) * max_packets * W);
-    if (bad(hipMalloc(&q->d_sync, sizeof(TxsSync)), "txq server sync") ||
-        bad(hipStreamCreateWithFlags(&q->srv_stream, hipStreamNonBlocking), "txq server stream"))
+    if (bad(hipStreamCreateWithFlags(&q->srv_stream, hipStreamNonBlocking), "txq server stream"))
         return QPP_DEVICE_ERROR;
     uint32_t wgs = 16, idle_ms = 200;
     if (const char *e = getenv("QPP_TXQ_SERVER_WGS")) wgs = (uint32_t)strtoul(e, nullptr, 10);
     if (const char *e = getenv("QPP_TXQ_SERVER_IDLE_MS")) idle_ms = (uint32_t)strtoul(e, nullptr, 10);
     q->srv_wgs = std::max(1u, std::min(wgs, ctx->n_cu));
+    if (bad(hipHostMalloc(&q->h_slots, sizeof(TxsSlot) * q->srv_wgs, fl), "txq server slots") ||
+        bad(hipHostGetDevicePointer(&v, q->h_slots, 0), "slots view"))
+        return QPP_DEVICE_ERROR;
+    q->v_slots = (TxsSlot *)v;
+    memset(q->h_slots, 0, sizeof(TxsSlot) * q->srv_wgs);
     idle_ms = std::min<uint32_t>(std::max(4u, idle_ms), 40000u);
     q->srv_idle_ticks = idle_ms * 100000u;  // s_memrealtime: 100 MHz
     q->srv_host_idle = std::chrono::microseconds(250u * idle_ms);
@@ -2284,10 +2309,11 @@ int qpp_txq_server_time(const qpp_txq *q, double *us) {
     return QPP_OK;
 }
 
-int qpp_txq_server_stamps(const qpp_txq *q, uint64_t out[6]) {
+int qpp_txq_server_stamps(const qpp_txq *q, uint64_t out[12]) {
     if (!q || !out || !q->persistent) return QPP_INTERNAL_ERROR;
     const TxsMail &m = *q->h_mail;
-    const uint64_t v[6] = {m.t_seen, m.pad0[0], m.pad0[1], m.pad0[2], m.pad0[3], m.t_done};
+    const uint64_t v[12] = {m.t_seen, m.pad0[0], m.pad0[1], m.pad0[2], m.pad0[3], m.t_done, m.pad0[4],
+                            m.pad1[0], m.pad1[1], m.pad1[2], m.pad1[3], m.pad1[4]};
     memcpy(out, v, sizeof v);
     return QPP_OK;
 }

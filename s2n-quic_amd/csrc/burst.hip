@@ -116,8 +116,23 @@ __device__ __forceinline__ uint32_t byte_of(uint4 v, uint32_t i) {  // byte i (<
 
 // The persistent txq server's per-workgroup copy of its cached key's iv | rk | hp_rk (LDS, after the tables and
 // the control words): no device-memory round trip per packet for them.
-constexpr uint32_t kTxsKey = kBurstLds + 64;
-constexpr uint32_t kTxsLds = kTxsKey + 512;
+constexpr uint32_t kTxsCtl = kBurstLds;         // LDS: the polled slot (304 B) and the exit flag, for every wave
+constexpr uint32_t kTxsStopFlag = kTxsCtl + 16 * kTxsPollLanes;
+constexpr uint32_t kTxsKey = kTxsCtl + 320;
+constexpr uint32_t kTxsTrace = kTxsKey + 512;  // QPP_TXS_TRACE: wave 0's stamps inside its packet (8 words)
+constexpr uint32_t kTxsLds = kTxsTrace + 32;
+static_assert(kTxsStopFlag + 4 <= kTxsKey && kTxsLds <= kLdsMax && kBurstWaves == (int)kTxsWaves, "server LDS");
+#ifndef QPP_TXS_TRACE
+#define QPP_TXS_TRACE 0  // 1: workgroup 0 stamps its phases into the mailbox (tools/diag/server_trace.py)
+#endif
+// wave 0, lane 0 of a server workgroup: s_memrealtime (low word) after all of this lane's loads have landed
+#define TXS_STAMP(j)                                                                          \
+    do {                                                                                      \
+        if (QPP_TXS_TRACE && LDSKEY && threadIdx.x == 0) {                                    \
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                      \
+            lds_st32(kTxsTrace + 4 * (j), (uint32_t)__builtin_amdgcn_s_memrealtime());        \
+        }                                                                                     \
+    } while (0)
 
 // One packet on one wave (all 64 lanes; d is wave-uniform).  LDSKEY: the key's iv and header-protection round keys
 // come from the server's LDS copy (kTxsKey) instead of the key record.
@@ -151,6 +166,7 @@ __device__ __forceinline__ void burst_packet(const AesLds &aes, const DevKey *__
         else if (i >= 0 && i < (int)a) v = ld16(p.base + 16u * (uint32_t)i);
         return v;
     };
+    TXS_STAMP(0);
     uint4 next = block(0);
     // header-protection round keys and header bytes: issued now, used after the GHASH tree (one memory round trip
     // off the end of the chain)
@@ -169,6 +185,7 @@ __device__ __forceinline__ void burst_packet(const AesLds &aes, const DevKey *__
         const uint32_t b = (uint32_t)i - a;  // data block b uses counter b + 2
         const uint4 raw = next;
         if (k + 1 < K) next = block(k + 1);
+        if (k == 0) TXS_STAMP(1);
         uint4 in = data ? raw : make_uint4(0, 0, 0, 0), ks = make_uint4(0, 0, 0, 0);
         if (data || j0) ks = aes.encrypt<NR>(make_uint4(p.n0, p.n1, p.n2, bswap32(data ? b + 2u : 1u)), rk);
         uint4 x = make_uint4(0, 0, 0, 0);
@@ -195,9 +212,11 @@ __device__ __forceinline__ void burst_packet(const AesLds &aes, const DevKey *__
         }
         acc = k ? gmul(tab(6), acc) ^ x : x;
     }
+    TXS_STAMP(2);
     // lane tree: level t combines lanes l and l + 2^t (l a multiple of 2^(t+1)) as v_l * H^(2^t) ^ v_(l+2^t)
 #pragma unroll
     for (int t = 0; t < 6; t++) acc = gmul(tab(t), acc) ^ shfl4_down(acc, 1u << t);
+    TXS_STAMP(3);
     const uint4 ek0 = pad ? shfl4(ek, (int)pad - 1)  // (pad == 0: no idle lane in pass 0)
                           : aes.encrypt<NR>(make_uint4(p.n0, p.n1, p.n2, bswap32(1u)), rk);
     const uint4 tag = shfl4(gmul(tab(0), acc), 0) ^ ek0;  // Y = Q * H, from lane 0
@@ -237,6 +256,7 @@ __device__ __forceinline__ void burst_packet(const AesLds &aes, const DevKey *__
                 }
             }
         }
+        TXS_STAMP(4);
         if (status && lane == 0) status[pi] = st;
     } else {
         const uint4 want = ld16(pay + p.len);
@@ -296,32 +316,26 @@ __global__ __launch_bounds__(kBurstWG) void aes_gcm_burst_kernel(const DevKey *_
 
 // ---------------------------------------------------------------- persistent transmit-queue server
 // qpp_txq_create_persistent: the seal of a GSO burst without a kernel launch per flush.  The transport's queue.flush()
-// (endpoint/mod.rs:158 -> socket/io/tx.rs:204-268) posts a flush by writing one 64-bit doorbell word into pinned
-// host memory; the workgroups below are already resident, with the AES tables built and the last key's GHASH tables
-// in LDS, and write `done` back into the same pinned page when the burst is sealed.
+// (endpoint/mod.rs:158 -> socket/io/tx.rs:204-268) posts a flush by writing into pinned host memory; the workgroups
+// below are already resident, with the AES tables built and the last key's GHASH tables and key words in LDS, and
+// write completion words back into the same memory when the burst is sealed.
 //
-// Protocol (one flush in flight; the host posts the next only after `done`):
-//   doorbell = seq << 32 | epoch << 24 | items   (items = kTxsStop: exit)
-// * every workgroup polls the doorbell itself (QPP_TXS_DIRECT; else workgroup 0 polls and forwards the word through
-//   device memory, one hop more).  A workgroup leaves on the stop word, or after idle_ticks without a new doorbell --
-//   the host never posts to a server that may be leaving on its own: after a quarter of that idle time without a
-//   post it stops the server and starts a new one first (api.cpp srv_submit), so a flush is seen by every workgroup
-//   or by none (the idle exit is for a host that went away);
-// * item i (one key, <= kBurstWaves packets, host-built) goes to workgroup i % grid, packet q of it to wave q; the
-//   descriptors sit at sdesc[i * kBurstWaves + q], so a wave reads its item and its descriptor in one round trip;
-// * a workgroup keeps the GHASH tables of the key it used last until a doorbell carries a new key epoch (the host
-//   bumps it whenever key records were installed since its previous post: a slot can have been reused); only then
-//   does it invalidate its caches (the plan and the ring are fine-grained host memory, never cached);
-// * completion: every storing wave drains its stores, the workgroup releases at system scope and counts itself in
-//   sync->arrive; the last one resets the count and writes done = seq (system scope).
-#ifndef QPP_TXS_DIRECT
-#define QPP_TXS_DIRECT 1
-#endif
-#ifndef QPP_TXS_TRACE
-#define QPP_TXS_TRACE 0  // 1: workgroup 0 stamps its phases into the mailbox (tools/diag/server_trace.py)
-#endif
-constexpr uint32_t kTxsCtl = kBurstLds;  // LDS: the doorbell word and the stop flag broadcast to the workgroup
-static_assert(kTxsKey >= kTxsCtl + 16 && kTxsLds <= kLdsMax, "server LDS");
+// Protocol (one flush in flight; the host posts the next only after every workgroup's `done`):
+// * workgroup b polls its own TxsSlot: one wave-wide read (19 lanes x 16 B) returns the flush seq, the key epoch,
+//   the workgroup's first work item and that item's descriptors, each tagged with the seq -- a read that raced the
+//   host's writes shows a stale tag and is simply repeated.  So the flush, its plan and its descriptors cost one PCIe
+//   round trip, and polls overlap (two in flight) so a new flush is seen within a fraction of one;
+// * item i (one key, <= 8 packets, host-built) goes to workgroup i % grid, packet q of it to wave q; items beyond the
+//   first of a workgroup (flushes of > grid items) are read from the items / sdesc arrays;
+// * a workgroup keeps the GHASH tables and key words of the key it used last until a flush carries a new key epoch
+//   (the host bumps it whenever key records were installed since its previous post: a slot can have been reused);
+//   only then does it invalidate its caches (plans and the ring are fine-grained host memory, never cached);
+// * completion: every storing wave drains its stores, the workgroup releases at system scope and writes its slot's
+//   done = seq; the host waits for all of them;
+// * a workgroup leaves on the stop word, or after idle_ticks without a flush -- the host never posts to a server
+//   that may be leaving on its own: after a quarter of that idle time without a post it stops the server and starts
+//   a new one first (api.cpp srv_submit), so a flush is seen by every workgroup or by none (the idle exit is for a
+//   host that went away).
 
 template <int NR>
 __device__ __forceinline__ void txs_item(const AesLds &aes, const DevKey *key, const qpp_pkt &d,
@@ -333,60 +347,80 @@ __device__ __forceinline__ void txs_item(const AesLds &aes, const DevKey *key, c
         burst_packet<NR, true, true>(aes, key, rk, d, 0, ring, nullptr, nullptr, QPP_HP_APPLY);
 }
 
+// one 16-byte chunk of the slot (lane < kTxsPollLanes), read past every cache (the host writes it)
+__device__ __forceinline__ uint4 txs_poll(const TxsSlot *slot, uint32_t lane) {
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (lane < kTxsPollLanes) {
+        uint64_t *p = (uint64_t *)((uint8_t *)slot + 16 * lane);
+        const uint64_t a = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const uint64_t b = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        v = make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
+    }
+    return v;
+}
+
 __global__ __launch_bounds__(kBurstWG) void txq_server_kernel(const DevKey *keys, const PowTables pow, TxsMail *mail,
-                                                              TxsSync *sync, const WorkItem *items,
+                                                              TxsSlot *slots, const WorkItem *items,
                                                               const qpp_pkt *sdesc, uint8_t *ring, uint32_t seq0,
                                                               uint32_t idle_ticks) {
     build_aes_tables(kBurstAes);
     __syncthreads();
     const AesLds aes = make_aes(kBurstAes);
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    TxsSlot *slot = slots + blockIdx.x;
     uint32_t seen = seq0, cached = 0xffffffffu, epoch = 0xffffffffu;
     for (;;) {
-        if (threadIdx.x == 0) {
-            uint64_t word = 0;
-            uint32_t stop = 0;
+        if (wave == 0) {
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-            if (QPP_TXS_DIRECT || blockIdx.x == 0) {
-                for (;;) {
-                    word = __hip_atomic_load(&mail->doorbell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    if ((uint32_t)(word >> 32) != seen) break;
-                    if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) { stop = 1; break; }
-                    __builtin_amdgcn_s_sleep(2);
+            uint32_t stop = 0;
+            uint4 cur = txs_poll(slot, lane);
+            for (;;) {
+                __builtin_amdgcn_s_sleep(4);
+                const uint4 nxt = txs_poll(slot, lane);  // in flight while `cur` is examined
+                const uint32_t seq = __shfl((int)cur.x, 0, 64), word = __shfl((int)cur.y, 0, 64);
+                if (seq != seen) {
+                    if ((word & kTxsItemsMask) == kTxsStop) {
+                        stop = 1;
+                        break;
+                    }
+                    // every part of this flush must carry its seq: the item (chunk 1; its tag in chunk 2) and the
+                    // descriptors 0 .. count - 1 (descriptor q in chunks 3 + 2q, 4 + 2q; its tag at .z of the second)
+                    const uint32_t item_cnt = __shfl((int)cur.z, 1, 64);
+                    bool ok = true;
+                    if (lane == 2) ok = cur.x == seq;
+                    if (lane >= 4 && lane < kTxsPollLanes && !(lane & 1) && (lane - 4) / 2 < item_cnt) ok = cur.z == seq;
+                    if (__all(ok)) break;
                 }
-                if ((uint32_t)(word & kTxsItemsMask) == kTxsStop) stop = 1;
+                if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) {
+                    stop = 1;
+                    break;
+                }
+                cur = nxt;
+            }
+            if (lane < kTxsPollLanes) lds_st128(kTxsCtl + 16 * lane, cur);
+            if (lane == 0) {
+                lds_st32(kTxsStopFlag, stop);
                 if (!stop && blockIdx.x == 0)
                     __hip_atomic_store(&mail->t_seen, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_SYSTEM);
-                if (!QPP_TXS_DIRECT) {
-                    if (stop) __hip_atomic_store(&sync->stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    else __hip_atomic_store(&sync->go, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-            } else {
-                for (;;) {
-                    if (__hip_atomic_load(&sync->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) { stop = 1; break; }
-                    word = __hip_atomic_load(&sync->go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    const uint32_t sq = (uint32_t)(word >> 32);
-                    if (sq != seen && sq != 0) break;
-                    __builtin_amdgcn_s_sleep(2);
-                }
+                // key records installed since this workgroup's caches last looked: visible from here on
+                if (!stop && (__shfl((int)cur.y, 0, 64) >> 24) != epoch) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
             }
-            // key records installed since this workgroup's caches last looked: visible from here on
-            if (!stop && ((uint32_t)word >> 24) != epoch) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-            lds_st64(kTxsCtl, make_uint2((uint32_t)word, (uint32_t)(word >> 32)));
-            lds_st32(kTxsCtl + 8, stop);
         }
         __syncthreads();
-        const uint2 w2 = lds_ld64(kTxsCtl);
-        const uint32_t stop = lds_ld32(kTxsCtl + 8);
-        __syncthreads();  // (the next doorbell's broadcast does not overwrite these before every wave read them)
+        const uint32_t stop = lds_ld32(kTxsStopFlag);
         if (stop) break;  // uniform
-        seen = w2.y;
-        const uint32_t n_items = w2.x & kTxsItemsMask, ep = w2.x >> 24;
-        // The plan and the key records change between flushes, so they are read with VECTOR loads, through the
-        // caches the acquire above invalidated: left alone, the compiler read the wave-uniform work item, descriptor
-        // and round keys with scalar loads, whose cache the fence does not cover, and every flush after the first
-        // sealed the first flush's descriptors again.  The pointers are re-laundered into VGPRs once per flush.
+        const uint4 hdr = lds_ld128(kTxsCtl);
+        const uint4 it0 = lds_ld128(kTxsCtl + 16);
+        const WorkItem w0{it0.x, it0.y, it0.z, it0.w};
+        const uint4 da = lds_ld128(kTxsCtl + 48 + 32 * wave), db = lds_ld128(kTxsCtl + 64 + 32 * wave);
+        qpp_pkt d0;
+        __builtin_memcpy((uint8_t *)&d0, &da, 16);
+        __builtin_memcpy((uint8_t *)&d0 + 16, &db, 8);
+        seen = hdr.x;
+        const uint32_t n_items = hdr.y & kTxsItemsMask, ep = hdr.y >> 24;
+        // Items beyond the slot's and the key records change between flushes: read with VECTOR loads through
+        // laundered pointers (wave-uniform addresses were otherwise scalar loads, whose cache no fence covers)
         const WorkItem *items_v = items;
         const qpp_pkt *sdesc_v = sdesc;
         const DevKey *keys_v = keys;
@@ -395,15 +429,16 @@ __global__ __launch_bounds__(kBurstWG) void txq_server_kernel(const DevKey *keys
             epoch = ep;
             cached = 0xffffffffu;
         }
-        uint64_t tr[4] = {0, 0, 0, 0};
-        if (QPP_TXS_TRACE && threadIdx.x == 0) tr[0] = __builtin_amdgcn_s_memrealtime();
+        uint64_t tr[4] = {0, 0, 0, 0}, clk0 = 0;
+        if (QPP_TXS_TRACE && threadIdx.x == 0) {
+            tr[0] = __builtin_amdgcn_s_memrealtime();
+            clk0 = __builtin_amdgcn_s_memtime();  // shader clock: its rate over the flush = the clock the flush ran at
+            tr[1] = tr[0];
+        }
         for (uint32_t it = blockIdx.x; it < n_items; it += gridDim.x) {
-            const WorkItem w = items_v[it];
-            const qpp_pkt d = sdesc_v[it * kBurstWaves + wave];
-            if (QPP_TXS_TRACE && threadIdx.x == 0 && !tr[1]) {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                tr[1] = __builtin_amdgcn_s_memrealtime();
-            }
+            const bool first = it == blockIdx.x;
+            const WorkItem w = first ? w0 : items_v[it];
+            const qpp_pkt d = first ? d0 : sdesc_v[it * kBurstWaves + wave];
             const DevKey *key = keys_v + w.key;
             if (w.key != cached) {  // uniform
                 __syncthreads();  // every wave is done with the previous key's tables
@@ -415,25 +450,29 @@ __global__ __launch_bounds__(kBurstWG) void txq_server_kernel(const DevKey *keys
             if (w.nr == 10) txs_item<10>(aes, key, d, wave, w.count, ring);
             else txs_item<14>(aes, key, d, wave, w.count, ring);
         }
-        // completion: this workgroup's ring stores reach the host before it counts itself
+        // completion: this workgroup's ring stores reach the host before its done word
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (QPP_TXS_TRACE && threadIdx.x == 0) tr[2] = __builtin_amdgcn_s_memrealtime();
         __syncthreads();
         if (threadIdx.x == 0) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-            const uint32_t prev = __hip_atomic_fetch_add(&sync->arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-            if (QPP_TXS_TRACE && blockIdx.x == 0) {
-                tr[3] = __builtin_amdgcn_s_memrealtime();
-                for (int j = 0; j < 4; j++)
-                    __hip_atomic_store(&mail->pad0[j], tr[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            }
-            if (prev == gridDim.x - 1) {
-                __hip_atomic_store(&sync->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (blockIdx.x == 0) {
+                if (QPP_TXS_TRACE) {
+                    tr[3] = __builtin_amdgcn_s_memrealtime();
+                    const uint64_t clk1 = __builtin_amdgcn_s_memtime();
+                    for (int j = 0; j < 4; j++)
+                        __hip_atomic_store(&mail->pad0[j], tr[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    __hip_atomic_store(&mail->pad0[4], clk1 - clk0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    for (int j = 0; j < 5; j++)
+                        __hip_atomic_store(&mail->pad1[j], lds_ld32(kTxsTrace + 4 * j), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_SYSTEM);
+                }
                 __hip_atomic_store(&mail->t_done, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_SYSTEM);
-                __hip_atomic_store(&mail->done, seen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             }
+            __hip_atomic_store(&slot->done, seen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
+        __syncthreads();  // (the next poll's LDS copy does not overwrite this flush's before every wave read it)
     }
 }
 
@@ -471,12 +510,10 @@ hipError_t launch_aes_gcm_burst(bool seal, const DevKey *keys, const qpp_pkt *de
     return hipGetLastError();
 }
 
-uint32_t txq_server_waves() { return (uint32_t)kBurstWaves; }
-
-hipError_t launch_txq_server(const DevKey *keys, const PowTables &pow, TxsMail *mail, TxsSync *sync,
+hipError_t launch_txq_server(const DevKey *keys, const PowTables &pow, TxsMail *mail, TxsSlot *slots,
                              const WorkItem *items, const qpp_pkt *sdesc, uint8_t *ring, uint32_t seq0,
                              uint32_t idle_ticks, uint32_t wgs, hipStream_t s) {
-    hipLaunchKernelGGL(txq_server_kernel, dim3(wgs), dim3(kBurstWG), kTxsLds, s, keys, pow, mail, sync, items,
+    hipLaunchKernelGGL(txq_server_kernel, dim3(wgs), dim3(kBurstWG), kTxsLds, s, keys, pow, mail, slots, items,
                        sdesc, ring, seq0, idle_ticks);
     return hipGetLastError();
 }

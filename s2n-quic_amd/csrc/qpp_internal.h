@@ -145,26 +145,35 @@ hipError_t launch_aes_gcm_burst(bool seal, const DevKey *keys, const qpp_pkt *de
                                 uint32_t n, uint32_t key_cap, uint32_t per, uint8_t *arena, uint8_t *masks,
                                 int8_t *status, uint32_t flags, uint32_t suites, const PowTables &pow, hipStream_t s);
 // Persistent transmit-queue server (burst.hip txq_server_kernel; api.cpp qpp_txq_create_persistent).
-// TxsMail: pinned, coherent host memory (the host writes doorbell, the server writes done); TxsSync: device memory.
-struct alignas(64) TxsMail {
-    uint64_t doorbell;  // seq << 32 | key epoch << 24 | work items (kTxsStop: exit)
-    // server-side timestamps of the last flush (s_memrealtime, 100 MHz): the leader saw the doorbell / the last
-    // workgroup finished (written before done)
-    uint64_t t_seen, t_done;
-    uint64_t pad0[5];  // QPP_TXS_TRACE: workgroup 0's broadcast / item read / packets done / arrival stamps
-    uint32_t done;      // seq of the last flush sealed
-    uint32_t pad1[15];
-};
-struct alignas(64) TxsSync {
-    uint64_t go;      // the leader's copy of the doorbell word for the other workgroups
-    uint32_t stop;    // set by the leader when the server exits
-    uint32_t arrive;  // workgroups done with the current flush
-    uint32_t pad[12];
-};
+// One TxsSlot per server workgroup in pinned, coherent host memory: the host writes the workgroup's first work item
+// and its descriptors (each tagged with the flush's seq) and then seq; the workgroup polls its slot (one wave-wide
+// read gets the flush, the item and the descriptors together) and writes `done` = seq when its packets are sealed.
+constexpr uint32_t kTxsWaves = 8;  // server workgroup = 8 waves, one packet per wave per work item
 constexpr uint32_t kTxsItemsMask = 0xffffffu;
 constexpr uint32_t kTxsStop = 0xffffffu;
-uint32_t txq_server_waves();  // packets per work item (one per wave); sdesc holds items x this many slots
-hipError_t launch_txq_server(const DevKey *keys, const PowTables &pow, TxsMail *mail, TxsSync *sync,
+struct alignas(16) TxsSlotDesc {
+    qpp_pkt d;
+    uint32_t tag;  // = seq of the flush this descriptor belongs to
+    uint32_t pad;
+};
+struct alignas(64) TxsSlot {
+    uint32_t seq;   // flush seq, written last
+    uint32_t word;  // key epoch << 24 | the flush's work items (kTxsStop: exit)
+    uint32_t pad0[2];
+    WorkItem item;  // this workgroup's first work item (count 0: none)
+    uint32_t item_tag, pad1[3];
+    TxsSlotDesc desc[kTxsWaves];
+    alignas(64) uint32_t done;  // written by the server: the seq whose packets this workgroup has sealed
+    uint32_t pad2[15];
+};
+static_assert(sizeof(TxsSlot) == 384 && offsetof(TxsSlot, desc) == 48 && offsetof(TxsSlot, done) == 320, "TxsSlot");
+constexpr uint32_t kTxsPollLanes = 19;  // 16-byte chunks of [seq .. desc[7]] = 304 bytes
+struct alignas(64) TxsMail {  // telemetry (s_memrealtime, 100 MHz)
+    uint64_t t_seen, t_done;  // workgroup 0 saw the flush / finished it
+    uint64_t pad0[6];         // QPP_TXS_TRACE: workgroup 0's phase stamps and shader cycles
+    uint32_t pad1[16];        // QPP_TXS_TRACE: wave 0's stamps inside its packet
+};
+hipError_t launch_txq_server(const DevKey *keys, const PowTables &pow, TxsMail *mail, TxsSlot *slots,
                              const WorkItem *items, const qpp_pkt *sdesc, uint8_t *ring, uint32_t seq0,
                              uint32_t idle_ticks, uint32_t wgs, hipStream_t s);
 // the burst power tables of keys[slots[i]] (AES packet keys with slot < pow.cap), after their V[m] are in place

@@ -134,6 +134,7 @@ def test_fused_rx_many_keys(suite, monkeypatch):
             k0 = ctx.key(suite, rng.integers(0, 256, qpp.HASH_LEN[suite], dtype=np.uint8).tobytes())
             pairs.append((k0, k0.derive_next_key()))
         mats = [(suite, *k.material()) for pair in pairs for k in pair]
+        slots = [(p[0].slot, p[1].slot) for p in pairs]  # (a freed key's handle has no slot any more)
         for c in range(32, 36):
             pairs[c][1].free()
         n = 6000
@@ -153,8 +154,7 @@ def test_fused_rx_many_keys(suite, monkeypatch):
             if i % 19 == 4:
                 pkt[-1 - i % 16] ^= 0x01  # tampered -> DECRYPT_ERROR
             chunks.append(bytes(pkt) + bytes(int(rng.integers(0, 5))))
-            rx.append((largest, (pairs[c][0].slot, pairs[c][1].slot if c < 32 else pairs[c][1].slot), off,
-                       len(header), len(pkt)))
+            rx.append((largest, slots[c], off, len(header), len(pkt)))
             orx.append((largest, (2 * c, 2 * c + 1), off, len(header), len(pkt)))
             off += len(chunks[-1])
         rx = np.array(rx, dtype=qpp.RX_DTYPE)

@@ -31,10 +31,12 @@ for i in range(600):
     t0 = time.perf_counter()
     q.flush()
     t1 = time.perf_counter()
-    st = (ctypes.c_uint64 * 6)()
+    st = (ctypes.c_uint64 * 12)()
     lib.qpp_txq_server_stamps(q.handle, st)
     if i >= 100:
-        rows.append([(t1 - t0) * 1e6] + [(st[j] - st[0]) / 100.0 for j in range(1, 6)])
+        lo = st[0] & 0xffffffff
+        rows.append([(t1 - t0) * 1e6] + [(st[j] - st[0]) / 100.0 for j in range(1, 6)] +
+                    [st[6] / max(1.0, (st[4] - st[1]) / 100.0)] + [((st[j] - lo) & 0xffffffff) / 100.0 for j in range(7, 12)])
 a = np.median(np.array(rows), axis=0)
 print("median us: host flush %.1f | from doorbell seen: broadcast %.2f item+desc %.2f packets %.2f arrive %.2f done %.2f"
-      % tuple(a))
+      " | shader clock %.0f MHz | wave 0 packet: start %.2f block in %.2f passes %.2f tree %.2f hp %.2f" % tuple(a))

@@ -2089,21 +2089,28 @@ static int srv_submit(qpp_txq *q) {
     RC_TRY(srv_start(q));
     q->srv_seq = srv_next(q->srv_seq);
     const uint32_t seq = q->srv_seq, word = (q->srv_epoch << 24) | items;
-    // each workgroup's slot: its first item and that item's descriptors, all tagged, then the seq (x86 stores are
-    // seen in order; the server also checks every tag, so a read that raced these stores is repeated)
+    // each workgroup's slot: its first item and that item's descriptors, every 16-byte chunk tagged, then the seq (x86
+    // stores are seen in order; the server reads each chunk in one load and checks every tag, so a read that raced
+    // these stores is repeated)
     for (uint32_t b = 0; b < q->srv_wgs; b++) {
         TxsSlot &sl = q->h_slots[b];
         sl.word = word;
-        if (b < items) {
-            sl.item = q->h_items[b];
-            for (uint32_t k = 0; k < sl.item.count; k++) {
-                sl.desc[k].d = q->h_sdesc[(size_t)b * W + k];
-                sl.desc[k].tag = seq;
-            }
-        } else {
-            sl.item = WorkItem{0, 0, 0, 0};
+        const WorkItem it = b < items ? q->h_items[b] : WorkItem{0, 0, 0, 0};
+        for (uint32_t k = 0; k < it.count; k++) {
+            const qpp_pkt &d = q->h_sdesc[(size_t)b * W + k];
+            TxsSlotDesc &sd = sl.desc[k];
+            sd.pn = d.pn;
+            sd.key_idx = d.key_idx;
+            __atomic_store_n(&sd.tag0, seq, __ATOMIC_RELEASE);  // (after the chunk's other words)
+            sd.off = d.off;
+            sd.lens = (uint32_t)d.aad_len | (uint32_t)d.pt_len << 16;
+            sd.misc = (uint32_t)d.pn_len | (uint32_t)d.flags << 8;
+            __atomic_store_n(&sd.tag1, seq, __ATOMIC_RELEASE);
         }
-        sl.item_tag = seq;
+        sl.it_key = it.key;
+        sl.it_count = it.count;
+        sl.it_nr = it.nr;
+        __atomic_store_n(&sl.it_tag, seq, __ATOMIC_RELEASE);
         __atomic_store_n(&sl.seq, seq, __ATOMIC_RELEASE);
     }
     q->srv_last_post = now;

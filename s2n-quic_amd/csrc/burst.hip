@@ -116,7 +116,7 @@ __device__ __forceinline__ uint32_t byte_of(uint4 v, uint32_t i) {  // byte i (<
 
 // The persistent txq server's per-workgroup copy of its cached key's iv | rk | hp_rk (LDS, after the tables and
 // the control words): no device-memory round trip per packet for them.
-constexpr uint32_t kTxsCtl = kBurstLds;         // LDS: the polled slot (304 B) and the exit flag, for every wave
+constexpr uint32_t kTxsCtl = kBurstLds;         // LDS: the polled slot (288 B) and the exit flag, for every wave
 constexpr uint32_t kTxsStopFlag = kTxsCtl + 16 * kTxsPollLanes;
 constexpr uint32_t kTxsKey = kTxsCtl + 320;
 constexpr uint32_t kTxsTrace = kTxsKey + 512;  // QPP_TXS_TRACE: wave 0's stamps inside its packet (8 words)
@@ -329,7 +329,8 @@ __global__ __launch_bounds__(kBurstWG) void aes_gcm_burst_kernel(const DevKey *_
 //   first of a workgroup (flushes of > grid items) are read from the items / sdesc arrays;
 // * a workgroup keeps the GHASH tables and key words of the key it used last until a flush carries a new key epoch
 //   (the host bumps it whenever key records were installed since its previous post: a slot can have been reused);
-//   only then does it invalidate its caches (plans and the ring are fine-grained host memory, never cached);
+// * every flush starts with a system-scope acquire: the ring is pinned host memory the GPU caches like any other, and
+//   the transport rewrites the same offsets flush after flush;
 // * completion: every storing wave drains its stores, the workgroup releases at system scope and writes its slot's
 //   done = seq; the host waits for all of them;
 // * a workgroup leaves on the stop word, or after idle_ticks without a flush -- the host never posts to a server
@@ -347,14 +348,14 @@ __device__ __forceinline__ void txs_item(const AesLds &aes, const DevKey *key, c
         burst_packet<NR, true, true>(aes, key, rk, d, 0, ring, nullptr, nullptr, QPP_HP_APPLY);
 }
 
-// one 16-byte chunk of the slot (lane < kTxsPollLanes), read past every cache (the host writes it)
+// one 16-byte chunk of the slot (lane < kTxsPollLanes), in ONE load past every cache (sc0 sc1: the host writes it;
+// a chunk is read whole, so its tag vouches for its other words)
 __device__ __forceinline__ uint4 txs_poll(const TxsSlot *slot, uint32_t lane) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     uint4 v = make_uint4(0, 0, 0, 0);
     if (lane < kTxsPollLanes) {
-        uint64_t *p = (uint64_t *)((uint8_t *)slot + 16 * lane);
-        const uint64_t a = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        const uint64_t b = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        v = make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
+        const u32x4 c = *((const volatile u32x4 *)slot + lane);
+        v = make_uint4(c.x, c.y, c.z, c.w);
     }
     return v;
 }
@@ -383,12 +384,12 @@ __global__ __launch_bounds__(kBurstWG) void txq_server_kernel(const DevKey *keys
                         stop = 1;
                         break;
                     }
-                    // every part of this flush must carry its seq: the item (chunk 1; its tag in chunk 2) and the
-                    // descriptors 0 .. count - 1 (descriptor q in chunks 3 + 2q, 4 + 2q; its tag at .z of the second)
-                    const uint32_t item_cnt = __shfl((int)cur.z, 1, 64);
+                    // every chunk of this flush must carry its seq (last word): the item (chunk 1) and the
+                    // descriptors 0 .. count - 1 (descriptor q in chunks 2 + 2q, 3 + 2q)
+                    const uint32_t item_cnt = __shfl((int)cur.y, 1, 64);
                     bool ok = true;
-                    if (lane == 2) ok = cur.x == seq;
-                    if (lane >= 4 && lane < kTxsPollLanes && !(lane & 1) && (lane - 4) / 2 < item_cnt) ok = cur.z == seq;
+                    if (lane == 1) ok = cur.w == seq;
+                    if (lane >= 2 && lane < kTxsPollLanes && (lane - 2) / 2 < item_cnt) ok = cur.w == seq;
                     if (__all(ok)) break;
                 }
                 if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) {
@@ -403,8 +404,11 @@ __global__ __launch_bounds__(kBurstWG) void txq_server_kernel(const DevKey *keys
                 if (!stop && blockIdx.x == 0)
                     __hip_atomic_store(&mail->t_seen, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_SYSTEM);
-                // key records installed since this workgroup's caches last looked: visible from here on
-                if (!stop && (__shfl((int)cur.y, 0, 64) >> 24) != epoch) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+                // Every flush: the CU's vector cache (and L2's non-coherent lines) dropped, so that this flush's ring
+                // bytes are read from the host, not the lines the previous flush left for the same offsets (the ring
+                // is reused flush after flush; without it, every flush after the first of one server launch sealed
+                // stale plaintext: tools/diag/server_mismatch.py), and key records installed since are visible
+                if (!stop) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
             }
         }
         __syncthreads();
@@ -412,11 +416,17 @@ __global__ __launch_bounds__(kBurstWG) void txq_server_kernel(const DevKey *keys
         if (stop) break;  // uniform
         const uint4 hdr = lds_ld128(kTxsCtl);
         const uint4 it0 = lds_ld128(kTxsCtl + 16);
-        const WorkItem w0{it0.x, it0.y, it0.z, it0.w};
-        const uint4 da = lds_ld128(kTxsCtl + 48 + 32 * wave), db = lds_ld128(kTxsCtl + 64 + 32 * wave);
+        const WorkItem w0{it0.x, 0u, it0.y, it0.z};  // (begin unused: its descriptors came with the slot)
+        const uint4 da = lds_ld128(kTxsCtl + 32 + 32 * wave), db = lds_ld128(kTxsCtl + 48 + 32 * wave);
         qpp_pkt d0;
-        __builtin_memcpy((uint8_t *)&d0, &da, 16);
-        __builtin_memcpy((uint8_t *)&d0 + 16, &db, 8);
+        d0.pn = (uint64_t)da.x | (uint64_t)da.y << 32;
+        d0.key_idx = da.z;
+        d0.off = db.x;
+        d0.aad_len = (uint16_t)db.y;
+        d0.pt_len = (uint16_t)(db.y >> 16);
+        d0.pn_len = (uint8_t)db.z;
+        d0.flags = (uint8_t)(db.z >> 8);
+        d0.reserved = 0;
         seen = hdr.x;
         const uint32_t n_items = hdr.y & kTxsItemsMask, ep = hdr.y >> 24;
         // Items beyond the slot's and the key records change between flushes: read with VECTOR loads through

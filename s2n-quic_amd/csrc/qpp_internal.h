@@ -151,23 +151,29 @@ hipError_t launch_aes_gcm_burst(bool seal, const DevKey *keys, const qpp_pkt *de
 constexpr uint32_t kTxsWaves = 8;  // server workgroup = 8 waves, one packet per wave per work item
 constexpr uint32_t kTxsItemsMask = 0xffffffu;
 constexpr uint32_t kTxsStop = 0xffffffu;
+// Every 16-byte chunk carries the flush's seq as its last word (the host stores it after the chunk's other words):
+// the server reads each chunk with ONE 16-byte load, so a chunk whose tag matches is wholly this flush's.  (With the
+// tag in only one chunk of a descriptor, a poll could combine a stale first half -- the previous flush's pn, key and
+// offset -- with a fresh second half, and seal a packet with the previous flush's descriptor.)
 struct alignas(16) TxsSlotDesc {
-    qpp_pkt d;
-    uint32_t tag;  // = seq of the flush this descriptor belongs to
-    uint32_t pad;
+    uint64_t pn;
+    uint32_t key_idx, tag0;
+    uint32_t off;
+    uint32_t lens;  // aad_len | pt_len << 16
+    uint32_t misc;  // pn_len | flags << 8
+    uint32_t tag1;
 };
 struct alignas(64) TxsSlot {
     uint32_t seq;   // flush seq, written last
     uint32_t word;  // key epoch << 24 | the flush's work items (kTxsStop: exit)
     uint32_t pad0[2];
-    WorkItem item;  // this workgroup's first work item (count 0: none)
-    uint32_t item_tag, pad1[3];
+    uint32_t it_key, it_count, it_nr, it_tag;  // this workgroup's first work item (count 0: none)
     TxsSlotDesc desc[kTxsWaves];
     alignas(64) uint32_t done;  // written by the server: the seq whose packets this workgroup has sealed
     uint32_t pad2[15];
 };
-static_assert(sizeof(TxsSlot) == 384 && offsetof(TxsSlot, desc) == 48 && offsetof(TxsSlot, done) == 320, "TxsSlot");
-constexpr uint32_t kTxsPollLanes = 19;  // 16-byte chunks of [seq .. desc[7]] = 304 bytes
+static_assert(sizeof(TxsSlot) == 384 && offsetof(TxsSlot, desc) == 32 && offsetof(TxsSlot, done) == 320, "TxsSlot");
+constexpr uint32_t kTxsPollLanes = 18;  // 16-byte chunks of [seq .. desc[7]] = 288 bytes
 struct alignas(64) TxsMail {  // telemetry (s_memrealtime, 100 MHz)
     uint64_t t_seen, t_done;  // workgroup 0 saw the flush / finished it
     uint64_t pad0[6];         // QPP_TXS_TRACE: workgroup 0's phase stamps and shader cycles

@@ -60,7 +60,23 @@ constexpr uint32_t kQLdsVe = 65536;    // V_e during the build
 #ifndef QPP_QUAD_WG256
 #define QPP_QUAD_WG256 768  // AES-256 (60 round-key words, 14 rounds of pipeline state)
 #endif
+#ifndef QPP_QUAD_NOCRYPTO
+#define QPP_QUAD_NOCRYPTO 0  // diagnostic: payload I/O only (no keystream, no GHASH products in the group loop)
+#endif
+#ifndef QPP_QUAD_NOIO
+#define QPP_QUAD_NOIO 0  // diagnostic: no payload loads/stores (compute floor of the kernel shape)
+#endif
+__device__ __forceinline__ uint4 ld_payload(const uint8_t *p, uint32_t salt) {
+#if QPP_QUAD_NOIO
+    return make_uint4(salt, salt * 3u, (uint32_t)(uintptr_t)p, salt ^ 0x5555u);
+#else
+    return ld16(p);
+#endif
+}
 __device__ __forceinline__ void st_payload(uint8_t *p, uint4 v) {
+#if QPP_QUAD_NOIO
+    return;
+#endif
 #if QPP_QUAD_NT
     st16_nt(p, v);
 #else
@@ -305,6 +321,21 @@ __device__ __forceinline__ void quad_packet(const AesLds &aes, const GhashT<true
                 ks[k] = aes.encrypt<NR>(make_uint4(m0, m1, m2, bswap32(c0 + 4 * k)), rk);
             });
         }
+#elif QPP_QUAD_NOCRYPTO
+#pragma unroll
+        for (int k = 0; k < NBG; k++) ks[k] = make_uint4(c0 + 4 * k, n0, n1, n2);
+        uint4 in[NBG];
+        if (inner) {
+            const uint32_t b = pay + 16 * (uint32_t)(t0 - 1);
+#pragma unroll
+            for (int k = 0; k < NBG; k++) in[k] = ld_payload(at(b + 64 * k), b + k);
+        } else {
+#pragma unroll
+            for (int k = 0; k < NBG; k++) {
+                const int j = t0 + 4 * k - 1;
+                in[k] = ld_payload(at(pay + (j >= 0 && 16 * j <= (int)len ? 16 * (uint32_t)j : 0u)), pay + j);
+            }
+        }
 #else
         // The nonce words are laundered where the loop uses them (a new page; the straddling group): left alone, the
         // compiler hoisted the page build's first-round lookups addresses out of the loop as loop invariants and
@@ -329,12 +360,12 @@ __device__ __forceinline__ void quad_packet(const AesLds &aes, const GhashT<true
         if (inner) {
             const uint32_t b = pay + 16 * (uint32_t)(t0 - 1);
 #pragma unroll
-            for (int k = 0; k < NBG; k++) in[k] = ld16(at(b + 64 * k));
+            for (int k = 0; k < NBG; k++) in[k] = ld_payload(at(b + 64 * k), b + k);
         } else {
 #pragma unroll
             for (int k = 0; k < NBG; k++) {
                 const int j = t0 + 4 * k - 1;
-                in[k] = ld16(at(pay + (j >= 0 && 16 * j <= (int)len ? 16 * (uint32_t)j : 0u)));
+                in[k] = ld_payload(at(pay + (j >= 0 && 16 * j <= (int)len ? 16 * (uint32_t)j : 0u)), pay + j);
             }
         }
 #endif
@@ -369,14 +400,14 @@ __device__ __forceinline__ void quad_packet(const AesLds &aes, const GhashT<true
             for (int k = 0; k < NBG; k++) st_payload(at(b + 64 * k), out[k]);
 #endif
 #pragma unroll
-            for (int k = 0; k < NBG; k++) w = gh.mulx(w, SEAL ? out[k] : in[k]);
+            for (int k = 0; k < NBG; k++) w = QPP_QUAD_NOCRYPTO ? w ^ (SEAL ? out[k] : in[k]) : gh.mulx(w, SEAL ? out[k] : in[k]);
         } else {
 #pragma unroll
             for (int k = 0; k < NBG; k++) {
                 const int t = t0 + 4 * k, j = t - 1;
                 const bool full = t >= 1 && j < nfull, part = rem && j == nfull, lenslot = has && t == m + 1;
                 if (full) st_payload(at(pay + 16 * (uint32_t)j), out[k]);
-                if (part) st_bytes(at(pay + 16 * (uint32_t)j), keep_bytes(out[k], (uint32_t)rem), (uint32_t)rem);
+                if (part && !QPP_QUAD_NOIO) st_bytes(at(pay + 16 * (uint32_t)j), keep_bytes(out[k], (uint32_t)rem), (uint32_t)rem);
                 // the length block rides in the slot after the payload when the group reaches it
                 const uint4 x = lenslot ? lenblk() : part ? keep_bytes(SEAL ? out[k] : in[k], (uint32_t)rem)
                                                         : (SEAL ? out[k] : in[k]);

@@ -20,7 +20,7 @@ def main(d):
         for r in csv.DictReader(open(f)):
             acc[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
     for k, cs in acc.items():
-        if "aes_gcm_kernel" not in k and "chacha_kernel" not in k:
+        if not any(s in k for s in ("aes_gcm", "chacha", "ttab")):
             continue
         print("== counters per dispatch:", k[:90])
         for c, v in sorted(cs.items()):

@@ -72,7 +72,7 @@ def _check(text):
 
 
 def test_resource_check_rejects_static_lds_and_scratch(tmp_path):
-    name = "_ZN3qpp12_GLOBAL__N_114aes_gcm_kernelILb1ELi4ELi512ELi10EEEvPK"
+    name = "_ZN3qpp12_GLOBAL__N_119aes_gcm_quad_kernelILb1ELi10EEEvPKNS_6DevKeyE"
     ok = tmp_path / "ok.res"
     ok.write_text(f"x: remark: Function Name: {name}\nx: remark:     ScratchSize [bytes/lane]: 0\n"
                   "x: remark:     LDS Size [bytes/block]: 0\n")
@@ -85,8 +85,8 @@ def test_resource_check_rejects_static_lds_and_scratch(tmp_path):
     scr.write_text(f"x: remark: Function Name: {name}\nx: remark:     ScratchSize [bytes/lane]: 12\n")
     r = _check(str(scr))
     assert r.returncode != 0 and "scratch" in r.stderr
-    # a non-default variant may use scratch (it is a tuning knob, not the product path)
+    # a kernel outside the no-spill set (AES-256) may use scratch; it may not add static LDS either
     other = tmp_path / "other.res"
-    other.write_text("x: remark: Function Name: _ZN3qpp12_GLOBAL__N_114aes_gcm_kernelILb1ELi2ELi1024ELi10EEEvPK\n"
+    other.write_text("x: remark: Function Name: _ZN3qpp12_GLOBAL__N_119aes_gcm_quad_kernelILb1ELi14EEEvPKNS_6DevKeyE\n"
                      "x: remark:     ScratchSize [bytes/lane]: 52\n")
     assert _check(str(other)).returncode == 0

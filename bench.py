@@ -569,6 +569,33 @@ def txq_bursts(args, ctx, keys, rank, world, max_over_ranks, burst=64):
     proto["aad_len"], proto["pt_len"], proto["pn_len"] = aad, pt, 4
     total = args.warmup + args.steps * 20
     t_start = None
+    if K == 1 and os.path.exists(os.path.join(ROOT, "tools", "libtxqdrive.so")):
+        # one flush at a time, timed around qpp_txq_flush in C (tools/txqdrive.c txq_latency): the engine's latency,
+        # not Python's per-call cost
+        lat_fn = ctypes.CDLL(os.path.join(ROOT, "tools", "libtxqdrive.so")).txq_latency
+        lat_fn.restype = ctypes.c_int
+        lat_fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_uint64,
+                           ctypes.c_void_p]
+        buf = np.zeros(total, dtype=np.float64)
+        if lat_fn(q.handle, proto.ctypes.data, burst, total, pn, buf.ctypes.data) != 0:
+            raise SystemExit("txq_latency failed")
+        lat = list(buf[args.warmup:] * 1e-6)
+        wall = max_over_ranks(float(np.sum(buf[args.warmup:])) * 1e-6)
+        n_timed = total - args.warmup
+        if rank == 0:
+            print(json.dumps({
+                "metric": f"txq {burst}-packet GSO bursts of {pt} B (sealed + HP in place on the pinned ring), 1 in "
+                          f"flight, flush latency median", "unit": "us", "n_gpus": world, "suite": args.suite,
+                "bursts": n_timed, "value": round(1e6 * max_over_ranks(float(np.median(lat))), 1),
+                "higher_is_better": False, "p10_us": round(1e6 * float(np.percentile(lat, 10)), 1),
+                "p90_us": round(1e6 * float(np.percentile(lat, 90)), 1),
+                "burst_gib_s": round(n_timed * burst * pt * world / wall / GiB, 3),
+                "path": "persistent server (qpp_txq_create_persistent)" if persistent else "launched kernels",
+                "driver": "tools/txqdrive.c txq_latency (qpp_txq_flush timed in C)",
+                "flushes_served_launched_starts": list(q.info())}), flush=True)
+        q.close()
+        ctx.close()
+        return
     if drive is not None:  # the transport's loop in C (tools/txqdrive.c): the engine, not Python, is measured
         drive(q.handle, proto.ctypes.data, burst, burst * stride, K, max(K, args.warmup * 4), 1 << 40)
         wall = drive(q.handle, proto.ctypes.data, burst, burst * stride, K, args.steps * 20, 1 << 41)

@@ -2068,9 +2068,14 @@ static int srv_submit(qpp_txq *q) {
     const uint32_t W = kTxsWaves;
     std::vector<uint32_t> &ord = q->order;
     ord.resize(n);
-    for (uint32_t i = 0; i < n; i++) ord[i] = i;
-    std::stable_sort(ord.begin(), ord.end(),
-                     [&sl](uint32_t a, uint32_t b) { return sl.h_desc[a].key_idx < sl.h_desc[b].key_idx; });
+    bool one_key = true;  // (the usual GSO burst: one connection's key; no sort then)
+    for (uint32_t i = 0; i < n; i++) {
+        ord[i] = i;
+        one_key = one_key && sl.h_desc[i].key_idx == sl.h_desc[0].key_idx;
+    }
+    if (!one_key)
+        std::stable_sort(ord.begin(), ord.end(),
+                         [&sl](uint32_t a, uint32_t b) { return sl.h_desc[a].key_idx < sl.h_desc[b].key_idx; });
     // packets per item: spread the flush over the server's workgroups, at most one packet per wave
     const uint32_t per = std::max(1u, std::min(W, (n + q->srv_wgs - 1) / q->srv_wgs));
     uint32_t items = 0;

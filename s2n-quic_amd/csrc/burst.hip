@@ -26,7 +26,8 @@ using namespace dev;
 constexpr uint32_t kBurstAes = 0;
 constexpr uint32_t kBurstGh = 65536;
 constexpr uint32_t kBurstTab = 8192;
-constexpr uint32_t kBurstLds = kBurstGh + 7 * kBurstTab;  // 120 KiB: one workgroup per CU
+constexpr uint32_t kBurstHpRk = kBurstGh + 7 * kBurstTab;  // the work item key's HP round keys (240 B)
+constexpr uint32_t kBurstLds = kBurstHpRk + 256;          // 120 KiB + 256 B: one workgroup per CU
 #ifndef QPP_BURST_WAVES
 #define QPP_BURST_WAVES 8  // measured: 4 waves 34 / 80 / 137 us seal at 64 / 4096 / 8192 packets, 8 waves 30 / 56 / 93, 12 waves 29 / 62 / 91
 #endif
@@ -156,9 +157,9 @@ __device__ __forceinline__ void burst_packet(const AesLds &aes, const DevKey *__
     uint8_t *pay = p.base + p.aad_len;
     const uint32_t a = (p.aad_len + 15u) >> 4, c = (p.len + 15u) >> 4, m = a + c + 1;
     const uint32_t K = (m + 63u) >> 6, pad = 64u * K - m;
-    // Each lane reads at most one 16-byte block per pass (a payload block or an AAD block).  Pass k + 1's read is
-    // issued before pass k's AES, so a packet pays one memory round trip, not one per pass (over PCIe, from the
-    // pinned ring of a txq flush, a round trip is ~1.5 us: most of a 64-packet flush once did nothing else).
+    // Each lane reads at most one 16-byte block per pass (a payload block or an AAD block).  The reads of a pair of
+    // passes are issued before the previous pair's AES, so a packet pays one memory round trip, not one per pass
+    // (over PCIe, from the pinned ring of a txq flush, a round trip is ~1.5-2.5 us).
     auto block = [&](uint32_t k) {
         const int i = (int)(lane + 64u * k) - (int)pad;
         uint4 v = make_uint4(0, 0, 0, 0);
@@ -167,36 +168,36 @@ __device__ __forceinline__ void burst_packet(const AesLds &aes, const DevKey *__
         return v;
     };
     TXS_STAMP(0);
-    uint4 next = block(0);
-    // header-protection round keys and header bytes: issued now, used after the GHASH tree (one memory round trip
-    // off the end of the chain)
+    uint4 nx0 = block(0), nx1 = K > 1 ? block(1) : make_uint4(0, 0, 0, 0);
+    // header-protection round keys and header bytes: issued now, used after the passes (one memory round trip off
+    // the end of the chain)
     constexpr int HNR = NR == 10 ? 10 : 14;
+    const bool hp_on = SEAL && (flags & (QPP_HP_MASK_OUT | QPP_HP_APPLY)) != 0;
     HpPrefetch<HNR> hpk;
-    if (SEAL && (flags & (QPP_HP_MASK_OUT | QPP_HP_APPLY)) && lane == 0 && p.pn_len >= 1 && p.pn_len <= 4) {
-        if constexpr (LDSKEY) hpk.load_hdr(p.base, p.aad_len - p.pn_len, flags);
-        else hpk.load(key->hp_rk, p.base, p.aad_len - p.pn_len, flags);
-    }
+    constexpr uint32_t hp_lds = LDSKEY ? kTxsKey + 16 + 240 : kBurstHpRk;  // the HP round keys in LDS
+    if (hp_on && lane == 0 && p.pn_len >= 1 && p.pn_len <= 4) hpk.load_hdr(p.base, p.aad_len - p.pn_len, flags);
     uint4 acc = make_uint4(0, 0, 0, 0), ct0 = acc, ct1 = acc;  // ct0/ct1: ciphertext blocks 0/1 where owned
     uint4 ek = acc;  // E_K(J0), computed in pass 0 by the idle lane pad - 1 inside the data lanes' AES stream
-    for (uint32_t k = 0; k < K; k++) {
+    // counter block of this lane in pass k (data block b uses counter b + 2; J0 = counter 1 for everything else)
+    auto ctr = [&](uint32_t k) {
+        const int i = (int)(lane + 64u * k) - (int)pad;
+        const bool data = i >= (int)a && i < (int)(a + c);
+        return make_uint4(p.n0, p.n1, p.n2, bswap32(data ? (uint32_t)(i - (int)a) + 2u : 1u));
+    };
+    // pass k's payload block, the stores and the Horner step (acc * H^64 ^ x)
+    auto pass = [&](uint32_t k, const uint4 &raw, const uint4 &ks) {
         const int i = (int)(lane + 64u * k) - (int)pad;  // block index in the GHASH sequence
         const bool data = i >= (int)a && i < (int)(a + c);
-        const bool j0 = k == 0 && i == -1;
-        const uint32_t b = (uint32_t)i - a;  // data block b uses counter b + 2
-        const uint4 raw = next;
-        if (k + 1 < K) next = block(k + 1);
-        if (k == 0) TXS_STAMP(1);
-        uint4 in = data ? raw : make_uint4(0, 0, 0, 0), ks = make_uint4(0, 0, 0, 0);
-        if (data || j0) ks = aes.encrypt<NR>(make_uint4(p.n0, p.n1, p.n2, bswap32(data ? b + 2u : 1u)), rk);
+        const uint32_t b = (uint32_t)i - a;
+        if (k == 0 && i == -1) ek = ks;
         uint4 x = make_uint4(0, 0, 0, 0);
-        if (j0) ek = ks;
         if (i >= 0 && i < (int)a) {
             const uint32_t off = 16u * (uint32_t)i;
             x = raw;
             if (p.aad_len - off < 16u) x = keep_bytes(x, p.aad_len - off);
         } else if (data) {
             const uint32_t r = p.len - 16u * b;
-            uint4 out = in ^ ks;
+            uint4 in = raw, out = raw ^ ks;
             if (r >= 16u) {
                 st16(pay + 16u * b, out);
             } else {
@@ -211,49 +212,86 @@ __device__ __forceinline__ void burst_packet(const AesLds &aes, const DevKey *__
             x = make_uint4(0, bswap32(p.aad_len * 8u), 0, bswap32(p.len * 8u));  // be64 bit lengths
         }
         acc = k ? gmul(tab(6), acc) ^ x : x;
+    };
+    auto rkey = [&](int r, uint32_t (&k)[4]) {
+        k[0] = rk[4 * r]; k[1] = rk[4 * r + 1]; k[2] = rk[4 * r + 2]; k[3] = rk[4 * r + 3];
+    };
+    // Passes in pairs: the two passes' AES chains are independent, so they run interleaved (one chain of dependent
+    // LDS rounds for both instead of one each); a pass past the packet (K odd) computes a discarded block.
+    for (uint32_t k = 0; k < K; k += 2) {
+        const uint4 r0 = nx0, r1 = nx1;
+        if (k + 2 < K) nx0 = block(k + 2);
+        if (k + 3 < K) nx1 = block(k + 3);
+        if (k == 0) TXS_STAMP(1);
+        const uint4 c0 = ctr(k), c1 = ctr(k + 1);
+        uint32_t kk[4];
+        rkey(0, kk);
+        uint32_t s0[4] = {c0.x ^ kk[0], c0.y ^ kk[1], c0.z ^ kk[2], c0.w ^ kk[3]};
+        uint32_t s1[4] = {c1.x ^ kk[0], c1.y ^ kk[1], c1.z ^ kk[2], c1.w ^ kk[3]};
+#pragma unroll
+        for (int r = 1; r < NR; r++) {
+            rkey(r, kk);
+            aes.round(s0, kk);
+            aes.round(s1, kk);
+        }
+        rkey(NR, kk);
+        const uint4 ks0 = aes.final(s0, kk), ks1 = aes.final(s1, kk);
+        pass(k, r0, ks0);
+        if (k + 1 < K) pass(k + 1, r1, ks1);
     }
     TXS_STAMP(2);
+    // Header protection (seal): the sample (ciphertext || tag)[4 - pn_len, 20 - pn_len) (payload.rs:151-169) lies in
+    // ciphertext blocks 0 and 1 unless the payload is short (then it runs into the tag: after the tag, below).  Every
+    // lane computes the mask of the same sample, in the same basic block as the lane tree, so that the two dependent
+    // chains (AES rounds, tree levels) overlap instead of adding up.
+    const uint32_t s_off = 4u - p.pn_len;
+    const bool hp_ok = hp_on && p.pn_len >= 1 && p.pn_len <= 4 && p.len >= s_off;  // (uniform)
+    const bool hp_early = hp_ok && p.len >= s_off + 16u;
+    uint4 hmask = make_uint4(0, 0, 0, 0);
+    if constexpr (SEAL) {
+        const uint32_t o0 = (pad + a) & 63u;
+        const uint4 c0 = shfl4(ct0, (int)o0), c1 = shfl4(ct1, (int)((o0 + 1u) & 63u));
+        const uint32_t sh = s_off & 3u;  // (pn_len outside 1..4: any shift, the mask is not used)
+        const uint4 smp = make_uint4(__builtin_amdgcn_alignbyte(c0.y, c0.x, sh), __builtin_amdgcn_alignbyte(c0.z, c0.y, sh),
+                                     __builtin_amdgcn_alignbyte(c0.w, c0.z, sh), __builtin_amdgcn_alignbyte(c1.x, c0.w, sh));
+        const uint4 smp0 = s_off == 0u ? c0 : smp;  // pn_len 4: the sample is block 0
+        hmask = aes.encrypt_lrk<HNR>(smp0, hp_lds);
+    }
     // lane tree: level t combines lanes l and l + 2^t (l a multiple of 2^(t+1)) as v_l * H^(2^t) ^ v_(l+2^t)
 #pragma unroll
     for (int t = 0; t < 6; t++) acc = gmul(tab(t), acc) ^ shfl4_down(acc, 1u << t);
     TXS_STAMP(3);
-    const uint4 ek0 = pad ? shfl4(ek, (int)pad - 1)  // (pad == 0: no idle lane in pass 0)
-                          : aes.encrypt<NR>(make_uint4(p.n0, p.n1, p.n2, bswap32(1u)), rk);
+    uint4 ek0;
+    if (pad) {
+        ek0 = shfl4(ek, (int)pad - 1);
+    } else {  // (pad == 0: no idle lane in pass 0)
+        ek0 = aes.encrypt<NR>(make_uint4(p.n0, p.n1, p.n2, bswap32(1u)), rk);
+    }
     const uint4 tag = shfl4(gmul(tab(0), acc), 0) ^ ek0;  // Y = Q * H, from lane 0
 
     if (SEAL) {
         if (lane == 0) st16(pay + p.len, tag);
         int8_t st = QPP_OK;
-        if (flags & (QPP_HP_MASK_OUT | QPP_HP_APPLY)) {
-            // sample = (ciphertext || tag)[4 - pn_len, 20 - pn_len)  (payload.rs:151-169), from registers
-            const uint32_t s = 4u - p.pn_len;
-            if (p.pn_len < 1 || p.pn_len > 4 || p.len < s) {
+        if (hp_on) {
+            if (!hp_ok) {
                 st = QPP_DECODE_ERROR;
-            } else {
+            } else if (hp_early) {
+                if (lane == 0) hpk.apply(hmask, p.base, p.aad_len - p.pn_len, p.pn_len, masks + 5 * (size_t)pi, flags);
+            } else {  // short payload: the sample runs into the tag
                 const uint32_t o0 = (pad + a) & 63u;
                 const uint4 c0 = shfl4(ct0, (int)o0), c1 = shfl4(ct1, (int)((o0 + 1u) & 63u));
-                uint4 smp;
-                if (p.len >= s + 16u) {  // the sample lies in ciphertext blocks 0 and 1
-                    smp = make_uint4(__builtin_amdgcn_alignbyte(c0.y, c0.x, s), __builtin_amdgcn_alignbyte(c0.z, c0.y, s),
-                                     __builtin_amdgcn_alignbyte(c0.w, c0.z, s), __builtin_amdgcn_alignbyte(c1.x, c0.w, s));
-                } else {  // short payload: the sample runs into the tag
-                    uint32_t w[4] = {0, 0, 0, 0};
+                uint32_t w[4] = {0, 0, 0, 0};
 #pragma unroll
-                    for (uint32_t q = 0; q < 16; q++) {
-                        const uint32_t pos = s + q;
-                        const uint32_t v = pos < p.len ? (pos < 16u ? byte_of(c0, pos) : byte_of(c1, pos - 16u))
-                                                       : byte_of(tag, pos - p.len);
-                        w[q >> 2] |= v << (8 * (q & 3));
-                    }
-                    smp = make_uint4(w[0], w[1], w[2], w[3]);
+                for (uint32_t q = 0; q < 16; q++) {
+                    const uint32_t pos = s_off + q;
+                    const uint32_t v = pos < p.len ? (pos < 16u ? byte_of(c0, pos) : byte_of(c1, pos - 16u))
+                                                   : byte_of(tag, pos - p.len);
+                    w[q >> 2] |= v << (8 * (q & 3));
                 }
-                if (lane == 0) {
-                    if constexpr (LDSKEY)
-                        hpk.finish_lds(aes, kTxsKey + 16 + 240, smp, p.base, p.aad_len - p.pn_len, p.pn_len,
-                                       masks + 5 * (size_t)pi, flags);
-                    else
-                        hpk.finish(aes, smp, p.base, p.aad_len - p.pn_len, p.pn_len, masks + 5 * (size_t)pi, flags);
-                }
+                const uint4 smp = make_uint4(w[0], w[1], w[2], w[3]);
+                if (lane == 0)
+                    hpk.apply(aes.encrypt_lrk<HNR>(smp, hp_lds), p.base, p.aad_len - p.pn_len, p.pn_len,
+                              masks + 5 * (size_t)pi, flags);
             }
         }
         TXS_STAMP(4);
@@ -301,6 +339,7 @@ __global__ __launch_bounds__(kBurstWG) void aes_gcm_burst_kernel(const DevKey *_
         pi0 = perm[w.begin + wave];
         d0 = descs[pi0];
     }
+    if (threadIdx.x < 60) lds_st32(kBurstHpRk + 4 * threadIdx.x, key->hp_rk[threadIdx.x]);  // (burst_tables' barrier)
     burst_tables(key, w.key, pow);
     const AesLds aes = make_aes(kBurstAes);
     uint32_t rk[4 * (NR + 1)];
@@ -370,6 +409,7 @@ __global__ __launch_bounds__(kBurstWG) void txq_server_kernel(const DevKey *keys
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
     TxsSlot *slot = slots + blockIdx.x;
     uint32_t seen = seq0, cached = 0xffffffffu, epoch = 0xffffffffu;
+    uint64_t t_seen = 0;  // thread 0: when this workgroup saw the flush (s_memrealtime)
     for (;;) {
         if (wave == 0) {
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -401,9 +441,9 @@ __global__ __launch_bounds__(kBurstWG) void txq_server_kernel(const DevKey *keys
             if (lane < kTxsPollLanes) lds_st128(kTxsCtl + 16 * lane, cur);
             if (lane == 0) {
                 lds_st32(kTxsStopFlag, stop);
-                if (!stop && blockIdx.x == 0)
-                    __hip_atomic_store(&mail->t_seen, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_SYSTEM);
+                // (telemetry stamp kept in a register and stored with t_done: a store here would be waited for by
+                // the acquire below and by this wave's first payload loads -- a PCIe write round trip)
+                t_seen = __builtin_amdgcn_s_memrealtime();
                 // Every flush: the CU's vector cache (and L2's non-coherent lines) dropped, so that this flush's ring
                 // bytes are read from the host, not the lines the previous flush left for the same offsets (the ring
                 // is reused flush after flush; without it, every flush after the first of one server launch sealed
@@ -479,6 +519,7 @@ __global__ __launch_bounds__(kBurstWG) void txq_server_kernel(const DevKey *keys
                 }
                 __hip_atomic_store(&mail->t_done, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(&mail->t_seen, t_seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
             __hip_atomic_store(&slot->done, seen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }

@@ -141,6 +141,24 @@ struct AesLds {
                           last(s[2], s[3], s[0], s[1], rk[2]), last(s[3], s[0], s[1], s[2], rk[3]));
     }
 
+    // Full AES of one block with the round keys in LDS at byte offset o (read where used: no 44 / 60 registers held)
+    template <int NR>
+    __device__ __forceinline__ uint4 encrypt_lrk(uint4 in, uint32_t o) const {
+        auto k4 = [&](int r, uint32_t (&k)[4]) {
+            const uint4 v = lds_ld128(o + 16u * (uint32_t)r);
+            k[0] = v.x; k[1] = v.y; k[2] = v.z; k[3] = v.w;
+        };
+        uint32_t k[4];
+        k4(0, k);
+        uint32_t s[4] = {in.x ^ k[0], in.y ^ k[1], in.z ^ k[2], in.w ^ k[3]};
+#pragma unroll
+        for (int r = 1; r < NR; r++) {
+            k4(r, k);
+            round(s, k);
+        }
+        k4(NR, k);
+        return final(s, k);
+    }
     // Full AES of one block (no caching): HP mask, key setup, page-crossing groups.
     template <int NR>
     __device__ __forceinline__ uint4 encrypt(uint4 in, const uint32_t *__restrict__ rk) const {
@@ -419,7 +437,11 @@ struct HpPrefetch {
     }
     __device__ __forceinline__ void finish(const AesLds &aes, uint4 sample, uint8_t *base, uint32_t hdr_len,
                                            uint32_t pn_len, uint8_t *mask_out, uint32_t flags) const {
-        const uint4 m = aes.encrypt<HNR>(sample, rk);
+        apply(aes.encrypt<HNR>(sample, rk), base, hdr_len, pn_len, mask_out, flags);
+    }
+    // m = AES_hp(sample), computed by the caller
+    __device__ __forceinline__ void apply(uint4 m, uint8_t *base, uint32_t hdr_len, uint32_t pn_len, uint8_t *mask_out,
+                                          uint32_t flags) const {
         if (flags & QPP_HP_MASK_OUT) {
             mask_out[0] = (uint8_t)m.x; mask_out[1] = (uint8_t)(m.x >> 8); mask_out[2] = (uint8_t)(m.x >> 16);
             mask_out[3] = (uint8_t)(m.x >> 24); mask_out[4] = (uint8_t)m.y;

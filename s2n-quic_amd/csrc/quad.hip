@@ -33,27 +33,6 @@ using namespace dev;
 
 constexpr uint32_t kQLdsPow = 131072;  // 4-bit tables of H^1..H^4
 constexpr uint32_t kQLdsVe = 65536;    // V_e during the build
-#ifndef QPP_QUAD_TOUCH
-#define QPP_QUAD_TOUCH 0
-#endif
-#ifndef QPP_QUAD_EARLY_LOADS
-#define QPP_QUAD_EARLY_LOADS 0
-#endif
-#ifndef QPP_QUAD_PIPE
-#define QPP_QUAD_PIPE ctr_keystream_inplace
-#endif
-#ifndef QPP_QUAD_NT
-#define QPP_QUAD_NT 1  // payload stores non-temporal
-#endif
-#ifndef QPP_QUAD_EK_REG
-#define QPP_QUAD_EK_REG 1  // seal: E_K(J0) kept in a register (else stashed in the tag slot and read back)
-#endif
-#ifndef QPP_QUAD_HP_EARLY
-#define QPP_QUAD_HP_EARLY 1  // seal: header protection right after group 0 (the sample is in its ciphertext blocks)
-#endif
-#ifndef QPP_QUAD_DEFER
-#define QPP_QUAD_DEFER 1  // interior groups: the last 64 bytes go out with the next group's first 64
-#endif
 #ifndef QPP_QUAD_WG
 #define QPP_QUAD_WG 768  // AES-128: 3 waves per SIMD (<= 168 VGPRs); 1024 (4 waves, <= 128) spilled
 #endif
@@ -77,11 +56,7 @@ __device__ __forceinline__ void st_payload(uint8_t *p, uint4 v) {
 #if QPP_QUAD_NOIO
     return;
 #endif
-#if QPP_QUAD_NT
-    st16_nt(p, v);
-#else
-    st16(p, v);
-#endif
+    st16_nt(p, v);  // streaming: the sealed / opened bytes are not read again
 }
 template <int NR>
 constexpr int kQuadWG = NR == 10 ? QPP_QUAD_WG : QPP_QUAD_WG256;
@@ -242,7 +217,7 @@ __device__ __forceinline__ void quad_packet(const AesLds &aes, const GhashT<true
     constexpr int HNR = NR == 10 ? 10 : 14;
     const bool want_hp = SEAL && (flags & (QPP_HP_MASK_OUT | QPP_HP_APPLY)) != 0;
     uint4 ek0 = make_uint4(0, 0, 0, 0);  // seal: E_K(J0) (slot 0: lane 0, group 0)
-    uint4 held = make_uint4(0, 0, 0, 0);  // QPP_QUAD_DEFER: the previous interior group's blocks k = 3
+    uint4 held = make_uint4(0, 0, 0, 0);  // the previous interior group's blocks k = 3 (deferred last chunk)
     bool held_ok = false;
     bool hp_done = false;                // seal: header protection applied after group 0 (quad-uniform)
     // Header protection as soon as the sample exists: the sample (ciphertext bytes [4 - pn_len, 20 - pn_len),
@@ -280,48 +255,7 @@ __device__ __forceinline__ void quad_packet(const AesLds &aes, const GhashT<true
         const int t0 = 16 * g + (int)s;
         uint4 ks[NBG];
         const uint32_t c0 = (uint32_t)t0 + 1u;
-#if QPP_QUAD_TOUCH
-        // Touch the next group's 256 payload bytes (one dword per lane, 64 B apart) before this group's keystream, so
-        // that its loads -- issued after the keystream, where their latency is exposed -- find the lines in L2.  The
-        // value is folded into `touch`, which nothing reads (kept alive by the asm below).
-        uint32_t tv = 0;
-        if (g + 1 < G) {
-            const uint32_t o = 16u * (uint32_t)(16 * (g + 1) - 1) + 64u * s;
-            __builtin_memcpy(&tv, at(pay + (o + 4 <= len + 16 ? o : 0u)), 4);
-        }
-#endif
-#if QPP_QUAD_EARLY_LOADS
-        // payload loads issued before the keystream: their latency passes under the AES pipeline
-        uint4 in[NBG];
-        if (inner) {
-            const uint32_t b = pay + 16 * (uint32_t)(t0 - 1);
-#pragma unroll
-            for (int k = 0; k < NBG; k++) in[k] = ld16(at(b + 64 * k));
-        } else {
-#pragma unroll
-            for (int k = 0; k < NBG; k++) {
-                const int j = t0 + 4 * k - 1;
-                in[k] = ld16(at(pay + (j >= 0 && 16 * j <= (int)len ? 16 * (uint32_t)j : 0u)));
-            }
-        }
-        // The nonce words are laundered where the loop uses them (a new page; the straddling group): left alone, the
-        // compiler hoisted the page build's first-round lookups addresses out of the loop as loop invariants and
-        // spilled them (16 scratch accesses per group in the open kernel).
-        uint32_t m0 = n0, m1 = n1, m2 = n2;
-        if ((g & 15) != 15) {  // uniform: no lane's counters straddle a 256-block page
-            if ((c0 >> 8) != pg.page) {
-                asm volatile("" : "+v"(m0), "+v"(m1), "+v"(m2));
-                pg.build(aes, rk, m0, m1, m2, c0 >> 8);
-            }
-            QPP_QUAD_PIPE<NR, NBG, 4>(aes, pg, rk, c0, ks);
-        } else {
-            asm volatile("" : "+v"(m0), "+v"(m1), "+v"(m2));
-            static_for<NBG>([&](auto kc) {
-                constexpr int k = decltype(kc)::value;
-                ks[k] = aes.encrypt<NR>(make_uint4(m0, m1, m2, bswap32(c0 + 4 * k)), rk);
-            });
-        }
-#elif QPP_QUAD_NOCRYPTO
+#if QPP_QUAD_NOCRYPTO
 #pragma unroll
         for (int k = 0; k < NBG; k++) ks[k] = make_uint4(c0 + 4 * k, n0, n1, n2);
         uint4 in[NBG];
@@ -346,7 +280,7 @@ __device__ __forceinline__ void quad_packet(const AesLds &aes, const GhashT<true
                 asm volatile("" : "+v"(m0), "+v"(m1), "+v"(m2));
                 pg.build(aes, rk, m0, m1, m2, c0 >> 8);
             }
-            QPP_QUAD_PIPE<NR, NBG, 4>(aes, pg, rk, c0, ks);
+            ctr_keystream_inplace<NR, NBG, 4>(aes, pg, rk, c0, ks);
         } else {
             asm volatile("" : "+v"(m0), "+v"(m1), "+v"(m2));
             static_for<NBG>([&](auto kc) {
@@ -373,17 +307,12 @@ __device__ __forceinline__ void quad_packet(const AesLds &aes, const GhashT<true
 #pragma unroll
         for (int k = 0; k < NBG; k++) out[k] = in[k] ^ ks[k];
         if constexpr (SEAL) {
-            // E_K(J0) (slot 0, lane 0) waits in the tag's place until the tag is known (4 VGPRs fewer across the loop;
-            // opening needs the received tag there and recomputes E_K(J0) on the quad at the end instead)
-#if QPP_QUAD_EK_REG
+            // E_K(J0) (slot 0, lane 0) kept in a register until the tag is known (opening recomputes it on the quad at
+            // the end instead)
             if (g == 0) ek0 = ks[0];
-#else
-            if (g == 0 && has && s == 0) st16(at(pay + len), ks[0]);
-#endif
         }
         if (inner) {
             const uint32_t b = pay + 16 * (uint32_t)(t0 - 1);
-#if QPP_QUAD_DEFER
             // The 64-byte segment that straddles two groups' ciphertext gets its two parts from stores a whole group
             // apart, and in between L2 had often written the first part back on its own (a second partial write of
             // the segment).  So between interior groups the last 64 bytes (blocks k = 3) wait for the next group and
@@ -395,10 +324,6 @@ __device__ __forceinline__ void quad_packet(const AesLds &aes, const GhashT<true
             held_ok = interior(g + 1) && (g + 1 < G - 1 || tail_slots > 12);  // uniform: the next group is interior
             if (held_ok) held = out[NBG - 1];
             else st_payload(at(b + 64 * (NBG - 1)), out[NBG - 1]);
-#else
-#pragma unroll
-            for (int k = 0; k < NBG; k++) st_payload(at(b + 64 * k), out[k]);
-#endif
 #pragma unroll
             for (int k = 0; k < NBG; k++) w = QPP_QUAD_NOCRYPTO ? w ^ (SEAL ? out[k] : in[k]) : gh.mulx(w, SEAL ? out[k] : in[k]);
         } else {
@@ -415,12 +340,7 @@ __device__ __forceinline__ void quad_packet(const AesLds &aes, const GhashT<true
                 len_done = len_done || lenslot;
             }
         }
-#if QPP_QUAD_TOUCH
-        asm volatile("" ::"v"(tv));
-#endif
-#if QPP_QUAD_HP_EARLY
         if (SEAL && g == 0) hp_early(out[0]);
-#endif
     };
     for (int g = 0; g + 1 < G; g++) group(std::integral_constant<int, 4>{}, g);
     if (G > 0) {  // the last group with as few counter blocks per lane as its longest packet needs
@@ -445,11 +365,7 @@ __device__ __forceinline__ void quad_packet(const AesLds &aes, const GhashT<true
     y = y ^ qperm<kQuadSwap2>(y);
 
     if constexpr (SEAL) {
-#if QPP_QUAD_EK_REG
         if (has && s == 0) st16(at(pay + len), y ^ ek0);  // tag = GHASH ^ E_K(J0)
-#else
-        if (has && s == 0) st16(at(pay + len), y ^ ld16(at(pay + len)));  // tag = GHASH ^ E_K(J0) (stashed at group 0)
-#endif
         const qpp_pkt dt = reload_desc(dptr);
         const uint32_t pn_len = dt.pn_len;
         const bool hp = want_hp && has && pn_len >= 1 && pn_len <= 4 && len >= 4 - pn_len;  // quad-uniform

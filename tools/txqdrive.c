@@ -4,6 +4,8 @@
  *
  *   double txq_drive(qpp_txq *q, const qpp_pkt *proto, size_t burst, size_t region_bytes, size_t regions,
  *                    size_t bursts, uint64_t pn0)  -> seconds for `bursts` bursts (all waited for), < 0 on error
+ *   int txq_latency(qpp_txq *q, const qpp_pkt *proto, size_t burst, size_t bursts, uint64_t pn0, double *lat_us)
+ *        -> one burst at a time: push, then qpp_txq_flush (seal and wait); lat_us[k] = that call's duration
  */
 #include <stdint.h>
 #include <stdlib.h>
@@ -42,4 +44,20 @@ double txq_drive(qpp_txq *q, const qpp_pkt *proto, size_t burst, size_t region_b
     free(d);
     free(tickets);
     return t;
+}
+
+int txq_latency(qpp_txq *q, const qpp_pkt *proto, size_t burst, size_t bursts, uint64_t pn0, double *lat_us) {
+    qpp_pkt *d = (qpp_pkt *)malloc(sizeof(qpp_pkt) * burst);
+    if (!d) return -1;
+    uint64_t pn = pn0;
+    for (size_t k = 0; k < bursts; k++) {
+        memcpy(d, proto, sizeof(qpp_pkt) * burst);
+        for (size_t i = 0; i < burst; i++) d[i].pn = pn++;
+        if (qpp_txq_push_descs(q, d, burst) != QPP_OK) return -3;
+        const double t0 = now_s();
+        if (qpp_txq_flush(q) != QPP_OK) return -4;
+        lat_us[k] = 1e6 * (now_s() - t0);
+    }
+    free(d);
+    return 0;
 }

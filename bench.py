@@ -403,10 +403,24 @@ def e2e(args, rank, world, local_rank):
 
     phase = {"rotate": 0.0, "pipeline": 0.0}
 
+    # The rotation runs in C (tools/txqdrive.c rotate_keys: update_batch, slot_batch, free_batch, set_conn_keys over
+    # raw handles, as the transport calls the ABI) when the helper is built; else through the Python wrappers
+    rot = None
+    if args.rotate and os.path.exists(os.path.join(ROOT, "tools", "libtxqdrive.so")):
+        rot = ctypes.CDLL(os.path.join(ROOT, "tools", "libtxqdrive.so")).rotate_keys
+        rot.restype = ctypes.c_int
+        rot.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+        handles = np.array([k.handle for k in keys], dtype=np.uint64)
+        for k in keys:
+            k.handle = None  # (owned by `handles` from here on)
+
     def step():
         nonlocal keys, slots
         t0 = time.perf_counter()
-        if args.rotate:
+        if rot is not None:
+            if rot(ctx.handle, handles.ctypes.data, len(handles), slots.ctypes.data) != 0:
+                raise SystemExit("rotate_keys failed")
+        elif args.rotate:
             new = ctx.update_keys(keys, slots_out=slots)  # the new slots in one call
             ctx.free_keys(keys)
             keys = new
@@ -458,6 +472,10 @@ def e2e(args, rank, world, local_rank):
         }), flush=True)
     for k in keys:
         k.free()
+    if rot is not None:
+        lib = qpp.lib()
+        for h in handles:
+            lib.qpp_key_free(ctypes.c_void_p(int(h)))
     ctx.host_free(host)
     ctx.close()
 

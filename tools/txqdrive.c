@@ -6,6 +6,10 @@
  *                    size_t bursts, uint64_t pn0)  -> seconds for `bursts` bursts (all waited for), < 0 on error
  *   int txq_latency(qpp_txq *q, const qpp_pkt *proto, size_t burst, size_t bursts, uint64_t pn0, double *lat_us)
  *        -> one burst at a time: push, then qpp_txq_flush (seal and wait); lat_us[k] = that call's duration
+ *   int rotate_keys(qpp_ctx *ctx, qpp_key **keys, size_t n, uint32_t *slots)
+ *        -> a KeySet rotation of every connection (BASELINE configs[4]): keys[i] <- its next-phase key
+ *           (qpp_key_update_batch), the old keys freed (qpp_key_free_batch), slots[i] = the new slots, and the
+ *           connection table repointed (qpp_ctx_set_conn_keys), as the transport would call it
  */
 #include <stdint.h>
 #include <stdlib.h>
@@ -60,4 +64,18 @@ int txq_latency(qpp_txq *q, const qpp_pkt *proto, size_t burst, size_t bursts, u
     }
     free(d);
     return 0;
+}
+
+int rotate_keys(qpp_ctx *ctx, qpp_key **keys, size_t n, uint32_t *slots) {
+    qpp_key **next = (qpp_key **)malloc(sizeof(qpp_key *) * (n ? n : 1));
+    if (!next) return -1;
+    int rc = qpp_key_update_batch((qpp_key *const *)keys, n, next);
+    if (rc == QPP_OK) {
+        qpp_key_slot_batch((const qpp_key *const *)next, n, slots);
+        qpp_key_free_batch((qpp_key *const *)keys, n);
+        memcpy(keys, next, sizeof(qpp_key *) * n);
+        rc = qpp_ctx_set_conn_keys(ctx, slots, n);
+    }
+    free(next);
+    return rc;
 }

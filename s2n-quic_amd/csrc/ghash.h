@@ -20,6 +20,9 @@ namespace dev {
 // {4-11,16-19,28-31}, and the same + 32) the lanes have distinct r, hence distinct j: one LDS cycle per group.
 // The word part of that order is a rotation of Z's words by q (W[k] = Z.w[(k + q) & 3], two v_cndmask levels),
 // the byte part a per-lane v_perm selector; the address (x << 8 | j << 4) is that one v_perm.
+#ifndef QPP_GHASH_DEPTH
+#define QPP_GHASH_DEPTH 9  // LDS reads in flight per GHASH product (PIPE)
+#endif
 template <bool PIPE>
 struct GhashT {
     uint32_t lc[4];   // byte i of lc[k] = 16 * j(k, i)
@@ -68,6 +71,7 @@ struct GhashT {
             const uint4 h = xor3(e, f, look<3, 3>(w));
             return xor3(g, h, c);
         }
+        if constexpr (QPP_GHASH_DEPTH != 9) return prod_d<QPP_GHASH_DEPTH>(w, c);
         uint4 l[16];
         auto issue = [&](auto ic) {
             constexpr int i = decltype(ic)::value;
@@ -93,6 +97,26 @@ struct GhashT {
         const uint4 f = xor3(l[12], l[13], l[14]);
         const uint4 h = xor3(e, f, l[15]);
         return xor3(g, h, c);
+    }
+    // D reads in flight (D a multiple of 3): each consumed triple's registers take the next 3 reads
+    template <int D>
+    __device__ __forceinline__ uint4 prod_d(const uint4 &w, uint4 c) const {
+        uint4 l[16], x[5];
+        auto issue = [&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            if constexpr (i < 16) l[i] = look<i / 4, i % 4>(w);
+        };
+        static_for<D>(issue);
+        static_for<5>([&](auto tc) {
+            constexpr int t = decltype(tc)::value;
+            __builtin_amdgcn_sched_barrier(0);
+            x[t] = xor3(l[3 * t], l[3 * t + 1], l[3 * t + 2]);
+            issue(std::integral_constant<int, 3 * t + D>{});
+            issue(std::integral_constant<int, 3 * t + D + 1>{});
+            issue(std::integral_constant<int, 3 * t + D + 2>{});
+        });
+        __builtin_amdgcn_sched_barrier(0);
+        return xor3(xor3(x[0], x[1], x[2]), xor3(x[3], x[4], l[15]), c);
     }
     // one chain step: W' = rot(Z * H ^ c)
     __device__ __forceinline__ uint4 mulx(const uint4 &w, uint4 c) const { return rot(prod(w, c)); }

@@ -34,28 +34,13 @@ using namespace dev;
 constexpr uint32_t kQLdsPow = 131072;  // 4-bit tables of H^1..H^4
 constexpr uint32_t kQLdsVe = 65536;    // V_e during the build
 #ifndef QPP_QUAD_WG
-#define QPP_QUAD_WG 768  // AES-128: 3 waves per SIMD (<= 168 VGPRs); 1024 (4 waves, <= 128) spilled
+#define QPP_QUAD_WG 768  // AES-128: 3 waves per SIMD (<= 168 VGPRs); 1024 (4 waves, <= 128) spills, 9 % slower (r03w4)
 #endif
 #ifndef QPP_QUAD_WG256
 #define QPP_QUAD_WG256 768  // AES-256 (60 round-key words, 14 rounds of pipeline state)
 #endif
-#ifndef QPP_QUAD_NOCRYPTO
-#define QPP_QUAD_NOCRYPTO 0  // diagnostic: payload I/O only (no keystream, no GHASH products in the group loop)
-#endif
-#ifndef QPP_QUAD_NOIO
-#define QPP_QUAD_NOIO 0  // diagnostic: no payload loads/stores (compute floor of the kernel shape)
-#endif
-__device__ __forceinline__ uint4 ld_payload(const uint8_t *p, uint32_t salt) {
-#if QPP_QUAD_NOIO
-    return make_uint4(salt, salt * 3u, (uint32_t)(uintptr_t)p, salt ^ 0x5555u);
-#else
-    return ld16(p);
-#endif
-}
+__device__ __forceinline__ uint4 ld_payload(const uint8_t *p) { return ld16(p); }
 __device__ __forceinline__ void st_payload(uint8_t *p, uint4 v) {
-#if QPP_QUAD_NOIO
-    return;
-#endif
     st16_nt(p, v);  // streaming: the sealed / opened bytes are not read again
 }
 template <int NR>
@@ -255,22 +240,6 @@ __device__ __forceinline__ void quad_packet(const AesLds &aes, const GhashT<true
         const int t0 = 16 * g + (int)s;
         uint4 ks[NBG];
         const uint32_t c0 = (uint32_t)t0 + 1u;
-#if QPP_QUAD_NOCRYPTO
-#pragma unroll
-        for (int k = 0; k < NBG; k++) ks[k] = make_uint4(c0 + 4 * k, n0, n1, n2);
-        uint4 in[NBG];
-        if (inner) {
-            const uint32_t b = pay + 16 * (uint32_t)(t0 - 1);
-#pragma unroll
-            for (int k = 0; k < NBG; k++) in[k] = ld_payload(at(b + 64 * k), b + k);
-        } else {
-#pragma unroll
-            for (int k = 0; k < NBG; k++) {
-                const int j = t0 + 4 * k - 1;
-                in[k] = ld_payload(at(pay + (j >= 0 && 16 * j <= (int)len ? 16 * (uint32_t)j : 0u)), pay + j);
-            }
-        }
-#else
         // The nonce words are laundered where the loop uses them (a new page; the straddling group): left alone, the
         // compiler hoisted the page build's first-round lookups addresses out of the loop as loop invariants and
         // spilled them (16 scratch accesses per group in the open kernel).
@@ -294,15 +263,14 @@ __device__ __forceinline__ void quad_packet(const AesLds &aes, const GhashT<true
         if (inner) {
             const uint32_t b = pay + 16 * (uint32_t)(t0 - 1);
 #pragma unroll
-            for (int k = 0; k < NBG; k++) in[k] = ld_payload(at(b + 64 * k), b + k);
+            for (int k = 0; k < NBG; k++) in[k] = ld_payload(at(b + 64 * k));
         } else {
 #pragma unroll
             for (int k = 0; k < NBG; k++) {
                 const int j = t0 + 4 * k - 1;
-                in[k] = ld_payload(at(pay + (j >= 0 && 16 * j <= (int)len ? 16 * (uint32_t)j : 0u)), pay + j);
+                in[k] = ld_payload(at(pay + (j >= 0 && 16 * j <= (int)len ? 16 * (uint32_t)j : 0u)));
             }
         }
-#endif
         uint4 out[NBG];
 #pragma unroll
         for (int k = 0; k < NBG; k++) out[k] = in[k] ^ ks[k];
@@ -325,14 +293,14 @@ __device__ __forceinline__ void quad_packet(const AesLds &aes, const GhashT<true
             if (held_ok) held = out[NBG - 1];
             else st_payload(at(b + 64 * (NBG - 1)), out[NBG - 1]);
 #pragma unroll
-            for (int k = 0; k < NBG; k++) w = QPP_QUAD_NOCRYPTO ? w ^ (SEAL ? out[k] : in[k]) : gh.mulx(w, SEAL ? out[k] : in[k]);
+            for (int k = 0; k < NBG; k++) w = gh.mulx(w, SEAL ? out[k] : in[k]);
         } else {
 #pragma unroll
             for (int k = 0; k < NBG; k++) {
                 const int t = t0 + 4 * k, j = t - 1;
                 const bool full = t >= 1 && j < nfull, part = rem && j == nfull, lenslot = has && t == m + 1;
                 if (full) st_payload(at(pay + 16 * (uint32_t)j), out[k]);
-                if (part && !QPP_QUAD_NOIO) st_bytes(at(pay + 16 * (uint32_t)j), keep_bytes(out[k], (uint32_t)rem), (uint32_t)rem);
+                if (part) st_bytes(at(pay + 16 * (uint32_t)j), keep_bytes(out[k], (uint32_t)rem), (uint32_t)rem);
                 // the length block rides in the slot after the payload when the group reaches it
                 const uint4 x = lenslot ? lenblk() : part ? keep_bytes(SEAL ? out[k] : in[k], (uint32_t)rem)
                                                         : (SEAL ? out[k] : in[k]);

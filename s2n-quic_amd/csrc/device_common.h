@@ -507,11 +507,13 @@ __device__ __forceinline__ uint32_t chacha_hp_word(const uint32_t hk[8], uint4 s
 //   table are INTERNAL_ERROR (never read).  `aes` views T-tables already in LDS.
 // AES_HP = false (the fused ChaCha receive, no T-tables in LDS): a header key that is not a ChaCha20 key is refused
 // (INTERNAL_ERROR) -- the host launches that kernel only when no AES record is live.  A header-key slot that holds no
-// key at all (freed) is refused by both forms, before any header byte is touched.
+// key at all (freed) is refused by both forms, before any header byte is written.
 template <bool AES_HP = true>
+// chosen (optional): the first 16 bytes (suite, nr, hp_nr, live) of the record of the key the packet was sent to,
+// loaded with the rest (the fused receive checks it is a live packet key without another round trip).
 __device__ __forceinline__ qpp_pkt rx_unprotect_one(const AesLds &aes, const DevKey *__restrict__ keys, uint32_t key_cap,
                                                     const qpp_rx_pkt &r, uint8_t *__restrict__ arena, int8_t *status,
-                                                    uint32_t i) {
+                                                    uint32_t i, uint4 *chosen = nullptr) {
     qpp_pkt d{};
     d.off = r.off;
     d.key_idx = r.key_idx[0];
@@ -530,25 +532,33 @@ __device__ __forceinline__ qpp_pkt rx_unprotect_one(const AesLds &aes, const Dev
         return d;
     }
     const DevKey *__restrict__ hk = keys + r.key_idx[0];
-    if (hk->live == 0 || (!AES_HP && hk->suite != QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256)) {
-        d.flags = QPP_PKT_SKIP;
-        status[i] = QPP_INTERNAL_ERROR;
-        return d;
-    }
-    // All three packet loads are issued before the mask is computed (no dependent byte loads after it): byte 0,
-    // the 4 bytes that may hold the PN (len >= hdr + 20 was checked above) and the sample.
+    // The three packet loads (byte 0, the 4 bytes that may hold the PN -- len >= hdr + 20 was checked above -- and
+    // the sample) are issued together with the key record's, before its check: one memory round trip for both
+    // instead of two in a row (a refused packet's bytes are read but never written)
     const uint4 smp = ld16(base + hdr + 4);
     uint32_t pnw;
     __builtin_memcpy(&pnw, base + hdr, 4);
     uint8_t b0 = base[0];
-    uint32_t m0, m1;
-    if (hk->suite == QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256) {
-        uint32_t k[8];
+    const uint4 hw = *(const uint4 *)hk;  // suite, nr, hp_nr, live
+    uint4 hw1 = make_uint4(0, 0, 0, 0);
+    if (chosen) hw1 = *(const uint4 *)(keys + r.key_idx[1]);
+    // the header key's round keys (AES: up to 15 x 4 words; ChaCha20: the first 8), issued now as well
+    uint32_t hrk[60];
 #pragma unroll
-        for (int j = 0; j < 8; j++) k[j] = hk->hp_rk[j];
-        m0 = chacha_hp_word(k, smp, &m1);
+    for (int q = 0; q < (AES_HP ? 15 : 2); q++) {
+        const uint4 v = ((const uint4 *)hk->hp_rk)[q];
+        hrk[4 * q] = v.x; hrk[4 * q + 1] = v.y; hrk[4 * q + 2] = v.z; hrk[4 * q + 3] = v.w;
+    }
+    if (hw.w == 0 || (!AES_HP && hw.x != QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256)) {
+        d.flags = QPP_PKT_SKIP;
+        status[i] = QPP_INTERNAL_ERROR;
+        return d;
+    }
+    uint32_t m0, m1;
+    if (hw.x == QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256) {
+        m0 = chacha_hp_word(hrk, smp, &m1);
     } else if constexpr (AES_HP) {
-        const uint4 m = hk->hp_nr == 10 ? aes.encrypt<10>(smp, hk->hp_rk) : aes.encrypt<14>(smp, hk->hp_rk);
+        const uint4 m = hw.z == 10 ? aes.encrypt<10>(smp, hrk) : aes.encrypt<14>(smp, hrk);
         m0 = m.x;
         m1 = m.y;
     } else {
@@ -565,7 +575,9 @@ __device__ __forceinline__ qpp_pkt rx_unprotect_one(const AesLds &aes, const Dev
     __builtin_memcpy(base + hdr, &pnw, 4);
     const uint64_t trunc = bswap32(pnw) >> (8u * (4u - pn_len));  // PN bytes big-endian
     d.pn = decode_packet_number(r.largest_pn & kPnMask, trunc, 8 * pn_len);
-    d.key_idx = (!is_long && (b0 & 0x04)) ? r.key_idx[1] : r.key_idx[0];
+    const bool phase1 = !is_long && (b0 & 0x04);
+    d.key_idx = phase1 ? r.key_idx[1] : r.key_idx[0];
+    if (chosen) *chosen = phase1 ? hw1 : hw;
     d.aad_len = (uint16_t)(hdr + pn_len);
     d.pt_len = (uint16_t)(r.len - hdr - pn_len - 16);
     d.pn_len = (uint8_t)pn_len;

@@ -465,6 +465,9 @@ __global__ __launch_bounds__(kQuadWG<NR>) void aes_gcm_quad_kernel(const DevKey 
 // It replaces unprotect_kernel + the three plan launches + the open launch (tests/test_gpu_rx_fused.py: bit-exact
 // against that path and the oracle).  A barrier that does not complete within a second (a workgroup that never became
 // resident) makes every workgroup leave: its packets bound for the open phase report INTERNAL_ERROR, payload untouched.
+#ifndef QPP_RX_TRACE
+#define QPP_RX_TRACE 0  // 1: workgroups 0, grid/2 and the last print their phase times (s_memrealtime)
+#endif
 constexpr uint32_t kRxCtl = kQLdsPow;     // LDS: barrier verdict; [kRxCtl + 64, +6 KiB) phase B scan sums
 constexpr uint32_t kRxHistMax = 16384;    // LDS bins [0, 64 KiB): keys per workgroup in phases A-C
 constexpr uint64_t kRxBarrierTicks = 100000000ull;  // 1 s of s_memrealtime (100 MHz)
@@ -502,12 +505,20 @@ __global__ __launch_bounds__(kQuadWG<NR>) void aes_gcm_quad_rx_kernel(const DevK
                                                                  int8_t *status, uint32_t *scratch, uint32_t *perm) {
     uint32_t *counts = scratch + 16, *cursor = counts + key_cap, *meta = cursor + key_cap;
     WorkItem *work = (WorkItem *)(meta + 4);  // 16-byte aligned: key_cap is even
+#if QPP_RX_TRACE
+    uint64_t ts[8];
+    ts[0] = __builtin_amdgcn_s_memrealtime();
+#define RX_TS(i) ts[i] = __builtin_amdgcn_s_memrealtime()
+#else
+#define RX_TS(i) (void)0
+#endif
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
     const uint32_t bins = min(key_cap, kRxHistMax);  // (the launch requires key_cap <= kRxHistMax)
     build_aes_tables(kLdsAes);
     for (uint32_t i = tid; i < bins; i += nt) lds_st32(4 * i, 0);
     __syncthreads();
     const AesLds aes = make_aes(kLdsAes);
+    RX_TS(1);
     // A: unprotect the slice, count per chosen key
     const uint32_t P = (n + gridDim.x - 1) / gridDim.x;
     const uint32_t lo = min(n, blockIdx.x * P), hi = min(n, lo + P);
@@ -515,11 +526,15 @@ __global__ __launch_bounds__(kQuadWG<NR>) void aes_gcm_quad_rx_kernel(const DevK
     // get INTERNAL_ERROR (descs_out as unprotect_kernel writes it: the multi-launch path's plan refuses them
     // likewise).  The verdict is kept in status (kRxOpen) for phase C, which must scatter exactly the packets phase A
     // counted (a record retired meanwhile must not change it); phase D overwrites kRxOpen.
+    // (the next packet's rx descriptor is loaded while this one is unprotected: one round trip off each packet)
+    qpp_rx_pkt r_next = lo + tid < hi ? rx[lo + tid] : qpp_rx_pkt{};
     for (uint32_t t = lo + tid; t < hi; t += nt) {
-        const qpp_pkt d = rx_unprotect_one(aes, keys, key_cap, rx[t], arena, status, t);
+        const qpp_rx_pkt r = r_next;
+        if (t + nt < hi) r_next = rx[t + nt];
+        uint4 kw;  // the chosen key's suite, nr, hp_nr, live (loaded with the header key's record)
+        const qpp_pkt d = rx_unprotect_one(aes, keys, key_cap, r, arena, status, t, &kw);
         if (!(d.flags & QPP_PKT_SKIP)) {
-            const DevKey *__restrict__ k = keys + d.key_idx;  // (< key_cap: checked by rx_unprotect_one)
-            const bool open = k->live == 1 && k->nr == (uint32_t)NR;
+            const bool open = kw.w == 1 && kw.y == (uint32_t)NR;
             status[t] = open ? kRxOpen : (int8_t)QPP_INTERNAL_ERROR;
             if (open) lds_add32(4 * d.key_idx, 1u);
         }
@@ -535,7 +550,9 @@ __global__ __launch_bounds__(kQuadWG<NR>) void aes_gcm_quad_rx_kernel(const DevK
         const uint32_t c = lds_ld32(4 * k);
         if (c) __hip_atomic_fetch_add(&counts[k], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    RX_TS(2);
     if (!rx_grid_sync(scratch, gridDim.x)) return bail();
+    RX_TS(3);
     // B: workgroup 0 -- each key's first perm index (cursor) and one work item per key with packets
     if (blockIdx.x == 0) {
         const uint32_t chunk = (key_cap + nt - 1) / nt, k0 = min(key_cap, tid * chunk), k1 = min(key_cap, k0 + chunk);
@@ -545,25 +562,33 @@ __global__ __launch_bounds__(kQuadWG<NR>) void aes_gcm_quad_rx_kernel(const DevK
             sum += c;
             nz += c != 0;
         }
-        lds_st32(kRxCtl + 64 + 4 * tid, sum);
-        lds_st32(kRxCtl + 64 + 4 * (nt + tid), nz);
-        __syncthreads();
-        if (tid == 0) {  // exclusive scans of the per-thread sums (<= 1024 entries)
-            uint32_t a = 0, b = 0;
-            for (uint32_t i = 0; i < nt; i++) {
-                const uint32_t x = lds_ld32(kRxCtl + 64 + 4 * i), y = lds_ld32(kRxCtl + 64 + 4 * (nt + i));
-                lds_st32(kRxCtl + 64 + 4 * i, a);
-                lds_st32(kRxCtl + 64 + 4 * (nt + i), b);
-                a += x;
-                b += y;
-            }
-            meta[0] = b;                    // work items
-            meta[1] = NR == 10 ? b : 0u;    // AES-128 items (all of them, or none)
-            meta[2] = NR == 10 ? a : 0u;    // AES-128 packets
-            meta[3] = NR == 10 ? 0u : a;    // AES-256 packets
+        // exclusive scans of the per-thread (sum, nz) in thread order: inclusive scan inside each wave (shuffles),
+        // the waves' totals through LDS (a thread-0 loop over 768 entries took ~40 us)
+        const uint32_t lane = tid & 63u, wv = tid >> 6, nwv = (nt + 63u) >> 6;
+        uint32_t is = sum, iz = nz;
+#pragma unroll
+        for (uint32_t o = 1; o < 64; o <<= 1) {
+            const uint32_t ps = (uint32_t)__shfl_up((int)is, o, 64), pz = (uint32_t)__shfl_up((int)iz, o, 64);
+            if (lane >= o) { is += ps; iz += pz; }
+        }
+        if (lane == 63) {
+            lds_st32(kRxCtl + 64 + 4 * wv, is);
+            lds_st32(kRxCtl + 64 + 4 * (16 + wv), iz);
         }
         __syncthreads();
-        uint32_t off = lds_ld32(kRxCtl + 64 + 4 * tid), item = lds_ld32(kRxCtl + 64 + 4 * (nt + tid));
+        uint32_t off = is - sum, item = iz - nz, ta = 0, tb = 0;
+        for (uint32_t v = 0; v < nwv; v++) {
+            const uint32_t ws = lds_ld32(kRxCtl + 64 + 4 * v), wz = lds_ld32(kRxCtl + 64 + 4 * (16 + v));
+            if (v < wv) { off += ws; item += wz; }
+            ta += ws;
+            tb += wz;
+        }
+        if (tid == 0) {
+            meta[0] = tb;                    // work items
+            meta[1] = NR == 10 ? tb : 0u;    // AES-128 items (all of them, or none)
+            meta[2] = NR == 10 ? ta : 0u;    // AES-128 packets
+            meta[3] = NR == 10 ? 0u : ta;    // AES-256 packets
+        }
         for (uint32_t k = k0; k < k1; k++) {
             const uint32_t c = counts[k];
             cursor[k] = off;
@@ -572,6 +597,7 @@ __global__ __launch_bounds__(kQuadWG<NR>) void aes_gcm_quad_rx_kernel(const DevK
         }
     }
     if (!rx_grid_sync(scratch, 2 * gridDim.x)) return bail();
+    RX_TS(4);
     // C: one block of perm per key this workgroup saw, then its packets into it
     for (uint32_t k = tid; k < bins; k += nt) {
         const uint32_t c = lds_ld32(4 * k);
@@ -580,9 +606,18 @@ __global__ __launch_bounds__(kQuadWG<NR>) void aes_gcm_quad_rx_kernel(const DevK
     __syncthreads();
     for (uint32_t t = lo + tid; t < hi; t += nt)
         if (status[t] == kRxOpen) perm[lds_add32(4 * descs_out[t].key_idx, 1u)] = t;
+    RX_TS(5);
     if (!rx_grid_sync(scratch, 3 * gridDim.x)) return bail();
+    RX_TS(6);
     // D: open, key-sorted slices (tables per key segment, as a planned batch)
     quad_slices<false, NR>(keys, descs_out, perm, work, meta, arena, nullptr, status, 0u, 0xffffffffu, 0u);
+#if QPP_RX_TRACE
+    RX_TS(7);
+    if (threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1 || blockIdx.x == gridDim.x / 2))
+        printf("rx wg %u: tables %.2f A %.2f bar1 %.2f B %.2f C %.2f bar3 %.2f D %.2f us\n", blockIdx.x,
+               (ts[1] - ts[0]) / 100.0, (ts[2] - ts[1]) / 100.0, (ts[3] - ts[2]) / 100.0, (ts[4] - ts[3]) / 100.0,
+               (ts[5] - ts[4]) / 100.0, (ts[6] - ts[5]) / 100.0, (ts[7] - ts[6]) / 100.0);
+#endif
 }
 
 template <bool SEAL, int NR>

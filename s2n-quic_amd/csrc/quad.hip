@@ -312,7 +312,10 @@ __device__ __forceinline__ void quad_packet(const AesLds &aes, const GhashT<true
     };
     for (int g = 0; g + 1 < G; g++) group(std::integral_constant<int, 4>{}, g);
     if (G > 0) {  // the last group with as few counter blocks per lane as its longest packet needs
-        if (tail_slots <= 12) group(std::integral_constant<int, 3>{}, G - 1);
+        // (small packets: a 300-B packet's second group needs 1 block per lane, not 3)
+        if (tail_slots <= 4) group(std::integral_constant<int, 1>{}, G - 1);
+        else if (tail_slots <= 8) group(std::integral_constant<int, 2>{}, G - 1);
+        else if (tail_slots <= 12) group(std::integral_constant<int, 3>{}, G - 1);
         else group(std::integral_constant<int, 4>{}, G - 1);
     }
     if (!len_done && (((m + 1) & 3) == (int)s)) w = gh.mulx(w, lenblk());

@@ -1,7 +1,7 @@
 #!/bin/bash
-# Same-box A/B: alternate benches of library builds (QPP_LIB) and AES variants (QPP_AES_VARIANT), 3 rounds.
+# Same-box A/B: alternate benches of library builds (QPP_LIB), ROUNDS rounds (default 3).
 # usage: CFGS="ab/a.so:0 ab/b.so:0 s2n-quic_amd/libqpp.so:1" [BENCH_ARGS="--suite aes256gcm --keys 64"] bash tools/ab.sh tag
-#   CFGS: space-separated <library path>:<variant index> pairs; BENCH_ARGS: extra bench.py arguments
+#   CFGS: space-separated <library path>:<label> pairs; BENCH_ARGS: extra bench.py arguments
 set -o pipefail
 [ -n "$CFGS" ] || { echo "CFGS is empty: nothing to compare (see the usage line)"; exit 2; }
 cd $GRAFT_REPO_ROOT
@@ -11,7 +11,7 @@ ROUNDS=${ROUNDS:-3}; STEPS=${STEPS:-6}
 for round in $(seq 1 $ROUNDS); do
   for cfg in $CFGS; do
     lib=${cfg%%:*}; var=${cfg##*:}
-    QPP_LIB=$PWD/$lib QPP_AES_VARIANT=$var timeout -k 10 200 python bench.py --steps $STEPS --warmup 2 --no-cpu $BENCH_ARGS > gpurun_out/$tag/r${round}_$(basename $lib .so)_$var.json 2>gpurun_out/$tag/err.txt || { echo "fail $cfg"; tail -5 gpurun_out/$tag/err.txt; exit 1; }
+    QPP_LIB=$PWD/$lib timeout -k 10 200 python bench.py --steps $STEPS --warmup 2 --no-cpu $BENCH_ARGS > gpurun_out/$tag/r${round}_$(basename $lib .so)_$var.json 2>gpurun_out/$tag/err.txt || { echo "fail $cfg"; tail -5 gpurun_out/$tag/err.txt; exit 1; }
     python -c "import json; d=json.load(open('gpurun_out/$tag/r${round}_$(basename $lib .so)_$var.json')); print('$round $cfg', d['value'], d['config']['seal_ms'], d['config']['open_ms'])"
   done
 done

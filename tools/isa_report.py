@@ -1,4 +1,4 @@
-"""Per-kernel ISA report for aes_gcm.hip / chacha.hip: the largest loop's instruction mix (where the time goes).
+"""Per-kernel ISA report for quad.hip / aes_gcm.hip / chacha.hip: the largest loop's instruction mix (where the time goes).
 usage: python tools/isa_report.py [source.hip] [kernel-substring ...]"""
 import collections
 import os
@@ -7,8 +7,8 @@ import subprocess
 import sys
 import tempfile
 
-SRC = sys.argv[1] if len(sys.argv) > 1 else "s2n-quic_amd/csrc/aes_gcm.hip"
-PATS = sys.argv[2:] or ["aes_gcm_kernel"]
+SRC = sys.argv[1] if len(sys.argv) > 1 else "s2n-quic_amd/csrc/quad.hip"
+PATS = sys.argv[2:] or ["aes_gcm_quad_kernel"]
 tmp = tempfile.mkdtemp()
 subprocess.check_call(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-c", os.path.abspath(SRC),
                        "-o", os.path.join(tmp, "x.o"), "-save-temps"], cwd=tmp, stderr=subprocess.DEVNULL)

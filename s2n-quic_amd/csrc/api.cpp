@@ -135,6 +135,12 @@ struct qpp_ctx {
     std::vector<qpp_txq *> servers;  // transmit queues with a persistent server kernel (qpp_txq_create_persistent)
     uint32_t *d_connmap = nullptr;    // qpp_ctx_set_conn_keys: connection -> key slot (device)
     size_t connmap_cap = 0, connmap_n = 0;
+    // its pinned staging copy (the caller's array is pageable: HIP does not promise an async copy from it has read it
+    // when the call returns), reused once connstage_ev shows the previous copy done
+    uint32_t *h_connstage = nullptr;
+    size_t connstage_cap = 0;
+    hipEvent_t connstage_ev = nullptr;
+    bool connstage_used = false;
     std::string last_error;
 };
 
@@ -186,6 +192,11 @@ uint32_t cu_avail(const qpp_ctx *ctx) {
     const uint32_t r = servers_cu(ctx);
     return ctx->n_cu > r ? ctx->n_cu - r : 1u;
 }
+// hipFree / hipHostFree wait for every stream of the device, a running server's too -- and a server only ends on its
+// idle timeout (200 ms by default), or never while flushes come.  So every free of device or pinned memory stops the
+// context's servers first (the next flush of their queue restarts them): growing a plan or a scratch buffer while a
+// persistent queue is live costs a server restart, not the idle time (tests/test_gpu_txq_server.py).
+int quiet_for_free(qpp_ctx *ctx) { return servers_stop(ctx); }
 
 bool valid_suite(int s) {
     return s == QPP_SUITE_TLS_AES_128_GCM_SHA256 || s == QPP_SUITE_TLS_AES_256_GCM_SHA384 ||
@@ -312,6 +323,7 @@ int take_kstage(qpp_ctx *ctx, size_t bytes, KStage **out) {
     if (bytes > k.cap) {
         size_t cap = std::max<size_t>(1 << 16, k.cap);
         while (cap < bytes) cap *= 2;
+        RC_TRY(quiet_for_free(ctx));
         if (k.d) hipFree(k.d);
         if (k.h) { secure_zero(k.h, k.cap); hipHostFree(k.h); }
         k.d = nullptr;
@@ -369,6 +381,7 @@ void mark_dirty(qpp_ctx *ctx, uint32_t slot) {
 int ensure_plan(qpp_ctx *ctx, StreamState *st, uint32_t n) {
     if (n <= st->plan_n_cap && ctx->key_cap <= st->plan_key_cap) return QPP_OK;
     HIP_TRY(ctx, hipStreamSynchronize(st->stream));  // the old scratch is no longer read
+    RC_TRY(quiet_for_free(ctx));
     PlanBuffers &p = st->plan;
     free_plan(p);
     st->plan_n_cap = st->plan_key_cap = 0;
@@ -396,6 +409,7 @@ int ensure_fips(qpp_ctx *ctx, StreamState *st, uint32_t n) {
     }
     if (n <= st->fips_n_cap) return QPP_OK;
     HIP_TRY(ctx, hipStreamSynchronize(st->stream));  // the old scratch is no longer read
+    RC_TRY(quiet_for_free(ctx));
     hipFree(st->fips_buf);
     st->fips_buf = nullptr;
     st->fips_n_cap = 0;
@@ -427,6 +441,7 @@ int ensure_stage(qpp_ctx *ctx, size_t bytes) {
     size_t cap = std::max<size_t>(4096, ctx->stage_cap);
     while (cap < bytes) cap *= 2;
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    RC_TRY(quiet_for_free(ctx));
     if (ctx->d_stage) hipFree(ctx->d_stage);
     if (ctx->h_stage) hipHostFree(ctx->h_stage);
     ctx->d_stage = ctx->h_stage = ctx->v_stage = nullptr;
@@ -777,6 +792,8 @@ int derive_batch_device(qpp_ctx *ctx, int suite, const uint8_t *secrets, const u
     KStage *ks = nullptr;
     RC_TRY(take_kstage(ctx, total, &ks));
     uint8_t *h = ks->h, *d = ks->d;
+    // the pinned stage holds secrets from here on: any exit below leaves them to the next take_kstage to zeroize
+    ks->pending = total;
     memcpy(h, secrets, n * hl);
     if (hp_in) memcpy(h + o_hp, hp_in, n * kl);
     memcpy(h + o_slot, slots.data(), 4 * n);
@@ -788,7 +805,7 @@ int derive_batch_device(qpp_ctx *ctx, int suite, const uint8_t *secrets, const u
     HIP_TRY(ctx, hipMemsetAsync(d, 0, total, s));
     HIP_TRY(ctx, hipEventRecord(ctx->keys_ready, s));
     ctx->key_gen++;
-    RC_TRY(release_kstage(ctx, ks, 0));
+    RC_TRY(release_kstage(ctx, ks, total));  // (zeroized below as well; an error exit in between leaves it pending)
     HIP_TRY(ctx, hipStreamSynchronize(s));  // the material comes back to the host handles
     const uint32_t nr = suite == QPP_SUITE_TLS_AES_128_GCM_SHA256 ? 10 : suite == QPP_SUITE_TLS_AES_256_GCM_SHA384 ? 14 : 0;
     for (size_t i = 0; i < n; i++) {
@@ -846,6 +863,7 @@ int pipe_init(qpp_ctx *ctx) {
 void pipe_release(qpp_ctx *ctx) {
     HostPipe *p = ctx->pipe;
     if (!p) return;
+    quiet_for_free(ctx);
     for (PipeSlot &sl : p->slots) {
         if (sl.arena) {
             hipMemsetAsync(sl.arena, 0, p->chunk_bytes, ctx->stream);
@@ -955,6 +973,8 @@ void qpp_ctx_destroy(qpp_ctx *ctx) {
     }
     hipFree(ctx->d_stage);
     hipFree(ctx->d_connmap);
+    if (ctx->h_connstage) hipHostFree(ctx->h_connstage);
+    if (ctx->connstage_ev) hipEventDestroy(ctx->connstage_ev);
     if (ctx->h_stage) hipHostFree(ctx->h_stage);
     for (KStage &k : ctx->kstage) {
         hipFree(k.d);
@@ -1388,6 +1408,7 @@ int qpp_unprotect_open_batch(qpp_ctx *ctx, const qpp_rx_pkt *rx, size_t n, uint8
         const uint32_t kc = ctx->key_cap;
         if (st->rx_scratch_keys < kc) {
             HIP_TRY(ctx, hipStreamSynchronize(st->stream));  // the old scratch is no longer read
+            RC_TRY(quiet_for_free(ctx));
             hipFree(st->rx_scratch);
             st->rx_scratch = nullptr;
             st->rx_scratch_keys = 0;
@@ -1556,6 +1577,7 @@ int qpp_ctx_set_conn_keys(qpp_ctx *ctx, const uint32_t *slots, size_t n) {
     hipStream_t s = ctx->pipe->comp;  // the remap launches' stream: earlier batches read the old table first
     if (n > ctx->connmap_cap) {
         HIP_TRY(ctx, hipStreamSynchronize(s));
+        RC_TRY(quiet_for_free(ctx));
         hipFree(ctx->d_connmap);
         ctx->d_connmap = nullptr;
         ctx->connmap_cap = ctx->connmap_n = 0;
@@ -1563,8 +1585,24 @@ int qpp_ctx_set_conn_keys(qpp_ctx *ctx, const uint32_t *slots, size_t n) {
         HIP_TRY(ctx, hipMalloc(&ctx->d_connmap, 4 * cap));
         ctx->connmap_cap = cap;
     }
-    // (a pageable source: the runtime has consumed it when the call returns)
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->d_connmap, slots, 4 * n, hipMemcpyHostToDevice, s));
+    // through the pinned stage: the caller may reuse `slots` on return (the previous copy from the stage is waited
+    // for first -- a host wait only when two tables are swapped back to back)
+    if (!ctx->connstage_ev) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->connstage_ev, hipEventDisableTiming));
+    if (ctx->connstage_used) HIP_TRY(ctx, hipEventSynchronize(ctx->connstage_ev));
+    ctx->connstage_used = false;
+    if (n > ctx->connstage_cap) {
+        RC_TRY(quiet_for_free(ctx));
+        if (ctx->h_connstage) hipHostFree(ctx->h_connstage);
+        ctx->h_connstage = nullptr;
+        ctx->connstage_cap = 0;
+        const size_t cap = std::max<size_t>(n, 1024);
+        HIP_TRY(ctx, hipHostMalloc(&ctx->h_connstage, 4 * cap, hipHostMallocDefault));
+        ctx->connstage_cap = cap;
+    }
+    memcpy(ctx->h_connstage, slots, 4 * n);
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->d_connmap, ctx->h_connstage, 4 * n, hipMemcpyHostToDevice, s));
+    HIP_TRY(ctx, hipEventRecord(ctx->connstage_ev, s));
+    ctx->connstage_used = true;
     ctx->connmap_n = n;
     return QPP_OK;
 }
@@ -1602,6 +1640,7 @@ int qpp_dev_alloc(qpp_ctx *ctx, size_t bytes, void **out) {
 void qpp_dev_free(qpp_ctx *ctx, void *ptr) {
     if (!ptr) return;
     hipSetDevice(ctx->device);
+    quiet_for_free(ctx);
     hipFree(ptr);
 }
 int qpp_host_alloc(qpp_ctx *ctx, size_t bytes, void **out) {
@@ -1609,8 +1648,10 @@ int qpp_host_alloc(qpp_ctx *ctx, size_t bytes, void **out) {
     HIP_TRY(ctx, hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault));
     return QPP_OK;
 }
-void qpp_host_free(qpp_ctx *, void *ptr) {
-    if (ptr) hipHostFree(ptr);
+void qpp_host_free(qpp_ctx *ctx, void *ptr) {
+    if (!ptr) return;
+    if (ctx) quiet_for_free(ctx);
+    hipHostFree(ptr);
 }
 int qpp_memcpy_d2d(qpp_ctx *ctx, void *dst, const void *src, size_t bytes, void *stream) {
     HIP_TRY(ctx, hipSetDevice(ctx->device));
@@ -1892,6 +1933,7 @@ int qpp_txq_create_async(qpp_ctx *ctx, size_t ring_bytes, size_t max_packets, si
 void qpp_txq_destroy(qpp_txq *q) {
     if (!q) return;
     hipSetDevice(q->ctx->device);
+    quiet_for_free(q->ctx);  // this queue's server and every other one of the context (the frees below)
     if (q->persistent) {
         srv_stop(q);
         std::vector<qpp_txq *> &v = q->ctx->servers;

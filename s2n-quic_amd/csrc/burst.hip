@@ -409,6 +409,15 @@ __global__ __launch_bounds__(kBurstWG) void txq_server_kernel(const DevKey *keys
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
     TxsSlot *slot = slots + blockIdx.x;
     uint32_t seen = seq0, cached = 0xffffffffu, epoch = 0xffffffffu;
+    {
+        // A server relaunched behind a posted flush (seq0 = posted - 1: the previous one left on its idle timeout
+        // before every workgroup had seen it) must not seal it again in the workgroups that did: the ring is sealed in
+        // place.  This workgroup's `done` equal to its slot's seq means it already has.  (Kernel start: no cache holds
+        // these host-written words yet.)
+        const uint32_t posted = *(const volatile uint32_t *)&slot->seq;
+        const uint32_t done = *(const volatile uint32_t *)&slot->done;
+        if (posted != seq0 && done == posted) seen = posted;
+    }
     uint64_t t_seen = 0;  // thread 0: when this workgroup saw the flush (s_memrealtime)
     for (;;) {
         if (wave == 0) {

@@ -108,6 +108,7 @@ __device__ __forceinline__ uint4 xor3(uint4 a, uint4 b, uint4 c) {
 // T3 = rotl16(T1), so only T0/T1 are stored (64 KiB replicated); per column: 4 lookups + 4 VALU.
 struct AesLds {
     uint32_t laneword;  // byte0 = 4 * (lane % 32), byte2 = table base >> 16
+    __device__ __forceinline__ uint32_t rot(uint32_t x) const { return x; }  // (AesQ4's lane convention: none here)
 
     // address of T0[byte K of w] (T1 is at +128): ONE v_perm_b32
     template <int K>
@@ -358,6 +359,188 @@ __device__ __forceinline__ AesLds make_aes(uint32_t base) {
     return AesLds{((threadIdx.x & 31u) << 2) | base};
 }
 
+// ---------------------------------------------------------------- AES on four T-tables, quarter-split (quad kernel)
+// All four tables T_m = rotl(T0, 8 m) are stored, so a column is T0[a] ^ T1[b] ^ T2[c] ^ T3[d] ^ k in two v_bitop3
+// (AesLds needs four VALU: the rotl16 that makes T2/T3 from T0/T1 and its xor) -- 6 VALU per column instead of 8.
+// They fit in the same 32 KiB of rows a 2-table layout with 32 copies needs by keeping 8 copies of each and
+// splitting every 32-lane LDS group into quarters q = (lane >> 3) & 3 that read DIFFERENT tables in the same
+// instruction: row x (256 B, lower 128 B used) holds dword 8 m + i = copy i of T_m[x], lane l reads copy l % 8,
+// so in lookup slot K (the column's term K: byte K of word c + K through T_K) quarter q reads table (K + q) % 4 and
+// the 32 lanes hit 32 distinct banks.  For that, quarter q holds every state word rotated left by 8 q bits: byte
+// (K + q) % 4 of its register is the natural byte K, and T_{K+q}[x] = rotl(T_K[x], 8 q), so the slot sums are the
+// natural column rotated by 8 q -- the lane's convention again -- provided the round key is rotated too (one
+// v_alignbit per round-key word, shared by the blocks a lane runs together).  The last round picks the S-box bytes
+// by per-lane v_perm selectors straight into natural order, so keystream and round-10 key are natural.
+// LDS: tables at [65536, 131072); the address is ONE v_perm (byte1 = state byte, byte0 = 4 + 32 m + 4 (lane % 8))
+// plus the instruction's offset 65532 (a 16-bit field: 65536 itself does not fit).  The upper 128 B of every row
+// are free.  (tools/q4_model.py checks this convention against FIPS-197 in Python.)
+struct AesQ4 {
+    static constexpr uint32_t kOff = 65532;  // region base 65536 minus the 4 in every byte0
+    uint32_t lw;        // byte m = 4 + 32 m + 4 (lane % 8): copy of T_m this lane reads
+    uint32_t sel[4];    // slot K: byte0 <- lw.b(T_K), byte1 <- w.b(T_K), bytes 2, 3 <- 0; T_K = (K + q) % 4
+    uint32_t selx;      // the counter byte (low byte of its word) through T_(3+q)%4 (CtrPageQ4::two_rounds)
+    uint32_t sh;        // rotl by 8 q = alignbit(x, x, sh)
+    uint32_t flo, fhi;  // last round: natural S-box bytes 0, 1 (from slots 0, 1) and 2, 3 (slots 2, 3)
+
+    __device__ __forceinline__ static AesQ4 make() {
+        AesQ4 a;
+        const uint32_t l = threadIdx.x & 7u, q = (threadIdx.x >> 3) & 3u;
+        a.lw = 0;
+#pragma unroll
+        for (uint32_t m = 0; m < 4; m++) a.lw |= (4u + 32u * m + 4u * l) << (8 * m);
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) {
+            const uint32_t t = (k + q) & 3u;
+            a.sel[k] = 0x0c0c0000u | ((4u + t) << 8) | t;
+        }
+        a.selx = 0x0c0c0400u | ((3u + q) & 3u);
+        a.sh = (32u - 8u * q) & 31u;
+        // slot K's table entry has the S-box value at bytes (1 + K + q) % 4 and (2 + K + q) % 4
+        a.flo = 0x0c0c0000u | ((4u + ((2u + q) & 3u)) << 8) | ((1u + q) & 3u);
+        a.fhi = ((4u + q) << 24) | (((3u + q) & 3u) << 16) | 0x0c0cu;
+        return a;
+    }
+    __device__ __forceinline__ uint32_t rot(uint32_t x) const { return __builtin_amdgcn_alignbit(x, x, sh); }
+    template <int K>
+    __device__ __forceinline__ uint32_t look(uint32_t w) const {
+        return lds_ld32(__builtin_amdgcn_perm(w, lw, sel[K]) + kOff);
+    }
+    __device__ __forceinline__ uint32_t lookx(uint32_t w) const {
+        return lds_ld32(__builtin_amdgcn_perm(w, lw, selx) + kOff);
+    }
+    // column from the 4 slot lookups (kr: the round key word rotated by rot())
+    __device__ __forceinline__ static uint32_t comb(uint32_t l0, uint32_t l1, uint32_t l2, uint32_t l3, uint32_t kr) {
+        return xor3(xor3(l0, l1, l2), l3, kr);
+    }
+    // last round from the 4 slot lookups: natural order, natural key word
+    __device__ __forceinline__ uint32_t fin(uint32_t l0, uint32_t l1, uint32_t l2, uint32_t l3, uint32_t k) const {
+        return xor3(__builtin_amdgcn_perm(l1, l0, flo), __builtin_amdgcn_perm(l3, l2, fhi), k);
+    }
+    __device__ __forceinline__ uint32_t col(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t kr) const {
+        return comb(look<0>(a), look<1>(b), look<2>(c), look<3>(d), kr);
+    }
+    __device__ __forceinline__ uint32_t last(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t k) const {
+        return fin(look<0>(a), look<1>(b), look<2>(c), look<3>(d), k);
+    }
+    // Full AES of one natural block (no caching): page-crossing groups, header protection, key setup
+    template <int NR>
+    __device__ __forceinline__ uint4 encrypt(uint4 in, const uint32_t *__restrict__ rk) const {
+        uint32_t s[4] = {rot(in.x ^ rk[0]), rot(in.y ^ rk[1]), rot(in.z ^ rk[2]), rot(in.w ^ rk[3])};
+#pragma unroll
+        for (int r = 1; r < NR; r++) {
+            uint32_t kr[4];
+#pragma unroll
+            for (int c = 0; c < 4; c++) kr[c] = rot(rk[4 * r + c]);
+            const uint32_t u0 = col(s[0], s[1], s[2], s[3], kr[0]), u1 = col(s[1], s[2], s[3], s[0], kr[1]);
+            const uint32_t u2 = col(s[2], s[3], s[0], s[1], kr[2]), u3 = col(s[3], s[0], s[1], s[2], kr[3]);
+            s[0] = u0; s[1] = u1; s[2] = u2; s[3] = u3;
+        }
+        const uint32_t *k = rk + 4 * NR;
+        return make_uint4(last(s[0], s[1], s[2], s[3], k[0]), last(s[1], s[2], s[3], s[0], k[1]),
+                          last(s[2], s[3], s[0], s[1], k[2]), last(s[3], s[0], s[1], s[2], k[3]));
+    }
+};
+
+// The AesQ4 tables at `base` (65536): thread t owns x = t % 256 (one S-box load) and writes its row's 32 used dwords in
+// an order rotated by x (a wave's stores of one step hit distinct banks).  Needs blockDim.x % 256 == 0.  No barrier.
+__device__ __forceinline__ void build_aes_tables_q4(uint32_t base) {
+    const uint32_t x = threadIdx.x & 255u;
+    const uint32_t s = d_sbox[x], s2 = xtime4(s);
+    const uint32_t t0 = s2 | (s << 8) | (s << 16) | ((s2 ^ s) << 24);
+    for (uint32_t d = threadIdx.x; d < 8192; d += blockDim.x) {
+        const uint32_t slot = ((d >> 8) + x) & 31u, m = slot >> 3;
+        lds_st32(base + 256u * x + 4u * slot, __builtin_amdgcn_alignbit(t0, t0, (32u - 8u * m) & 31u));
+    }
+}
+
+// CtrPage in the AesQ4 convention (every constant rotated by 8 q; the counter byte x3 natural)
+struct CtrPageQ4 {
+    uint32_t k0, k1, k2, k3;  // round-1 output (k0 without the varying slot-3 term)
+    uint32_t l0, l1, l2, l3;  // round-2 output without the varying terms
+    uint32_t x3;              // rk[3] byte 3 (xored with the counter's low byte)
+    uint32_t page;            // c >> 8 these constants belong to
+
+    __device__ __forceinline__ void build(const AesQ4 &a, const uint32_t *__restrict__ rk, uint32_t n0, uint32_t n1,
+                                          uint32_t n2, uint32_t pg) {
+        const uint32_t s0 = a.rot(n0 ^ rk[0]), s1 = a.rot(n1 ^ rk[1]), s2 = a.rot(n2 ^ rk[2]),
+                       s3 = a.rot(bswap32(pg << 8) ^ rk[3]);
+        // round 1; the counter's low byte is natural byte 3 of word 3: slot 3 of column 0
+        k0 = xor3(a.look<0>(s0), a.look<1>(s1), a.look<2>(s2)) ^ a.rot(rk[4]);
+        k1 = a.col(s1, s2, s3, s0, a.rot(rk[5]));
+        k2 = a.col(s2, s3, s0, s1, a.rot(rk[6]));
+        k3 = a.col(s3, s0, s1, s2, a.rot(rk[7]));
+        // round 2 without column 0's terms (slot 0 of col 0, slot 3 of col 1, slot 2 of col 2, slot 1 of col 3)
+        l0 = xor3(a.look<1>(k1), a.look<2>(k2), a.look<3>(k3)) ^ a.rot(rk[8]);
+        l1 = xor3(a.look<0>(k1), a.look<1>(k2), a.look<2>(k3)) ^ a.rot(rk[9]);
+        l2 = xor3(a.look<0>(k2), a.look<1>(k3), a.look<3>(k1)) ^ a.rot(rk[10]);
+        l3 = xor3(a.look<0>(k3), a.look<2>(k1), a.look<3>(k2)) ^ a.rot(rk[11]);
+        x3 = rk[3] >> 24;
+        page = pg;
+    }
+    // state after rounds 1 and 2 for counter c (same page), AesQ4 convention
+    __device__ __forceinline__ void two_rounds(const AesQ4 &a, uint32_t c, uint32_t (&v)[4]) const {
+        const uint32_t u0 = k0 ^ a.lookx(c ^ x3);  // natural T3[x] rotated: T_(3+q)[x]
+        v[0] = l0 ^ a.look<0>(u0);
+        v[1] = l1 ^ a.look<3>(u0);
+        v[2] = l2 ^ a.look<2>(u0);
+        v[3] = l3 ^ a.look<1>(u0);
+    }
+};
+
+// ctr_keystream_inplace on AesQ4 (same unit order and pipeline; the round's 4 key words rotated once per round for
+// all NB blocks)
+template <int NR, int NB, int STRIDE = 1>
+__device__ __forceinline__ void ctr_keystream_q4(const AesQ4 &a, const CtrPageQ4 &pg, const uint32_t *__restrict__ rk,
+                                                 uint32_t c0, uint4 (&ks)[NB]) {
+    static_assert(NB >= 1 && NB <= 4, "pipeline depth NB - 1 lookups groups of 4 within the 15-read counter");
+    constexpr int D = NB - 1;
+    constexpr int U = (NR - 2) * 4 * NB;  // units of rounds 3..NR
+    uint32_t st[NB][4];
+    uint32_t nw[4];
+    uint32_t kr[4];
+    uint32_t ld[D + 1][4];
+#pragma unroll
+    for (int j = 0; j < NB; j++) pg.two_rounds(a, c0 + STRIDE * j, st[j]);
+    auto issue = [&](auto uc) {
+        constexpr int u = decltype(uc)::value;
+        constexpr int j = (u / 4) % NB, c = u % 4;
+        const uint32_t *s = st[j];
+        uint32_t *l = ld[u % (D + 1)];
+        l[0] = a.look<0>(s[c]);
+        l[1] = a.look<1>(s[(c + 1) & 3]);
+        l[2] = a.look<2>(s[(c + 2) & 3]);
+        l[3] = a.look<3>(s[(c + 3) & 3]);
+    };
+    auto combine = [&](auto uc) {
+        constexpr int u = decltype(uc)::value;
+        constexpr int r = 3 + u / (4 * NB), j = (u / 4) % NB, c = u % 4;
+        const uint32_t *l = ld[u % (D + 1)];
+        if constexpr (r < NR) {
+            if constexpr (u % (4 * NB) == 0) {
+#pragma unroll
+                for (int i = 0; i < 4; i++) kr[i] = a.rot(rk[4 * r + i]);
+            }
+            nw[c] = AesQ4::comb(l[0], l[1], l[2], l[3], kr[c]);
+        } else {
+            nw[c] = a.fin(l[0], l[1], l[2], l[3], rk[4 * r + c]);
+        }
+        if constexpr (c == 3) {
+#pragma unroll
+            for (int i = 0; i < 4; i++) st[j][i] = nw[i];
+        }
+    };
+    static_for<D>([&](auto uc) { issue(uc); });
+    static_for<U>([&](auto uc) {
+        constexpr int u = decltype(uc)::value;
+        if constexpr (u + D < U) issue(std::integral_constant<int, u + D>{});
+        __builtin_amdgcn_sched_barrier(0);
+        combine(uc);
+        __builtin_amdgcn_sched_barrier(0);
+    });
+#pragma unroll
+    for (int j = 0; j < NB; j++) ks[j] = make_uint4(st[j][0], st[j][1], st[j][2], st[j][3]);
+}
+
 // ---------------------------------------------------------------- packet view, header protection (both AES kernels)
 struct PacketView {
     uint8_t *base;       // packet start (AAD)
@@ -508,10 +691,11 @@ __device__ __forceinline__ uint32_t chacha_hp_word(const uint32_t hk[8], uint4 s
 // AES_HP = false (the fused ChaCha receive, no T-tables in LDS): a header key that is not a ChaCha20 key is refused
 // (INTERNAL_ERROR) -- the host launches that kernel only when no AES record is live.  A header-key slot that holds no
 // key at all (freed) is refused by both forms, before any header byte is written.
-template <bool AES_HP = true>
 // chosen (optional): the first 16 bytes (suite, nr, hp_nr, live) of the record of the key the packet was sent to,
 // loaded with the rest (the fused receive checks it is a live packet key without another round trip).
-__device__ __forceinline__ qpp_pkt rx_unprotect_one(const AesLds &aes, const DevKey *__restrict__ keys, uint32_t key_cap,
+// AES: the T-table view (AesLds, or AesQ4 in the quad kernels).
+template <bool AES_HP = true, typename AES = AesLds>
+__device__ __forceinline__ qpp_pkt rx_unprotect_one(const AES &aes, const DevKey *__restrict__ keys, uint32_t key_cap,
                                                     const qpp_rx_pkt &r, uint8_t *__restrict__ arena, int8_t *status,
                                                     uint32_t i, uint4 *chosen = nullptr) {
     qpp_pkt d{};
@@ -558,7 +742,7 @@ __device__ __forceinline__ qpp_pkt rx_unprotect_one(const AesLds &aes, const Dev
     if (hw.x == QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256) {
         m0 = chacha_hp_word(hrk, smp, &m1);
     } else if constexpr (AES_HP) {
-        const uint4 m = hw.z == 10 ? aes.encrypt<10>(smp, hrk) : aes.encrypt<14>(smp, hrk);
+        const uint4 m = hw.z == 10 ? aes.template encrypt<10>(smp, hrk) : aes.template encrypt<14>(smp, hrk);
         m0 = m.x;
         m1 = m.y;
     } else {

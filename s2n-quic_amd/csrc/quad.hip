@@ -39,6 +39,30 @@ constexpr uint32_t kQLdsVe = 65536;    // V_e during the build
 #ifndef QPP_QUAD_WG256
 #define QPP_QUAD_WG256 768  // AES-256 (60 round-key words, 14 rounds of pipeline state)
 #endif
+#ifndef QPP_QUAD_Q4
+#define QPP_QUAD_Q4 1  // AES on four quarter-split T-tables (AesQ4); 0: two tables + rotl16 (AesLds)
+#endif
+#if QPP_QUAD_Q4
+using QAes = AesQ4;
+using QPage = CtrPageQ4;
+__device__ __forceinline__ QAes make_qaes() { return AesQ4::make(); }
+__device__ __forceinline__ void build_qaes() { build_aes_tables_q4(kLdsAes); }
+template <int NR, int NB, int STRIDE>
+__device__ __forceinline__ void qkeystream(const QAes &a, const QPage &pg, const uint32_t *rk, uint32_t c0,
+                                           uint4 (&ks)[NB]) {
+    ctr_keystream_q4<NR, NB, STRIDE>(a, pg, rk, c0, ks);
+}
+#else
+using QAes = AesLds;
+using QPage = CtrPage;
+__device__ __forceinline__ QAes make_qaes() { return make_aes(kLdsAes); }
+__device__ __forceinline__ void build_qaes() { build_aes_tables(kLdsAes); }
+template <int NR, int NB, int STRIDE>
+__device__ __forceinline__ void qkeystream(const QAes &a, const QPage &pg, const uint32_t *rk, uint32_t c0,
+                                           uint4 (&ks)[NB]) {
+    ctr_keystream_inplace<NR, NB, STRIDE>(a, pg, rk, c0, ks);
+}
+#endif
 __device__ __forceinline__ uint4 ld_payload(const uint8_t *p) { return ld16(p); }
 __device__ __forceinline__ void st_payload(uint8_t *p, uint4 v) {
     st16_nt(p, v);  // streaming: the sealed / opened bytes are not read again
@@ -94,7 +118,7 @@ __device__ void quad_tables(const DevKey *__restrict__ key) {
     __syncthreads();  // the tables of H are dead
     build8(kQLdsVe + 3 * 2048);  // tables of H^4 (the Horner step)
     __syncthreads();  // V_e are dead
-    build_aes_tables(kLdsAes);
+    build_qaes();
     __syncthreads();
 }
 
@@ -119,16 +143,16 @@ constexpr int kQuadBcast2 = 0xaa;  // [2, 2, 2, 2]
 constexpr int kQuadRot1 = 0x39;  // [1, 2, 3, 0]
 constexpr int kQuadRot3 = 0x93;  // [3, 0, 1, 2]
 template <int NR>
-__device__ __forceinline__ uint32_t aes_quad(const AesLds &a, const uint32_t *__restrict__ rk_g, uint32_t col, uint32_t s) {
+__device__ __forceinline__ uint32_t aes_quad(const QAes &a, const uint32_t *__restrict__ rk_g, uint32_t col, uint32_t s) {
     uint32_t rk[NR + 1];
 #pragma unroll
     for (int r = 0; r <= NR; r++) rk[r] = rk_g[4 * r + s];
-    uint32_t x = col ^ rk[0];
+    uint32_t x = a.rot(col ^ rk[0]);  // (the lane's convention: AesQ4 rotates every word by 8 q)
 #pragma unroll
     for (int r = 1; r <= NR; r++) {
         const uint32_t b = qperm<kQuadRot1>(x), c = qperm<kQuadSwap2>(x), d = qperm<kQuadRot3>(x);
         if (r < NR) {
-            x = a.col(x, b, c, d, rk[r]);
+            x = a.col(x, b, c, d, a.rot(rk[r]));
         } else {
             x = a.last(x, b, c, d, rk[r]);
         }
@@ -138,18 +162,19 @@ __device__ __forceinline__ uint32_t aes_quad(const AesLds &a, const uint32_t *__
 
 // The descriptor again at the packet's tail (through a laundered pointer, so that the compiler reloads it instead of
 // keeping its fields in VGPRs across the group loop: the loop needs only the payload offset, length and nonce)
-__device__ __forceinline__ qpp_pkt reload_desc(const qpp_pkt *p) {
-    uint64_t a = (uint64_t)p;
-    asm volatile("" : "+v"(a));
-    return *(const qpp_pkt *)a;
+// (the base is uniform and the index a lane's own packet: no 64-bit pointer is kept live across the loop)
+__device__ __forceinline__ qpp_pkt reload_desc(const qpp_pkt *descs, uint32_t i) {
+    uint32_t v = i;
+    asm volatile("" : "+v"(v));
+    return descs[v];
 }
 
 // One packet per quad; s = lane % 4.  has = false: the quad has no packet (its lanes only keep the wave's loop shape).
 // Addresses are 32-bit offsets into the arena (SGPR base + VGPR offset).
 template <int NR, bool SEAL>
-__device__ __forceinline__ void quad_packet(const AesLds &aes, const GhashT<true> &gh, const DevKey *__restrict__ key,
+__device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> &gh, const DevKey *__restrict__ key,
                                             bool has, const qpp_pkt &d,
-                                            const qpp_pkt *__restrict__ dptr, uint32_t pkt_index,
+                                            const qpp_pkt *__restrict__ descs, uint32_t pkt_index,
                                             uint8_t *__restrict__ arena, uint8_t *masks, int8_t *status,
                                             uint32_t flags, uint32_t s) {
     // loop state
@@ -183,7 +208,7 @@ __device__ __forceinline__ void quad_packet(const AesLds &aes, const GhashT<true
             k[4 * r] = v.x; k[4 * r + 1] = v.y; k[4 * r + 2] = v.z; k[4 * r + 3] = v.w;
         }
     };
-    CtrPage pg;
+    QPage pg;
     {
         uint32_t rk[4 * (NR + 1)];
         round_keys(rk);
@@ -210,7 +235,7 @@ __device__ __forceinline__ void quad_packet(const AesLds &aes, const GhashT<true
     // has at least 20 - pn_len bytes.  The header bytes are then written while the packet's first 64-byte segment still
     // holds group 0's ciphertext in L2 (one memory write for both, not two), and nothing is read back.
     auto hp_early = [&](const uint4 &ct) {
-        const qpp_pkt dt = reload_desc(dptr);
+        const qpp_pkt dt = reload_desc(descs, pkt_index);
         const uint32_t pn_len = dt.pn_len;
         if (!(want_hp && has && pn_len >= 1 && pn_len <= 4 && len + pn_len >= 20)) return;  // quad-uniform
         const uint4 b0 = qperm<kQuadBcast1>(ct), b1 = qperm<kQuadBcast2>(ct);  // ciphertext blocks 0 and 1
@@ -249,7 +274,7 @@ __device__ __forceinline__ void quad_packet(const AesLds &aes, const GhashT<true
                 asm volatile("" : "+v"(m0), "+v"(m1), "+v"(m2));
                 pg.build(aes, rk, m0, m1, m2, c0 >> 8);
             }
-            ctr_keystream_inplace<NR, NBG, 4>(aes, pg, rk, c0, ks);
+            qkeystream<NR, NBG, 4>(aes, pg, rk, c0, ks);
         } else {
             asm volatile("" : "+v"(m0), "+v"(m1), "+v"(m2));
             static_for<NBG>([&](auto kc) {
@@ -295,14 +320,18 @@ __device__ __forceinline__ void quad_packet(const AesLds &aes, const GhashT<true
 #pragma unroll
             for (int k = 0; k < NBG; k++) w = gh.mulx(w, SEAL ? out[k] : in[k]);
         } else {
+            // (rem laundered here: left alone, the compiler hoisted keep_bytes' four masks out of the group loop and
+            // held them -- and spilled others -- for the whole packet)
+            uint32_t rl = (uint32_t)rem;
+            asm volatile("" : "+v"(rl));
 #pragma unroll
             for (int k = 0; k < NBG; k++) {
                 const int t = t0 + 4 * k, j = t - 1;
                 const bool full = t >= 1 && j < nfull, part = rem && j == nfull, lenslot = has && t == m + 1;
                 if (full) st_payload(at(pay + 16 * (uint32_t)j), out[k]);
-                if (part) st_bytes(at(pay + 16 * (uint32_t)j), keep_bytes(out[k], (uint32_t)rem), (uint32_t)rem);
+                if (part) st_bytes(at(pay + 16 * (uint32_t)j), keep_bytes(out[k], rl), rl);
                 // the length block rides in the slot after the payload when the group reaches it
-                const uint4 x = lenslot ? lenblk() : part ? keep_bytes(SEAL ? out[k] : in[k], (uint32_t)rem)
+                const uint4 x = lenslot ? lenblk() : part ? keep_bytes(SEAL ? out[k] : in[k], rl)
                                                         : (SEAL ? out[k] : in[k]);
                 if (full || part || lenslot) w = gh.mulx(w, x);
                 len_done = len_done || lenslot;
@@ -337,7 +366,7 @@ __device__ __forceinline__ void quad_packet(const AesLds &aes, const GhashT<true
 
     if constexpr (SEAL) {
         if (has && s == 0) st16(at(pay + len), y ^ ek0);  // tag = GHASH ^ E_K(J0)
-        const qpp_pkt dt = reload_desc(dptr);
+        const qpp_pkt dt = reload_desc(descs, pkt_index);
         const uint32_t pn_len = dt.pn_len;
         const bool hp = want_hp && has && pn_len >= 1 && pn_len <= 4 && len >= 4 - pn_len;  // quad-uniform
         if (hp && !hp_done) {  // short payloads: the sample runs into the tag
@@ -364,7 +393,7 @@ __device__ __forceinline__ void quad_packet(const AesLds &aes, const GhashT<true
     } else {
         // E_K(J0) on the quad (column s in lane s; J0 = nonce || be32(1)), compared column by column with the received
         // tag, the verdict OR-ed over the quad: all 16 bytes compared, no early exit
-        const qpp_pkt dt = reload_desc(dptr);
+        const qpp_pkt dt = reload_desc(descs, pkt_index);
         const uint32_t j0 = s == 0 ? key->iv[0]
                           : s == 1 ? key->iv[1] ^ bswap32((uint32_t)(dt.pn >> 32))
                           : s == 2 ? key->iv[2] ^ bswap32((uint32_t)dt.pn)
@@ -414,7 +443,7 @@ __device__ __forceinline__ void quad_slices(const DevKey *__restrict__ keys, con
         const uint32_t mid = (i + j) >> 1;
         if (work[mid].begin <= lo) i = mid; else j = mid;
     }
-    const AesLds aes = make_aes(kLdsAes);
+    const QAes aes = make_qaes();
     const GhashT<true> gh = GhashT<true>::make();
     const uint32_t s = threadIdx.x & 3u, q = threadIdx.x >> 2;
     for (; lo < hi; i++) {  // key segments of the slice
@@ -437,7 +466,7 @@ __device__ __forceinline__ void quad_slices(const DevKey *__restrict__ keys, con
                 if (status && s == 0) status[pi] = QPP_INTERNAL_ERROR;
                 has = false;
             }
-            quad_packet<NR, SEAL>(aes, gh, key, has, d, descs + pi, pi, arena, masks, status, flags, s);
+            quad_packet<NR, SEAL>(aes, gh, key, has, d, descs, pi, arena, masks, status, flags, s);
         }
         lo = end;
     }
@@ -517,10 +546,10 @@ __global__ __launch_bounds__(kQuadWG<NR>) void aes_gcm_quad_rx_kernel(const DevK
 #endif
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
     const uint32_t bins = min(key_cap, kRxHistMax);  // (the launch requires key_cap <= kRxHistMax)
-    build_aes_tables(kLdsAes);
+    build_qaes();
     for (uint32_t i = tid; i < bins; i += nt) lds_st32(4 * i, 0);
     __syncthreads();
-    const AesLds aes = make_aes(kLdsAes);
+    const QAes aes = make_qaes();
     RX_TS(1);
     // A: unprotect the slice, count per chosen key
     const uint32_t P = (n + gridDim.x - 1) / gridDim.x;

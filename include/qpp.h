@@ -64,15 +64,17 @@ void qpp_ctx_destroy(qpp_ctx *ctx);
 void *qpp_ctx_stream(qpp_ctx *ctx);
 int qpp_ctx_synchronize(qpp_ctx *ctx);
 /* AES-GCM batches of at most max_packets packets (default 16384, env QPP_BURST_MAX) run one wave per packet
- * (latency: a 64-packet GSO burst); larger ones one lane per packet (throughput).  ChaCha20-Poly1305 batches switch
- * at max_packets / 4.  0 = always lane per packet.  Outputs are identical either way. */
+ * (latency: a 64-packet GSO burst); larger ones by the throughput kernels (quad / wave-item; qpp_ctx_set_aes_kernel).  ChaCha20-Poly1305 batches switch
+ * at max_packets / 4.  0 = never one wave per packet.  Outputs are identical either way. */
 int qpp_ctx_set_burst_max(qpp_ctx *ctx, size_t max_packets);
-/* AES-GCM batches larger than burst_max: the lane kernel (one key per 1024-packet workgroup) serves batches with at
- * least 1024 packets per live AES key, the wave-item kernel (one key per 64-packet wave) batches with fewer (many
- * keys, few packets each: key-update churn).  This forces one of them (env QPP_AES_KERNEL=lane|wave); outputs are
- * identical. */
+/* AES-GCM batches larger than burst_max: the quad kernel (four lanes per packet, one workgroup per CU over a slice of
+ * the key-sorted packets) serves batches with at least 1024 packets per live AES key, the wave-item kernel (one key
+ * per 64-packet wave) batches with fewer (many keys, few packets each: key-update churn).  This forces one of them
+ * (env QPP_AES_KERNEL=quad|wave); outputs are identical.  QPP_AES_KERNEL_LANE is the round-1..3 name of the quad
+ * selector (the lane-per-packet kernel it named was replaced by the quad kernel) and is kept for source compatibility. */
 #define QPP_AES_KERNEL_AUTO 0
-#define QPP_AES_KERNEL_LANE 1
+#define QPP_AES_KERNEL_QUAD 1
+#define QPP_AES_KERNEL_LANE QPP_AES_KERNEL_QUAD
 #define QPP_AES_KERNEL_WAVE 2
 int qpp_ctx_set_aes_kernel(qpp_ctx *ctx, int kernel);
 /* FIPS mode: the s2n-quic-crypto `fips` cargo feature (cipher_suite/ring.rs:13-31, aead/fips.rs:13-60).  AES packet
@@ -407,6 +409,11 @@ int qpp_event_elapsed_ms(qpp_ctx *ctx, void *start, void *stop, float *ms);
 int qpp_stream_wait_event(qpp_ctx *ctx, void *stream, void *event);
 /* Last HIP error string of this context (for diagnostics). */
 const char *qpp_ctx_last_error(qpp_ctx *ctx);
+/* Workgroups of the fused receive launch (qpp_unprotect_open_batch) that left on a grid-barrier timeout since the
+ * context was created: a cooperative launch whose workgroups could not all be resident within a second (a foreign
+ * kernel holding CUs).  Their packets bound for the open phase reported QPP_INTERNAL_ERROR with the payload untouched
+ * and the header already unprotected.  0 in normal operation.  Waits for the context's batch streams. */
+int qpp_ctx_rx_timeouts(qpp_ctx *ctx, uint64_t *count);
 
 #ifdef __cplusplus
 }

@@ -6,15 +6,17 @@
 //   HP    HeaderKey::header_protection_mask -> new_mask             src/header_key.rs:52-56
 // with the nonce of Iv::nonce (src/iv.rs:27-39).
 //
-// Mapping: one LANE per packet.  A packet's CTR keystream, its ciphertext and its
-// GHASH chain stay in one lane's registers from the first block to the tag, so there is no
-// cross-lane traffic at all.  A workgroup = 1024 packets that share one key (the plan kernels
-// group a mixed-key batch), because both lookup tables live in LDS:
-//   [0, 64 KiB)     GHASH tables T_j[x] = (x at byte j) * H, 16 positions x 256 entries x 16 B
+// This file holds the MANY-KEY throughput kernel (aes_gcm_wave_kernel), the key setup kernels and the AES launchers;
+// the one-key-per-slice throughput kernel is quad.hip's (four lanes per packet), the small-batch kernel burst.hip's.
+//
+// aes_gcm_wave_kernel (DESIGN.md §3 "Many keys"): one LANE per packet, one key per 64-packet WAVE.  A packet's CTR
+// keystream, its ciphertext and its GHASH chain stay in one lane's registers from the first block to the tag; the
+// wave's payload moves through a per-wave LDS staging area (Stage, coalesced 64-B chunks).  LDS:
+//   [0, 64 KiB)     per-wave 4-bit GHASH tables of the wave's key (Ghash4, 8 KiB per wave)
 //   [64, 128 KiB)   AES T0/T1 replicated once per LDS bank: row x = 256 B = T0[x] x 32 banks | T1[x] x 32 banks,
 //                   so a lane's lookup always hits bank (lane % 32): conflict-free, and its address
 //                   (x << 8 | lane*4 | 64 KiB) is ONE v_perm_b32 from the state word.
-//   [128, 130 KiB)  V[m] = H * x^m staging for the GHASH table build.
+//   [128, 160 KiB)  payload staging (Stage<NB>).
 // AES rounds: T0[a] ^ T1[b] ^ rotl16(T0[c] ^ T1[d]) ^ rk (T2 = rotl16 T0, T3 = rotl16 T1).
 #include <stdlib.h>
 #include <string.h>

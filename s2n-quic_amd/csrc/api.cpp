@@ -141,6 +141,7 @@ struct qpp_ctx {
     size_t connstage_cap = 0;
     hipEvent_t connstage_ev = nullptr;
     bool connstage_used = false;
+    uint32_t *d_diag = nullptr;  // device counters: [0] fused-receive workgroups that left on a barrier timeout
     std::string last_error;
 };
 
@@ -577,22 +578,23 @@ uint32_t suite_mask(const qpp_ctx *ctx) {
     return m;
 }
 
-// Which AES-GCM kernel serves an n-packet batch: the wave-per-packet burst kernel for small batches; the lane kernel
-// (one key per 1024-packet workgroup, 8-bit GHASH tables) when the batch has >= kWaveKernelPacketsPerKey packets per
-// live AES key; else the wave-item kernel (one key per 64-packet wave, 4-bit tables).  QPP_AES_KERNEL=lane|wave
-// forces one of the two throughput kernels (A/B).
-enum class AesPath { burst, lane, wave };
+// Which AES-GCM kernel serves an n-packet batch: the wave-per-packet burst kernel for small batches; the quad kernel
+// (quad.hip: four lanes per packet, one workgroup per CU over a slice of the key-sorted packets, 8-bit GHASH tables
+// rebuilt per key segment) when the batch has >= kWaveKernelPacketsPerKey packets per live AES key; else the wave-item
+// kernel (aes_gcm.hip: one key per 64-packet wave, 4-bit tables).  QPP_AES_KERNEL=quad|wave forces one of the two
+// throughput kernels (A/B).
+enum class AesPath { burst, quad, wave };
 AesPath aes_path(const qpp_ctx *ctx, uint32_t n) {
     if (n <= ctx->burst_max) return AesPath::burst;
-    if (ctx->aes_kernel) return ctx->aes_kernel == QPP_AES_KERNEL_LANE ? AesPath::lane : AesPath::wave;
+    if (ctx->aes_kernel) return ctx->aes_kernel == QPP_AES_KERNEL_QUAD ? AesPath::quad : AesPath::wave;
     const uint64_t aes_keys = (uint64_t)ctx->live_by_suite[QPP_SUITE_TLS_AES_128_GCM_SHA256] +
                               ctx->live_by_suite[QPP_SUITE_TLS_AES_256_GCM_SHA384];
-    return (uint64_t)n < kWaveKernelPacketsPerKey * aes_keys ? AesPath::wave : AesPath::lane;
+    return (uint64_t)n < kWaveKernelPacketsPerKey * aes_keys ? AesPath::wave : AesPath::quad;
 }
 uint32_t aes_per_item(const qpp_ctx *ctx, AesPath p, uint32_t n) {
     return p == AesPath::burst ? burst_packets_per_item(n, ctx->n_cu)
            : p == AesPath::wave ? kWavePacketsPerItem
-                                : kLanePerItem;
+                                : kQuadPerItem;
 }
 hipError_t launch_aes(const qpp_ctx *ctx, AesPath p, bool seal, const qpp_pkt *descs, const PlanBuffers &pb, uint32_t n,
                       uint8_t *arena, uint8_t *masks, int8_t *status, uint32_t flags, hipStream_t s) {
@@ -627,7 +629,7 @@ int enqueue_seal(qpp_ctx *ctx, StreamState *st, const qpp_pkt *descs, uint32_t n
     if (!(flags & QPP_ONLY_CHACHA)) RC_TRY(fips_gate(ctx, st, descs, n, status, refused));
     if (!(flags & QPP_ONLY_CHACHA) && (suite_mask(ctx) & kAesSuites)) {
         const AesPath path = aes_path(ctx, n);
-        const uint32_t one = path == AesPath::lane ? single_aes_slot(ctx) : UINT32_MAX;
+        const uint32_t one = path == AesPath::quad ? single_aes_slot(ctx) : UINT32_MAX;
         if (one != UINT32_MAX) {
             HIP_TRY(ctx, launch_aes_gcm_single(true, ctx->d_keys, descs, one, ctx->h_keys[one].nr, n, cu_avail(ctx), arena,
                                                masks, status, flags, s));
@@ -648,7 +650,7 @@ int enqueue_open(qpp_ctx *ctx, StreamState *st, const qpp_pkt *descs, uint32_t n
     hipStream_t s = st->stream;
     if (!(flags & QPP_ONLY_CHACHA) && (suite_mask(ctx) & kAesSuites)) {
         const AesPath path = aes_path(ctx, n);
-        const uint32_t one = path == AesPath::lane ? single_aes_slot(ctx) : UINT32_MAX;
+        const uint32_t one = path == AesPath::quad ? single_aes_slot(ctx) : UINT32_MAX;
         if (one != UINT32_MAX) {
             HIP_TRY(ctx, launch_aes_gcm_single(false, ctx->d_keys, descs, one, ctx->h_keys[one].nr, n, cu_avail(ctx), arena,
                                                nullptr, status, 0, s));
@@ -898,7 +900,9 @@ int qpp_ctx_create(int device, qpp_ctx **out) {
     ctx->n_cu = (uint32_t)prop.multiProcessorCount;
     if (const char *e = getenv("QPP_BURST_MAX")) ctx->burst_max = (uint32_t)strtoul(e, nullptr, 10);
     if (const char *e = getenv("QPP_AES_KERNEL"))
-        ctx->aes_kernel = !strcmp(e, "lane") ? QPP_AES_KERNEL_LANE : !strcmp(e, "wave") ? QPP_AES_KERNEL_WAVE : 0;
+        ctx->aes_kernel = !strcmp(e, "quad") || !strcmp(e, "lane") ? QPP_AES_KERNEL_QUAD
+                        : !strcmp(e, "wave")                     ? QPP_AES_KERNEL_WAVE
+                                                                 : 0;
     int rc = QPP_OK;
     do {
         if (fail(ctx, hipSetDevice(device), "hipSetDevice")) { rc = QPP_DEVICE_ERROR; break; }
@@ -910,6 +914,10 @@ int qpp_ctx_create(int device, qpp_ctx **out) {
             break;
         }
         if (!stream_state(ctx, ctx->stream)) { rc = QPP_DEVICE_ERROR; break; }
+        if (fail(ctx, hipMalloc(&ctx->d_diag, 64), "diag") || fail(ctx, hipMemset(ctx->d_diag, 0, 64), "diag")) {
+            rc = QPP_DEVICE_ERROR;
+            break;
+        }
         rc = grow_keys(ctx, 64);
     } while (0);
     if (rc) {
@@ -973,6 +981,7 @@ void qpp_ctx_destroy(qpp_ctx *ctx) {
     }
     hipFree(ctx->d_stage);
     hipFree(ctx->d_connmap);
+    hipFree(ctx->d_diag);
     if (ctx->h_connstage) hipHostFree(ctx->h_connstage);
     if (ctx->connstage_ev) hipEventDestroy(ctx->connstage_ev);
     if (ctx->h_stage) hipHostFree(ctx->h_stage);
@@ -1000,6 +1009,16 @@ int qpp_ctx_synchronize(qpp_ctx *ctx) {
 }
 
 const char *qpp_ctx_last_error(qpp_ctx *ctx) { return ctx ? ctx->last_error.c_str() : "no context"; }
+
+int qpp_ctx_rx_timeouts(qpp_ctx *ctx, uint64_t *count) {
+    if (!ctx || !count) return QPP_INTERNAL_ERROR;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    for (StreamState *st : ctx->streams) HIP_TRY(ctx, hipStreamSynchronize(st->stream));
+    uint32_t v = 0;
+    HIP_TRY(ctx, hipMemcpy(&v, ctx->d_diag, 4, hipMemcpyDeviceToHost));
+    *count = v;
+    return QPP_OK;
+}
 
 int qpp_ctx_key_slots(qpp_ctx *ctx, uint32_t *capacity, uint32_t *high_water, uint32_t *retired) {
     if (!ctx) return QPP_INTERNAL_ERROR;
@@ -1403,7 +1422,7 @@ int qpp_unprotect_open_batch(qpp_ctx *ctx, const qpp_rx_pkt *rx, size_t n, uint8
     const uint32_t a128 = ctx->live_by_suite[QPP_SUITE_TLS_AES_128_GCM_SHA256],
                    a256 = ctx->live_by_suite[QPP_SUITE_TLS_AES_256_GCM_SHA384];
     if (!(flags & QPP_ONLY_CHACHA) && !(fz && fz[0] == '0') && !ctx->live_by_suite[QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256] &&
-        (a128 > 0) != (a256 > 0) && aes_path(ctx, (uint32_t)n) == AesPath::lane && ctx->key_cap <= quad_rx_max_keys()) {
+        (a128 > 0) != (a256 > 0) && aes_path(ctx, (uint32_t)n) == AesPath::quad && ctx->key_cap <= quad_rx_max_keys()) {
         RC_TRY(ensure_plan(ctx, st, (uint32_t)n));  // perm
         const uint32_t kc = ctx->key_cap;
         if (st->rx_scratch_keys < kc) {
@@ -1418,7 +1437,7 @@ int qpp_unprotect_open_batch(qpp_ctx *ctx, const qpp_rx_pkt *rx, size_t n, uint8
         HIP_TRY(ctx, hipMemsetAsync(st->rx_scratch, 0, 4 * (16 + 2 * (size_t)kc), st->stream));
         const uint32_t grid = std::min<uint32_t>(cu_avail(ctx), std::max<uint32_t>(1, (uint32_t)((n + 191) / 192)));
         HIP_TRY(ctx, launch_aes_gcm_quad_rx(a128 ? 10 : 14, grid, st->stream, ctx->d_keys, kc, rx, (uint32_t)n, arena,
-                                            descs_out, status, st->rx_scratch, st->plan.perm));
+                                            descs_out, status, st->rx_scratch, st->plan.perm, ctx->d_diag));
         return note_work(ctx, st);
     }
     // No AES record live at all (packet or header keys): every header and packet key a packet can name is ChaCha20,

@@ -26,7 +26,7 @@ for path in sys.argv[1:]:
                    or re.search(r"aes_gcm_quad_rx_kernelILi10E", name))
         if lds and dyn_lds and int(lds.group(1)) != 0:
             bad.append(f"{name}: {lds.group(1)} B of static LDS on top of the dynamic 160 KiB")
-        # (a few per-packet spills outside the group loop are tolerated: tools/isa_spills.py lists where they are)
+        # (a few per-packet spills outside the group loop are tolerated: tools/isa_report.py shows where they are)
         if scr and default and int(scr.group(1)) > 32:
             bad.append(f"{name}: {scr.group(1)} B/lane of scratch")
 if bad:

@@ -1,5 +1,5 @@
-// ghash.h — GHASH on LDS tables (gfx950): the 8-bit byte tables of the lane kernel (one key per workgroup) and the
-// per-wave 4-bit tables of the many-key kernels.  Shared by aes_gcm.hip and tools/ubench/aes_core.hip.
+// ghash.h — GHASH on LDS tables (gfx950): the 8-bit byte tables of the quad kernel (one key per workgroup segment) and
+// the per-wave 4-bit tables of the many-key kernels.  Shared by aes_gcm.hip and tools/ubench/aes_core.hip.
 #pragma once
 
 #include "device_common.h"

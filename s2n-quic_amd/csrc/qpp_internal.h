@@ -95,7 +95,7 @@ struct WorkItem {
 constexpr int kMinPacketsPerItem = 4;
 constexpr uint32_t kWavePacketsPerItem = 64;  // aes_gcm_wave_kernel: one wave, one key, <= 64 packets per work item
 constexpr uint32_t kWaveKernelPacketsPerKey = 1024;  // batches with fewer packets per live AES key take the wave kernel
-constexpr uint32_t kLanePerItem = 0x7fffffffu;  // aes_gcm_quad_kernel: one work item per key (workgroups take equal slices)
+constexpr uint32_t kQuadPerItem = 0x7fffffffu;  // aes_gcm_quad_kernel: one work item per key (workgroups take equal slices)
 constexpr uint32_t kBurstMaxDefault = 16384;  // AES batches up to this many packets run one wave per packet
 constexpr uint32_t kChachaBurstShift = 2;     // ChaCha20-Poly1305 batches up to burst_max >> 2 do (its lane kernel
                                               // fills the chip with fewer packets: crossover ~6 Ki vs ~20 Ki)
@@ -186,23 +186,24 @@ hipError_t launch_txq_server(const DevKey *keys, const PowTables &pow, TxsMail *
 hipError_t launch_pow_setup(const DevKey *keys, const uint32_t *slots, uint32_t count, const PowTables &pow,
                             hipStream_t s);
 // suites: bit (1 << suite) for every suite with a live key in the context (launches only what can occur)
-// plan with per = kLanePerItem; one workgroup per CU, each an equal slice of the key-sorted packets
+// plan with per = kQuadPerItem; one workgroup per CU, each an equal slice of the key-sorted packets
 hipError_t launch_aes_gcm(bool seal, const DevKey *keys, const qpp_pkt *descs, const PlanBuffers &pb, uint32_t n,
                           uint32_t n_cu, uint8_t *arena, uint8_t *masks, int8_t *status, uint32_t flags,
                           uint32_t suites, hipStream_t s);
-// one live AES key (slot, nr): the lane kernel over descs[0, n) without a plan; packets of any other slot are refused
+// one live AES key (slot, nr): the quad kernel over descs[0, n) without a plan; packets of any other slot are refused
 // (status INTERNAL_ERROR)
 hipError_t launch_aes_gcm_single(bool seal, const DevKey *keys, const qpp_pkt *descs, uint32_t slot, uint32_t nr,
                                  uint32_t n, uint32_t n_cu, uint8_t *arena, uint8_t *masks, int8_t *status,
                                  uint32_t flags, hipStream_t s);
-// quad.hip: the quad-layout (4 lanes per packet, 1024-thread workgroups) throughput kernel behind the two above
+// quad.hip: the quad-layout (4 lanes per packet, 768-thread workgroups) throughput kernel behind the two above
 // quad.hip: fused unprotect -> PN expand -> key-phase choice -> open for any mix of live packet keys of ONE AES size
 // (nr), one cooperative launch of `grid` workgroups (<= the CUs it may use; key_cap <= quad_rx_max_keys(), even).
 // scratch: 16 + 2 key_cap + 4 + 4 (key_cap + 1) words, the first 16 + 2 key_cap zeroed before the launch; perm: n words.
+// timeouts: a device word every workgroup that left on a barrier timeout increments (qpp_ctx_rx_timeouts).
 uint32_t quad_rx_max_keys();
 hipError_t launch_aes_gcm_quad_rx(uint32_t nr, uint32_t grid, hipStream_t s, const DevKey *keys, uint32_t key_cap,
                                   const qpp_rx_pkt *rx, uint32_t n, uint8_t *arena, qpp_pkt *descs_out, int8_t *status,
-                                  uint32_t *scratch, uint32_t *perm);
+                                  uint32_t *scratch, uint32_t *perm, uint32_t *timeouts);
 hipError_t launch_aes_gcm_quad(bool seal, uint32_t nr, dim3 grid, hipStream_t s, const DevKey *keys,
                                const qpp_pkt *descs, const PlanBuffers &pb, uint8_t *arena, uint8_t *masks,
                                int8_t *status, uint32_t flags, uint32_t single, uint32_t n_single);

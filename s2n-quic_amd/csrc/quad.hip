@@ -1,17 +1,17 @@
 // quad.hip — AES-128/256-GCM seal/open + AES header protection, "quad" layout: FOUR lanes per packet (gfx950).
 //
-// Replaces the aws-lc-rs calls behind quic/s2n-quic-crypto (as aes_gcm.hip's lane kernel does):
+// Replaces the aws-lc-rs calls behind quic/s2n-quic-crypto:
 //   seal  <LessSafeKey as Aead>::encrypt -> seal_in_place_scatter   src/aead/default.rs:44-62
 //   open  <LessSafeKey as Aead>::decrypt -> open_in_place           src/aead/default.rs:65-93
 //   HP    HeaderKey::header_protection_mask -> new_mask             src/header_key.rs:52-56
 // with the nonce of Iv::nonce (src/iv.rs:27-39).
 //
-// Why four lanes per packet (tools/ubench/aes_core.hip): the AES + GHASH core runs 16 % more blocks per
-// second at 4 waves per SIMD than at 2, and the lane-per-packet kernel cannot get there: its per-wave payload staging
-// (32 KiB of LDS next to 128 KiB of tables) and its ~220 VGPRs hold it at 2.  Here the 4 lanes of a quad move a
+// Why four lanes per packet (tools/ubench/aes_core.hip): the AES + GHASH core runs more blocks per second
+// the more waves a SIMD holds, and the round-2 lane-per-packet kernel (deleted in round 3) was held at 2 by its per-wave
+// payload staging (32 KiB of LDS next to 128 KiB of tables) and its ~220 VGPRs.  Here the 4 lanes of a quad move a
 // packet's bytes themselves -- lane s takes counter slots t = 4 k + s, so each wave instruction loads 64 contiguous
 // bytes of each of 16 packets and one 4-block group of a lane covers 256 contiguous bytes of its packet -- with no
-// staging at all, and a workgroup is 1024 threads (16 waves, <= 128 VGPRs).
+// staging at all; a workgroup is 768 threads (12 waves, 3 per SIMD, <= 168 VGPRs: QPP_QUAD_WG).
 //
 // GHASH over four lanes: the sequence X_1..X_n (AAD blocks, ciphertext blocks, length block) is dealt to the lanes
 // by virtual slot (AAD block i at t = i + 1 - a, ciphertext block j at t = j + 1, length block at t = m + 1; lane
@@ -21,7 +21,7 @@
 //
 // LDS (160 KiB, one workgroup per CU):
 //   [0, 64K)     8-bit GHASH tables of H^4 (GhashT layout)
-//   [64K, 128K)  AES T0/T1 (AesLds)
+//   [64K, 128K)  AES tables (AesQ4: T0..T3, 8 copies each, in the lower 128 B of 256 rows; AesLds: T0/T1 x 32)
 //   [128K, 160K) 4-bit GHASH tables of H^1..H^4 (Ghash4 layout, power e at 128K + 8K (e - 1))
 // While a key's tables are built, [64K, 72K) holds V_e[m] = H^e x^m (e = 1..4), before the AES tables overwrite it.
 #include "device_common.h"
@@ -534,7 +534,8 @@ template <int NR>
 __global__ __launch_bounds__(kQuadWG<NR>) void aes_gcm_quad_rx_kernel(const DevKey *__restrict__ keys,
                                                                  uint32_t key_cap, const qpp_rx_pkt *__restrict__ rx,
                                                                  uint32_t n, uint8_t *arena, qpp_pkt *descs_out,
-                                                                 int8_t *status, uint32_t *scratch, uint32_t *perm) {
+                                                                 int8_t *status, uint32_t *scratch, uint32_t *perm,
+                                                                 uint32_t *timeouts) {
     uint32_t *counts = scratch + 16, *cursor = counts + key_cap, *meta = cursor + key_cap;
     WorkItem *work = (WorkItem *)(meta + 4);  // 16-byte aligned: key_cap is even
 #if QPP_RX_TRACE
@@ -572,8 +573,11 @@ __global__ __launch_bounds__(kQuadWG<NR>) void aes_gcm_quad_rx_kernel(const DevK
         }
         descs_out[t] = d;
     }
-    // a barrier that timed out: this workgroup's packets that were to be opened report INTERNAL_ERROR, untouched
+    // a barrier that timed out: this workgroup's packets that were to be opened report INTERNAL_ERROR, untouched (their
+    // headers stay unprotected, as the multi-launch path leaves a packet its open refuses), and the context's timeout
+    // counter says so (qpp_ctx_rx_timeouts)
     auto bail = [&]() {
+        if (tid == 0) __hip_atomic_fetch_add(timeouts, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         for (uint32_t t = lo + tid; t < hi; t += nt)
             if (status[t] == kRxOpen) status[t] = QPP_INTERNAL_ERROR;
     };
@@ -664,9 +668,9 @@ uint32_t quad_rx_max_keys() { return kRxHistMax; }
 
 hipError_t launch_aes_gcm_quad_rx(uint32_t nr, uint32_t grid, hipStream_t s, const DevKey *keys, uint32_t key_cap,
                                   const qpp_rx_pkt *rx, uint32_t n, uint8_t *arena, qpp_pkt *descs_out, int8_t *status,
-                                  uint32_t *scratch, uint32_t *perm) {
+                                  uint32_t *scratch, uint32_t *perm, uint32_t *timeouts) {
     if (key_cap > kRxHistMax || (key_cap & 1u)) return hipErrorInvalidValue;
-    void *args[] = {&keys, &key_cap, &rx, &n, &arena, &descs_out, &status, &scratch, &perm};
+    void *args[] = {&keys, &key_cap, &rx, &n, &arena, &descs_out, &status, &scratch, &perm, &timeouts};
     // cooperative: the grid barriers need every workgroup resident (one per CU: grid <= the CUs it may use)
     if (nr == 10)
         return hipLaunchCooperativeKernel(reinterpret_cast<const void *>(&aes_gcm_quad_rx_kernel<10>), dim3(grid),

@@ -29,7 +29,8 @@ OK, DECODE_ERROR, DECRYPT_ERROR, INTERNAL_ERROR, UNSUPPORTED, DEVICE_ERROR = 0, 
 ROTATION_NOT_SUPPORTED = 6  # dc open::Error::RotationNotSupported
 HP_MASK_OUT, HP_APPLY, ONLY_AES, ONLY_CHACHA = 0x1, 0x2, 0x10, 0x20
 KEY_BY_CONN = 0x40  # host batches: key_idx = connection index (qpp_ctx_set_conn_keys)
-AES_KERNEL_AUTO, AES_KERNEL_LANE, AES_KERNEL_WAVE = 0, 1, 2
+AES_KERNEL_AUTO, AES_KERNEL_QUAD, AES_KERNEL_WAVE = 0, 1, 2
+AES_KERNEL_LANE = AES_KERNEL_QUAD  # round-1..3 name of the quad selector (qpp.h)
 ENDPOINT_CLIENT, ENDPOINT_SERVER = 0, 1
 
 # qpp_pkt (24 bytes) as a numpy structured dtype
@@ -46,7 +47,7 @@ assert RX_DTYPE.itemsize == 24
 # every symbol include/qpp.h declares (tests/test_abi.py checks the library exports them all)
 EXPORTS = [
     "qpp_abi_version", "qpp_ctx_create", "qpp_ctx_destroy", "qpp_ctx_stream", "qpp_ctx_synchronize",
-    "qpp_ctx_last_error", "qpp_key_new", "qpp_key_new_raw", "qpp_key_update", "qpp_key_free", "qpp_key_free_batch", "qpp_ctx_set_aes_kernel", "qpp_key_slot", "qpp_key_slot_batch",
+    "qpp_ctx_last_error", "qpp_ctx_rx_timeouts", "qpp_key_new", "qpp_key_new_raw", "qpp_key_update", "qpp_key_free", "qpp_key_free_batch", "qpp_ctx_set_aes_kernel", "qpp_key_slot", "qpp_key_slot_batch",
     "qpp_key_suite", "qpp_tag_len", "qpp_sample_len", "qpp_confidentiality_limit", "qpp_integrity_limit",
     "qpp_key_material", "qpp_initial_keys", "qpp_seal", "qpp_seal_scatter", "qpp_open", "qpp_hp_mask",
     "qpp_seal_batch", "qpp_open_batch", "qpp_hp_mask_batch", "qpp_dev_alloc", "qpp_dev_free", "qpp_host_alloc",
@@ -95,6 +96,7 @@ def lib():
             "qpp_ctx_stream": (vp, [vp]),
             "qpp_ctx_synchronize": (ctypes.c_int, [vp]),
             "qpp_ctx_last_error": (ctypes.c_char_p, [vp]),
+            "qpp_ctx_rx_timeouts": (ctypes.c_int, [vp, ctypes.POINTER(u64)]),
             "qpp_key_new": (ctypes.c_int, [vp, ctypes.c_int, vp, sz, ctypes.POINTER(vp)]),
             "qpp_key_new_raw": (ctypes.c_int, [vp, ctypes.c_int, vp, sz, vp, vp, sz, ctypes.POINTER(vp)]),
             "qpp_key_update": (ctypes.c_int, [vp, ctypes.POINTER(vp)]),
@@ -200,6 +202,7 @@ class DeviceBuffer:
         p = vp()
         ctx._check(lib().qpp_dev_alloc(ctx.handle, self.nbytes, ctypes.byref(p)), "dev_alloc")
         self.ptr = p.value
+        ctx._bufs.append(self)
 
     def upload(self, arr, stream=None, offset=0):
         a = np.ascontiguousarray(arr)
@@ -216,7 +219,8 @@ class DeviceBuffer:
 
     def free(self):
         if self.ptr:
-            lib().qpp_dev_free(self.ctx.handle, self.ptr)
+            if self.ctx.handle:
+                lib().qpp_dev_free(self.ctx.handle, self.ptr)
             self.ptr = None
 
 
@@ -230,11 +234,27 @@ class Context:
             raise QppError(rc, f"qpp_ctx_create(device={device}): no usable gfx950 GPU (no CPU fallback exists)")
         self.handle = h.value
         self.device = device
+        # what this wrapper handed out, released in order by close(): device work drained first, then events,
+        # streams, device buffers and pinned host memory, and the context last -- nothing is left for the HIP
+        # runtime's (or a profiler's) process-exit teardown to destroy behind a context that no longer exists
+        self._bufs, self._events, self._streams, self._host = [], [], [], {}
 
     def close(self):
-        if self.handle:
-            lib().qpp_ctx_destroy(self.handle)
-            self.handle = None
+        if not self.handle:
+            return
+        h = self.handle
+        lib().qpp_ctx_synchronize(h)
+        for e in self._events:
+            lib().qpp_event_destroy(h, e)
+        for s in self._streams:
+            lib().qpp_stream_destroy(h, s)
+        for b in self._bufs:
+            b.free()
+        for p in self._host:
+            lib().qpp_host_free(h, p)
+        self._bufs, self._events, self._streams, self._host = [], [], [], {}
+        lib().qpp_ctx_destroy(h)
+        self.handle = None
 
     def __enter__(self):
         return self
@@ -256,7 +276,7 @@ class Context:
         self._check(lib().qpp_ctx_set_burst_max(self.handle, int(max_packets)), "set_burst_max")
 
     def set_aes_kernel(self, kernel):
-        """AES_KERNEL_AUTO / _LANE / _WAVE for batches above burst_max (identical outputs; A/B and tests)."""
+        """AES_KERNEL_AUTO / _QUAD / _WAVE for batches above burst_max (identical outputs; A/B and tests)."""
         self._check(lib().qpp_ctx_set_aes_kernel(self.handle, int(kernel)), "set_aes_kernel")
 
     def set_fips(self, on=True):
@@ -415,7 +435,13 @@ class Context:
     def event(self):
         e = vp()
         self._check(lib().qpp_event_create(self.handle, ctypes.byref(e)), "event")
+        self._events.append(e.value)
         return e.value
+
+    def event_destroy(self, ev):
+        if ev in self._events:
+            self._events.remove(ev)
+            lib().qpp_event_destroy(self.handle, ev)
 
     def record(self, ev, stream=None):
         self._check(lib().qpp_event_record(self.handle, ev, stream), "record")
@@ -423,10 +449,19 @@ class Context:
     def new_stream(self):
         st = vp()
         self._check(lib().qpp_stream_create(self.handle, ctypes.byref(st)), "stream")
+        self._streams.append(st.value)
         return st.value
 
     def stream_destroy(self, stream):
+        if stream in self._streams:
+            self._streams.remove(stream)
         lib().qpp_stream_destroy(self.handle, stream)
+
+    def rx_timeouts(self):
+        """fused-receive workgroups that left on a grid-barrier timeout since creation (qpp_ctx_rx_timeouts)"""
+        c = u64()
+        self._check(lib().qpp_ctx_rx_timeouts(self.handle, ctypes.byref(c)), "rx_timeouts")
+        return c.value
 
     def synchronize(self):
         """whole device (qpp_ctx_synchronize): every stream, key installs and retirements included"""
@@ -436,14 +471,17 @@ class Context:
         self._check(lib().qpp_stream_wait_event(self.handle, stream, ev), "wait_event")
 
     def host_alloc(self, nbytes):
-        """pinned host memory as a numpy uint8 array (host_free it, or it lives until the process ends)"""
+        """pinned host memory as a numpy uint8 array (host_free it, or close() releases it: no view may outlive either)"""
         p = vp()
         self._check(lib().qpp_host_alloc(self.handle, int(nbytes), ctypes.byref(p)), "host_alloc")
+        self._host[p.value] = int(nbytes)
         return np.ctypeslib.as_array((ctypes.c_uint8 * int(nbytes)).from_address(p.value))
 
     def host_free(self, arr):
         """release a host_alloc array (no view of it may be used afterwards)"""
-        lib().qpp_host_free(self.handle, arr.ctypes.data)
+        p = arr.ctypes.data
+        self._host.pop(p, None)
+        lib().qpp_host_free(self.handle, p)
 
     def elapsed_ms(self, e0, e1):
         ms = ctypes.c_float()

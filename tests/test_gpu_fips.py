@@ -23,10 +23,10 @@ def ctx():
     c.close()
 
 
-@pytest.fixture(params=["burst", "lane", "wave"])
+@pytest.fixture(params=["burst", "quad", "wave"])
 def path(request, ctx):
     ctx.set_burst_max(1 << 30 if request.param == "burst" else 0)
-    ctx.set_aes_kernel({"burst": qpp.AES_KERNEL_AUTO, "lane": qpp.AES_KERNEL_LANE,
+    ctx.set_aes_kernel({"burst": qpp.AES_KERNEL_AUTO, "quad": qpp.AES_KERNEL_QUAD,
                         "wave": qpp.AES_KERNEL_WAVE}[request.param])
     yield request.param
     ctx.set_burst_max(16384)

@@ -300,7 +300,7 @@ def test_random_operation_sequence(seed):
                 new_key()
             elif op == "knob":
                 knobs[0] = int(rng.choice([0, 64, 16384]))
-                knobs[1] = int(rng.choice([qpp.AES_KERNEL_AUTO, qpp.AES_KERNEL_LANE, qpp.AES_KERNEL_WAVE]))
+                knobs[1] = int(rng.choice([qpp.AES_KERNEL_AUTO, qpp.AES_KERNEL_QUAD, qpp.AES_KERNEL_WAVE]))
                 ctx.set_burst_max(knobs[0])
                 ctx.set_aes_kernel(knobs[1])
             elif op == "check":
@@ -403,7 +403,7 @@ def test_random_fips_sequence(seed):
                 add(ctx.key(s, _secret(rng, s)))
             elif op == "knob":
                 ctx.set_burst_max(int(rng.choice([0, 64, 16384])))
-                ctx.set_aes_kernel(int(rng.choice([qpp.AES_KERNEL_AUTO, qpp.AES_KERNEL_LANE, qpp.AES_KERNEL_WAVE])))
+                ctx.set_aes_kernel(int(rng.choice([qpp.AES_KERNEL_AUTO, qpp.AES_KERNEL_QUAD, qpp.AES_KERNEL_WAVE])))
         assert refused > 20
     finally:
         for k in keys:

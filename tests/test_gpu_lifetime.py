@@ -245,7 +245,7 @@ def test_key_update_batch_matches_chain(ctx):
         k.free()
 
 
-@pytest.mark.parametrize("kernel", ["burst", "lane"])
+@pytest.mark.parametrize("kernel", ["burst", "quad"])
 def test_bad_slots_are_refused(ctx, kernel):
     """key_idx outside the table, of a freed key or of a header key: INTERNAL_ERROR, the packet untouched, every other
     packet of the batch bit-exact (the kernels never dereference a slot outside the table)."""
@@ -357,12 +357,12 @@ def test_host_pipeline(ctx, ops):
 
 @pytest.mark.parametrize("suite", [1, 2])
 def test_single_live_key_batches_run_without_a_plan(suite):
-    """With exactly one live packet key (an AES one) the lane kernel runs without the plan launches
+    """With exactly one live packet key (an AES one) the quad kernel runs without the plan launches
     (api.cpp single_aes_slot); packets naming any other slot are still refused with INTERNAL_ERROR and left untouched,
     the rest are bit-exact, and open round-trips."""
     c = qpp.Context(0)
     try:
-        c.set_burst_max(0)  # the lane kernel, not the wave-per-packet one
+        c.set_burst_max(0)  # the quad kernel, not the wave-per-packet one
         rng = np.random.default_rng(70 + suite)
         k = c.key(suite, _secret(rng, suite))
         n = 4096

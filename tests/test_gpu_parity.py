@@ -23,12 +23,12 @@ def ctx():
     c.close()
 
 
-@pytest.fixture(params=["burst", "lane", "wave"])
+@pytest.fixture(params=["burst", "quad", "wave"])
 def path(request, ctx):
     """AES-GCM kernel path: wave per packet (small batches), lane per packet with one key per 1024-packet workgroup,
     or lane per packet with one key per 64-packet wave (many keys); same outputs."""
     ctx.set_burst_max(1 << 30 if request.param == "burst" else 0)
-    ctx.set_aes_kernel({"burst": qpp.AES_KERNEL_AUTO, "lane": qpp.AES_KERNEL_LANE,
+    ctx.set_aes_kernel({"burst": qpp.AES_KERNEL_AUTO, "quad": qpp.AES_KERNEL_QUAD,
                         "wave": qpp.AES_KERNEL_WAVE}[request.param])
     yield request.param
     ctx.set_burst_max(16384)
@@ -349,7 +349,7 @@ def test_full_size_round_trip(ctx, suite):
         k.free()
 
 
-@pytest.mark.parametrize("kernel", ["lane", "wave"])
+@pytest.mark.parametrize("kernel", ["quad", "wave"])
 def test_full_size_many_keys(ctx, kernel):
     """1 Mi x 1200 B over 4096 AES keys (BASELINE configs[4]'s key count; 2048 AES-128 + 2048 AES-256, ~256 packets
     per key) through both throughput kernels: a seeded 2000-packet sample is bit-exact against the oracle (ciphertext,
@@ -362,7 +362,7 @@ def test_full_size_many_keys(ctx, kernel):
                                         for _ in range(2048)], 1)
     slots = [k.slot for k in batch]
     okeys = orc.make_keys([(k.suite, *k.material()) for k in batch])
-    ctx.set_aes_kernel(qpp.AES_KERNEL_LANE if kernel == "lane" else qpp.AES_KERNEL_WAVE)
+    ctx.set_aes_kernel(qpp.AES_KERNEL_QUAD if kernel == "quad" else qpp.AES_KERNEL_WAVE)
     try:
         descs, arena = qpp.make_batch(n, pt_len, slots, seed=0x5eed0077)
         d_desc, d_arena, d_mask, d_status = (ctx.alloc(descs.nbytes), ctx.alloc(arena.nbytes), ctx.alloc(5 * n),

@@ -81,7 +81,7 @@ def _run(ctx, rx, arena, monkeypatch, fused):
 @pytest.mark.parametrize("suite", [1, 2])
 def test_fused_rx_equals_two_launch_path_and_oracle(ctx, suite, monkeypatch):
     rng = np.random.default_rng(40 + suite)
-    ctx.set_burst_max(0)  # lane-kernel batches at test size (the fused path is the lane kernel's)
+    ctx.set_burst_max(0)  # quad-kernel batches at test size (the fused path is the quad kernel's)
     try:
         k0 = ctx.key(suite, rng.integers(0, 256, qpp.HASH_LEN[suite], dtype=np.uint8).tobytes())
         k1 = k0.derive_next_key()
@@ -127,7 +127,7 @@ def test_fused_rx_many_keys(suite, monkeypatch):
     rng = np.random.default_rng(90 + suite)
     ctx = qpp.Context(0)
     ctx.set_burst_max(0)
-    ctx.set_aes_kernel(qpp.AES_KERNEL_LANE)  # the throughput kernel's regime at test size (fused path's condition)
+    ctx.set_aes_kernel(qpp.AES_KERNEL_QUAD)  # the throughput kernel's regime at test size (fused path's condition)
     try:
         pairs = []
         for c in range(36):

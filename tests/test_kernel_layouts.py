@@ -82,7 +82,8 @@ def test_resource_check_rejects_static_lds_and_scratch(tmp_path):
     r = _check(str(lds))
     assert r.returncode != 0 and "static LDS" in r.stderr
     scr = tmp_path / "scr.res"
-    scr.write_text(f"x: remark: Function Name: {name}\nx: remark:     ScratchSize [bytes/lane]: 12\n")
+    # (up to 32 B/lane -- a few per-packet spills outside the group loop -- is tolerated; more is refused)
+    scr.write_text(f"x: remark: Function Name: {name}\nx: remark:     ScratchSize [bytes/lane]: 48\n")
     r = _check(str(scr))
     assert r.returncode != 0 and "scratch" in r.stderr
     # a kernel outside the no-spill set (AES-256) may use scratch; it may not add static LDS either

@@ -20,7 +20,7 @@ def test_fused_rx_many_keys(suite, monkeypatch):
     rng = np.random.default_rng(90 + suite)
     ctx = qpp.Context(0)
     ctx.set_burst_max(0)
-    ctx.set_aes_kernel(qpp.AES_KERNEL_LANE)  # the throughput kernel's regime at test size (fused path's condition)
+    ctx.set_aes_kernel(qpp.AES_KERNEL_QUAD)  # the throughput kernel's regime at test size (fused path's condition)
     try:
         pairs = []
         for c in range(36):

@@ -376,8 +376,15 @@ typedef struct qpp_rx_pkt {
  * key_idx = chosen slot, aad_len = header_len + pn_len, pt_len, pn_len; flags = QPP_PKT_SKIP when rejected);
  * status[i] = QPP_OK, QPP_DECODE_ERROR (no room for the sample, short.rs / payload.rs), QPP_DECRYPT_ERROR, or
  * QPP_INTERNAL_ERROR (a slot outside the table, a key_idx[0] slot holding no key -- nothing touched -- or a chosen
- * packet key that is not live).  One launch (HP removal inside the open kernel) when the context's only live packet
- * key is AES or no AES record is live; identical outputs either way (env QPP_RX_FUSED=0 forces two launches).
+ * packet key that is not live: header unprotected, payload untouched).  QPP_ONLY_AES / QPP_ONLY_CHACHA: packets whose
+ * (live) key is of the other family are unprotected but not opened, their status left as it was.
+ * Launches: with any live AES packet key and a batch of the quad kernel's size (>= 1024 packets per live AES key),
+ * ONE cooperative launch unprotects, groups by the chosen key and opens the AES packets of both sizes, and one more
+ * launch on the same stream opens the ChaCha20 packets it sorted out (when ChaCha20 keys are live); with no AES record
+ * live, one launch of the ChaCha20 kernel; otherwise unprotect + plan + open kernels.  Identical outputs on every path
+ * (env QPP_RX_FUSED=0 forces the multi-launch one).  The cooperative launch needs all its workgroups resident at once:
+ * if they are not within a second (CUs held by a foreign kernel), its AES packets report QPP_INTERNAL_ERROR with the
+ * header unprotected and the payload untouched, and qpp_ctx_rx_timeouts counts it.
  * rx, descs_out, arena and status are device pointers.  Asynchronous. */
 int qpp_unprotect_open_batch(qpp_ctx *ctx, const qpp_rx_pkt *rx, size_t n, uint8_t *arena, qpp_pkt *descs_out,
                              int8_t *status, uint32_t flags, void *stream);

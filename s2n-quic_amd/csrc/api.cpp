@@ -1415,14 +1415,17 @@ int qpp_unprotect_open_batch(qpp_ctx *ctx, const qpp_rx_pkt *rx, size_t n, uint8
     RC_TRY(flush_keys(ctx));
     StreamState *st = nullptr;
     RC_TRY(batch_stream(ctx, stream, &st));
-    // Live packet keys all of ONE AES size (any number of them, any header-key suite) and a batch of the throughput
-    // kernel's size: ONE fused cooperative launch -- unprotect, group by the chosen key, open (quad.hip; the same
-    // outputs as the launches below).  QPP_RX_FUSED=0 forces the multi-launch path (A/B, tests).
+    // Any live AES packet key (any number of them, both sizes, beside ChaCha20 keys, any header-key suite) and a batch
+    // of the quad kernel's size: ONE fused cooperative launch -- unprotect, group by the chosen key, open the AES
+    // packets (quad.hip) -- and, when ChaCha20 packet keys are live, the ChaCha20 packets it sorted out opened by one
+    // more launch on the same stream (no host round trip).  The same outputs as the launches below.  QPP_RX_FUSED=0
+    // forces the multi-launch path (A/B, tests).
     const char *fz = getenv("QPP_RX_FUSED");
     const uint32_t a128 = ctx->live_by_suite[QPP_SUITE_TLS_AES_128_GCM_SHA256],
                    a256 = ctx->live_by_suite[QPP_SUITE_TLS_AES_256_GCM_SHA384];
-    if (!(flags & QPP_ONLY_CHACHA) && !(fz && fz[0] == '0') && !ctx->live_by_suite[QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256] &&
-        (a128 > 0) != (a256 > 0) && aes_path(ctx, (uint32_t)n) == AesPath::quad && ctx->key_cap <= quad_rx_max_keys()) {
+    const bool chacha = !(flags & QPP_ONLY_AES) && ctx->live_by_suite[QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256];
+    if (!(flags & QPP_ONLY_CHACHA) && !(fz && fz[0] == '0') && a128 + a256 > 0 &&
+        aes_path(ctx, (uint32_t)n) == AesPath::quad && ctx->key_cap <= quad_rx_max_keys()) {
         RC_TRY(ensure_plan(ctx, st, (uint32_t)n));  // perm
         const uint32_t kc = ctx->key_cap;
         if (st->rx_scratch_keys < kc) {
@@ -1436,8 +1439,11 @@ int qpp_unprotect_open_batch(qpp_ctx *ctx, const qpp_rx_pkt *rx, size_t n, uint8
         }
         HIP_TRY(ctx, hipMemsetAsync(st->rx_scratch, 0, 4 * (16 + 2 * (size_t)kc), st->stream));
         const uint32_t grid = std::min<uint32_t>(cu_avail(ctx), std::max<uint32_t>(1, (uint32_t)((n + 191) / 192)));
-        HIP_TRY(ctx, launch_aes_gcm_quad_rx(a128 ? 10 : 14, grid, st->stream, ctx->d_keys, kc, rx, (uint32_t)n, arena,
-                                            descs_out, status, st->rx_scratch, st->plan.perm, ctx->d_diag));
+        HIP_TRY(ctx, launch_aes_gcm_quad_rx(a256 ? (a128 ? 0u : 14u) : 10u, grid, st->stream, ctx->d_keys, kc, rx, (uint32_t)n, arena, descs_out, status,
+                                            st->rx_scratch, st->plan.perm, ctx->d_diag, chacha));
+        if (chacha)
+            HIP_TRY(ctx, launch_chacha_sel(ctx->d_keys, kc, descs_out, (uint32_t)n, arena, status, st->plan.perm,
+                                           st->rx_scratch + 2, st->stream));
         return note_work(ctx, st);
     }
     // No AES record live at all (packet or header keys): every header and packet key a packet can name is ChaCha20,

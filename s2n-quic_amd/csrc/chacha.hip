@@ -103,17 +103,29 @@ __device__ __forceinline__ uint32_t chacha_rho(uint32_t p) { return (p + (p >> 4
 // RX (open only): the fused receive path for a context with no live AES record -- each lane first unprotects its
 // packet of rx[] (rx_unprotect_one: HP removal, PN expansion, key phase; ChaCha20 header keys only), writes the
 // qpp_pkt to descs_out and opens it with the key the phase picked.  Same outputs as unprotect_kernel + this kernel.
+// Selection mode (sel != nullptr, open only): the packets are descs[sel[sel_meta[1] + i]], i < min(n, sel_meta[0]) --
+// the ChaCha20 packets the fused receive kernel (quad.hip) sorted behind its AES packets, their count on the device.
 template <bool SEAL, bool RX = false>
 __global__ __launch_bounds__(256, 3) void chacha_kernel(const DevKey *__restrict__ keys, uint32_t key_cap,
                                                     const qpp_pkt *__restrict__ descs, uint32_t n,
                                                     uint8_t *__restrict__ arena, uint8_t *masks, int8_t *status,
                                                     uint32_t flags, const qpp_rx_pkt *__restrict__ rx = nullptr,
-                                                    qpp_pkt *__restrict__ descs_out = nullptr) {
-    const uint32_t pi = blockIdx.x * blockDim.x + threadIdx.x;
+                                                    qpp_pkt *__restrict__ descs_out = nullptr,
+                                                    const uint32_t *__restrict__ sel = nullptr,
+                                                    const uint32_t *__restrict__ sel_meta = nullptr) {
+    const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t pi = slot;  // the packet (descriptor, status and mask index)
+    if (sel) {
+        const uint32_t cnt = min(n, sel_meta[0]);
+        if (blockIdx.x * blockDim.x >= cnt) return;  // (workgroup-uniform: the grid is sized for n)
+        n = cnt;
+        pi = slot < cnt ? sel[sel_meta[1] + slot] : 0u;
+    }
+    const bool valid = slot < n;
     qpp_pkt d;
     if constexpr (RX) {
         static_assert(!SEAL, "the receive path opens");
-        if (pi < n) {
+        if (valid) {
             d = rx_unprotect_one<false>(AesLds{0}, keys, key_cap, rx[pi], arena, status, pi);
             descs_out[pi] = d;
         } else {
@@ -121,15 +133,15 @@ __global__ __launch_bounds__(256, 3) void chacha_kernel(const DevKey *__restrict
             d.flags = QPP_PKT_SKIP;  // helper lane
         }
     } else {
-        d = descs[pi < n ? pi : n - 1];  // (any valid descriptor for helper lanes)
+        d = valid ? descs[pi] : sel ? descs[sel[sel_meta[1]]] : descs[n - 1];  // (any valid descriptor for helper lanes)
     }
     const bool bad_slot = d.key_idx >= key_cap;    // never dereferenced: the packet is refused
     const DevKey *__restrict__ key = keys + (bad_slot ? 0u : d.key_idx);
     // a slot outside the table, a freed slot or a header-key-only slot holds no packet key: refused (no AES kernel
     // takes such a packet either: the plan gives it no work item with a round count)
     const bool refused = bad_slot || key->live != 1;
-    if (refused && pi < n && status && !(d.flags & QPP_PKT_SKIP)) status[pi] = QPP_INTERNAL_ERROR;
-    const bool has = pi < n && !refused && key->suite == QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256 &&
+    if (refused && valid && status && !(d.flags & QPP_PKT_SKIP)) status[pi] = QPP_INTERNAL_ERROR;
+    const bool has = valid && !refused && key->suite == QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256 &&
                      !(d.flags & QPP_PKT_SKIP);
     if (!__any(has)) return;  // wave-uniform: AES packets go to the AES kernels
     const uint32_t lane = threadIdx.x & 63u;
@@ -522,7 +534,9 @@ __global__ __launch_bounds__(1024) void hp_mask_kernel(const DevKey *__restrict_
 //   (header_crypto.rs:98-123: first byte, pn_len = (b0 & 3) + 1, PN bytes) -> expand the PN against the space's
 //   largest acknowledged PN (packet/number/mod.rs:191-238) -> the packet key by the key-phase bit 0x04
 //   (key_phase.rs:12,46; KeySet::decrypt_packet, keyset.rs:113-143; long headers: key_idx[0]) -> the qpp_pkt the
-//   open kernels consume.  A packet too short for the sample is DECODE_ERROR and marked QPP_PKT_SKIP.
+//   open kernels consume.  A packet too short for the sample is DECODE_ERROR and marked QPP_PKT_SKIP; a packet whose
+//   chosen key is not a live packet key is INTERNAL_ERROR here already (no open kernel takes it, whatever the batch's
+//   QPP_ONLY_* flags; the fused receive kernel decides the same in its phase A).
 __global__ __launch_bounds__(1024) void unprotect_kernel(const DevKey *__restrict__ keys, uint32_t key_cap,
                                                         const qpp_rx_pkt *__restrict__ rx, uint32_t n,
                                                         uint8_t *__restrict__ arena, qpp_pkt *descs_out,
@@ -532,7 +546,10 @@ __global__ __launch_bounds__(1024) void unprotect_kernel(const DevKey *__restric
     __syncthreads();
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    descs_out[i] = rx_unprotect_one(make_aes(0), keys, key_cap, rx[i], arena, status, i);
+    uint4 kw;
+    const qpp_pkt d = rx_unprotect_one(make_aes(0), keys, key_cap, rx[i], arena, status, i, &kw);
+    if (!(d.flags & QPP_PKT_SKIP) && kw.w != 1) status[i] = QPP_INTERNAL_ERROR;
+    descs_out[i] = d;
 }
 
 }  // namespace
@@ -565,6 +582,16 @@ hipError_t launch_chacha(bool seal, const DevKey *keys, uint32_t key_cap, const 
     else
         hipLaunchKernelGGL(chacha_kernel<false>, grid, block, lds, s, keys, key_cap, descs, n, arena, masks, status, flags,
                            nullptr, nullptr);
+    return hipGetLastError();
+}
+
+hipError_t launch_chacha_sel(const DevKey *keys, uint32_t key_cap, const qpp_pkt *descs, uint32_t n_max,
+                             uint8_t *arena, int8_t *status, const uint32_t *sel, const uint32_t *sel_meta, hipStream_t s) {
+    if (!n_max) return hipSuccess;
+    const dim3 grid((n_max + 255) / 256), block(256);
+    const uint32_t lds = 4u * kChachaWaveLds;
+    hipLaunchKernelGGL((chacha_kernel<false, false>), grid, block, lds, s, keys, key_cap, descs, n_max, arena, nullptr,
+                       status, 0u, nullptr, nullptr, sel, sel_meta);
     return hipGetLastError();
 }
 

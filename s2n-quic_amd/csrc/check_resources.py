@@ -23,7 +23,7 @@ for path in sys.argv[1:]:
                                           "aes_gcm_burst_kernel", "txq_server_kernel"))
         # the throughput kernels whose hot loops must not spill (AES-128: the headline)
         default = ("aes_gcm_wave_kernel" in name or re.search(r"aes_gcm_quad_kernelILb[01]ELi10E", name)
-                   or re.search(r"aes_gcm_quad_rx_kernelILi10E", name))
+                   or re.search(r"aes_gcm_quad_rx_kernelILi10E", name))  # (the AES-128-only receive instance)
         if lds and dyn_lds and int(lds.group(1)) != 0:
             bad.append(f"{name}: {lds.group(1)} B of static LDS on top of the dynamic 160 KiB")
         # (a few per-packet spills outside the group loop are tolerated: tools/isa_report.py shows where they are)

@@ -196,14 +196,19 @@ hipError_t launch_aes_gcm_single(bool seal, const DevKey *keys, const qpp_pkt *d
                                  uint32_t n, uint32_t n_cu, uint8_t *arena, uint8_t *masks, int8_t *status,
                                  uint32_t flags, hipStream_t s);
 // quad.hip: the quad-layout (4 lanes per packet, 768-thread workgroups) throughput kernel behind the two above
-// quad.hip: fused unprotect -> PN expand -> key-phase choice -> open for any mix of live packet keys of ONE AES size
-// (nr), one cooperative launch of `grid` workgroups (<= the CUs it may use; key_cap <= quad_rx_max_keys(), even).
-// scratch: 16 + 2 key_cap + 4 + 4 (key_cap + 1) words, the first 16 + 2 key_cap zeroed before the launch; perm: n words.
-// timeouts: a device word every workgroup that left on a barrier timeout increments (qpp_ctx_rx_timeouts).
+// quad.hip: fused unprotect -> PN expand -> key-phase choice -> open for any mix of live packet keys (AES-128 and
+// AES-256 opened in the launch -- aes = 10 / 14 when only one size is live, 0 for both; ChaCha20 packets, when `chacha`, sorted to perm[scratch[3], + scratch[2]) for
+// launch_chacha_sel behind it), one cooperative launch of `grid` workgroups (<= the CUs it may use; key_cap <=
+// quad_rx_max_keys(), even).  scratch: 16 + 2 key_cap + 4 + 4 (key_cap + 1) words, the first 16 + 2 key_cap zeroed
+// before the launch; perm: n words.  timeouts: a device word every workgroup that left on a barrier timeout increments
+// (qpp_ctx_rx_timeouts).
 uint32_t quad_rx_max_keys();
-hipError_t launch_aes_gcm_quad_rx(uint32_t nr, uint32_t grid, hipStream_t s, const DevKey *keys, uint32_t key_cap,
+hipError_t launch_aes_gcm_quad_rx(uint32_t aes, uint32_t grid, hipStream_t s, const DevKey *keys, uint32_t key_cap,
                                   const qpp_rx_pkt *rx, uint32_t n, uint8_t *arena, qpp_pkt *descs_out, int8_t *status,
-                                  uint32_t *scratch, uint32_t *perm, uint32_t *timeouts);
+                                  uint32_t *scratch, uint32_t *perm, uint32_t *timeouts, bool chacha);
+// chacha.hip: open descs[sel[sel_meta[1] + i]] for i < min(n_max, sel_meta[0]) (count and base on the device)
+hipError_t launch_chacha_sel(const DevKey *keys, uint32_t key_cap, const qpp_pkt *descs, uint32_t n_max,
+                             uint8_t *arena, int8_t *status, const uint32_t *sel, const uint32_t *sel_meta, hipStream_t s);
 hipError_t launch_aes_gcm_quad(bool seal, uint32_t nr, dim3 grid, hipStream_t s, const DevKey *keys,
                                const qpp_pkt *descs, const PlanBuffers &pb, uint8_t *arena, uint8_t *masks,
                                int8_t *status, uint32_t flags, uint32_t single, uint32_t n_single);

@@ -486,17 +486,21 @@ __global__ __launch_bounds__(kQuadWG<NR>) void aes_gcm_quad_kernel(const DevKey 
 
 // ---------------------------------------------------------------- fused receive path, any key mix, ONE launch
 // crypto::unprotect + crypto::decrypt for a GRO batch (quic/s2n-quic-core/src/crypto/packet_protection.rs; the key by
-// the key-phase bit, crypto/application/keyset.rs:113-143), whatever the connections' keys, as one cooperative
-// launch in four phases separated by grid barriers:
-//   A. each workgroup unprotects its slice of rx[] (one lane per packet: rx_unprotect_one -- HP mask, first byte and
-//      PN unmasked in place, PN expanded, key chosen), writes descs_out[], and counts its packets per chosen key in
-//      LDS (the GHASH table area is free until phase D);
-//   B. workgroup 0 turns the global counts into each key's first perm index and one work item per key;
-//   C. each workgroup reserves a block per key (one atomic per key it saw) and scatters its packets into perm[];
-//   D. the quad open over the key-sorted perm, exactly as aes_gcm_quad_kernel runs a planned batch.
-// It replaces unprotect_kernel + the three plan launches + the open launch (tests/test_gpu_rx_fused.py: bit-exact
-// against that path and the oracle).  A barrier that does not complete within a second (a workgroup that never became
-// resident) makes every workgroup leave: its packets bound for the open phase report INTERNAL_ERROR, payload untouched.
+// the key-phase bit, crypto/application/keyset.rs:113-143; the suite per key, cipher_suite/negotiated.rs:15-125),
+// whatever the connections' keys and suites, as one cooperative launch in four phases separated by grid barriers:
+//   A. each workgroup unprotects its slice of rx[] (one lane per packet: rx_unprotect_one -- HP mask of any suite,
+//      first byte and PN unmasked in place, PN expanded, key chosen), writes descs_out[], and counts its packets per
+//      chosen key in LDS (the GHASH table area is free until phase D);
+//   B. workgroup 0 turns the global counts into each key's first perm index -- AES-128 keys first, then AES-256, then
+//      ChaCha20 -- and one work item per AES key;
+//   C. each workgroup reserves a block per key it saw (one atomic per key) and scatters its packets into perm[];
+//   D. the quad open over the key-sorted AES-128 packets, then the AES-256 ones, exactly as aes_gcm_quad_kernel runs a
+//      planned batch (both round counts in one launch: the segment's NR is a template instance, the tables per key).
+// The ChaCha20-Poly1305 packets (perm[scratch[3], + scratch[2])) are opened by chacha_kernel in selection mode, launched
+// right behind on the same stream (no host round trip).  It replaces unprotect_kernel + the three plan launches + the
+// open launches (tests/test_gpu_rx_fused.py: bit-exact against that path and the oracle).  A barrier that does not
+// complete within a second (a workgroup that never became resident) makes every workgroup leave: its packets bound for
+// the open phase report INTERNAL_ERROR, payload untouched, and the context's timeout counter is raised.
 #ifndef QPP_RX_TRACE
 #define QPP_RX_TRACE 0  // 1: workgroups 0, grid/2 and the last print their phase times (s_memrealtime)
 #endif
@@ -505,8 +509,8 @@ constexpr uint32_t kRxHistMax = 16384;    // LDS bins [0, 64 KiB): keys per work
 constexpr uint64_t kRxBarrierTicks = 100000000ull;  // 1 s of s_memrealtime (100 MHz)
 constexpr int8_t kRxOpen = 0x7f;  // status of a packet bound for the open phase (never a final status)
 
-// scratch (device, words): [0] barrier count, [1] failed | counts[key_cap] @16 | cursor[key_cap] | meta[4] | work[]
-// (the first 16 + 2 key_cap words are zeroed before each launch)
+// scratch (device, words): [0] barrier count, [1] failed, [2] ChaCha packets, [3] their first perm index |
+// counts[key_cap] @16 | cursor[key_cap] | meta[4] | work[]  (the first 16 + 2 key_cap words are zeroed before each launch)
 __device__ bool rx_grid_sync(uint32_t *scratch, uint32_t target) {
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -530,12 +534,22 @@ __device__ bool rx_grid_sync(uint32_t *scratch, uint32_t target) {
     return lds_ld32(kRxCtl) != 0;
 }
 
-template <int NR>
-__global__ __launch_bounds__(kQuadWG<NR>) void aes_gcm_quad_rx_kernel(const DevKey *__restrict__ keys,
+// the open class of a live packet key: 0 AES-128, 1 AES-256, 2 ChaCha20-Poly1305 (3: not opened here)
+__device__ __forceinline__ uint32_t rx_class(uint4 kw, bool chacha) {
+    if (kw.w != 1) return 3u;
+    if (kw.x == QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256) return chacha ? 2u : 3u;
+    return kw.y == 10 ? 0u : kw.y == 14 ? 1u : 3u;
+}
+
+// AES: 10 or 14 when the live AES packet keys are all of one size (that instance alone: no registers spent on the
+// other), 0 for both sizes in one launch
+static_assert(kQuadWG<10> == kQuadWG<14>, "the fused receive runs both round counts in one launch");
+template <int AES>
+__global__ __launch_bounds__(kQuadWG<10>) void aes_gcm_quad_rx_kernel(const DevKey *__restrict__ keys,
                                                                  uint32_t key_cap, const qpp_rx_pkt *__restrict__ rx,
                                                                  uint32_t n, uint8_t *arena, qpp_pkt *descs_out,
                                                                  int8_t *status, uint32_t *scratch, uint32_t *perm,
-                                                                 uint32_t *timeouts) {
+                                                                 uint32_t *timeouts, uint32_t chacha) {
     uint32_t *counts = scratch + 16, *cursor = counts + key_cap, *meta = cursor + key_cap;
     WorkItem *work = (WorkItem *)(meta + 4);  // 16-byte aligned: key_cap is even
 #if QPP_RX_TRACE
@@ -555,10 +569,11 @@ __global__ __launch_bounds__(kQuadWG<NR>) void aes_gcm_quad_rx_kernel(const DevK
     // A: unprotect the slice, count per chosen key
     const uint32_t P = (n + gridDim.x - 1) / gridDim.x;
     const uint32_t lo = min(n, blockIdx.x * P), hi = min(n, lo + P);
-    // A packet goes to the open phase when its chosen key is a live packet key of this launch's AES size; the others
-    // get INTERNAL_ERROR (descs_out as unprotect_kernel writes it: the multi-launch path's plan refuses them
-    // likewise).  The verdict is kept in status (kRxOpen) for phase C, which must scatter exactly the packets phase A
-    // counted (a record retired meanwhile must not change it); phase D overwrites kRxOpen.
+    // A packet goes to the open phase when its chosen key is a live packet key (an AES one, or a ChaCha20 one when the
+    // launch opens those too); the others get INTERNAL_ERROR (descs_out as unprotect_kernel writes it: the multi-launch
+    // path's plan refuses them likewise) -- except a ChaCha20 packet of an AES-only batch, which the multi-launch path
+    // leaves alone as well.  The verdict is kept in status (kRxOpen) for phase C, which must scatter exactly the packets
+    // phase A counted (a record retired meanwhile must not change it); phase D (or the ChaCha launch) overwrites it.
     // (the next packet's rx descriptor is loaded while this one is unprotected: one round trip off each packet)
     qpp_rx_pkt r_next = lo + tid < hi ? rx[lo + tid] : qpp_rx_pkt{};
     for (uint32_t t = lo + tid; t < hi; t += nt) {
@@ -567,9 +582,13 @@ __global__ __launch_bounds__(kQuadWG<NR>) void aes_gcm_quad_rx_kernel(const DevK
         uint4 kw;  // the chosen key's suite, nr, hp_nr, live (loaded with the header key's record)
         const qpp_pkt d = rx_unprotect_one(aes, keys, key_cap, r, arena, status, t, &kw);
         if (!(d.flags & QPP_PKT_SKIP)) {
-            const bool open = kw.w == 1 && kw.y == (uint32_t)NR;
-            status[t] = open ? kRxOpen : (int8_t)QPP_INTERNAL_ERROR;
-            if (open) lds_add32(4 * d.key_idx, 1u);
+            const uint32_t cls = rx_class(kw, chacha != 0);
+            if (cls < 3) {
+                status[t] = kRxOpen;
+                lds_add32(4 * d.key_idx, 1u);
+            } else if (!(kw.w == 1 && kw.x == QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256)) {
+                status[t] = QPP_INTERNAL_ERROR;
+            }
         }
         descs_out[t] = d;
     }
@@ -589,47 +608,70 @@ __global__ __launch_bounds__(kQuadWG<NR>) void aes_gcm_quad_rx_kernel(const DevK
     RX_TS(2);
     if (!rx_grid_sync(scratch, gridDim.x)) return bail();
     RX_TS(3);
-    // B: workgroup 0 -- each key's first perm index (cursor) and one work item per key with packets
+    // B: workgroup 0 -- each key's first perm index (cursor; AES-128 keys, then AES-256, then ChaCha20) and one work
+    // item per AES key with packets (AES-128 items first: the planned-batch layout quad_slices reads from meta)
     if (blockIdx.x == 0) {
         const uint32_t chunk = (key_cap + nt - 1) / nt, k0 = min(key_cap, tid * chunk), k1 = min(key_cap, k0 + chunk);
-        uint32_t sum = 0, nz = 0;
+        auto cls_of = [&](uint32_t k) { return rx_class(*(const uint4 *)(keys + k), chacha != 0); };
+        // per thread: packets of each class (0..2) and AES keys with packets of each AES class (3, 4)
+        uint32_t v[5] = {0, 0, 0, 0, 0};
         for (uint32_t k = k0; k < k1; k++) {
             const uint32_t c = counts[k];
-            sum += c;
-            nz += c != 0;
+            if (!c) continue;
+            const uint32_t cls = cls_of(k);  // (< 3: phase A counted only packets of open classes)
+            v[cls] += c;
+            if (cls < 2) v[3 + cls] += 1;
         }
-        // exclusive scans of the per-thread (sum, nz) in thread order: inclusive scan inside each wave (shuffles),
+        // exclusive scans of the five per-thread counts in thread order: inclusive scan inside each wave (shuffles),
         // the waves' totals through LDS (a thread-0 loop over 768 entries took ~40 us)
         const uint32_t lane = tid & 63u, wv = tid >> 6, nwv = (nt + 63u) >> 6;
-        uint32_t is = sum, iz = nz;
+        uint32_t is[5];
+#pragma unroll
+        for (int j = 0; j < 5; j++) is[j] = v[j];
 #pragma unroll
         for (uint32_t o = 1; o < 64; o <<= 1) {
-            const uint32_t ps = (uint32_t)__shfl_up((int)is, o, 64), pz = (uint32_t)__shfl_up((int)iz, o, 64);
-            if (lane >= o) { is += ps; iz += pz; }
+#pragma unroll
+            for (int j = 0; j < 5; j++) {
+                const uint32_t p = (uint32_t)__shfl_up((int)is[j], o, 64);
+                if (lane >= o) is[j] += p;
+            }
         }
         if (lane == 63) {
-            lds_st32(kRxCtl + 64 + 4 * wv, is);
-            lds_st32(kRxCtl + 64 + 4 * (16 + wv), iz);
+#pragma unroll
+            for (int j = 0; j < 5; j++) lds_st32(kRxCtl + 64 + 4 * (16 * j + wv), is[j]);
         }
         __syncthreads();
-        uint32_t off = is - sum, item = iz - nz, ta = 0, tb = 0;
-        for (uint32_t v = 0; v < nwv; v++) {
-            const uint32_t ws = lds_ld32(kRxCtl + 64 + 4 * v), wz = lds_ld32(kRxCtl + 64 + 4 * (16 + v));
-            if (v < wv) { off += ws; item += wz; }
-            ta += ws;
-            tb += wz;
+        uint32_t ex[5], tot[5];
+#pragma unroll
+        for (int j = 0; j < 5; j++) {
+            ex[j] = is[j] - v[j];
+            tot[j] = 0;
         }
+        for (uint32_t w = 0; w < nwv; w++) {
+#pragma unroll
+            for (int j = 0; j < 5; j++) {
+                const uint32_t ws = lds_ld32(kRxCtl + 64 + 4 * (16 * j + w));
+                if (w < wv) ex[j] += ws;
+                tot[j] += ws;
+            }
+        }
+        uint32_t off[3] = {ex[0], tot[0] + ex[1], tot[0] + tot[1] + ex[2]};
+        uint32_t item[2] = {ex[3], tot[3] + ex[4]};
         if (tid == 0) {
-            meta[0] = tb;                    // work items
-            meta[1] = NR == 10 ? tb : 0u;    // AES-128 items (all of them, or none)
-            meta[2] = NR == 10 ? ta : 0u;    // AES-128 packets
-            meta[3] = NR == 10 ? 0u : ta;    // AES-256 packets
+            meta[0] = tot[3] + tot[4];     // work items
+            meta[1] = tot[3];              // AES-128 items
+            meta[2] = tot[0];              // AES-128 packets
+            meta[3] = tot[1];              // AES-256 packets
+            scratch[2] = tot[2];           // ChaCha20 packets ...
+            scratch[3] = tot[0] + tot[1];  // ... from this perm index on
         }
         for (uint32_t k = k0; k < k1; k++) {
             const uint32_t c = counts[k];
-            cursor[k] = off;
-            if (c) work[item++] = WorkItem{k, off, c, (uint32_t)NR};
-            off += c;
+            if (!c) continue;
+            const uint32_t cls = cls_of(k);
+            cursor[k] = off[cls];
+            if (cls < 2) work[item[cls]++] = WorkItem{k, off[cls], c, cls ? 14u : 10u};
+            off[cls] += c;
         }
     }
     if (!rx_grid_sync(scratch, 2 * gridDim.x)) return bail();
@@ -645,8 +687,9 @@ __global__ __launch_bounds__(kQuadWG<NR>) void aes_gcm_quad_rx_kernel(const DevK
     RX_TS(5);
     if (!rx_grid_sync(scratch, 3 * gridDim.x)) return bail();
     RX_TS(6);
-    // D: open, key-sorted slices (tables per key segment, as a planned batch)
-    quad_slices<false, NR>(keys, descs_out, perm, work, meta, arena, nullptr, status, 0u, 0xffffffffu, 0u);
+    // D: open, key-sorted slices (tables per key segment, as a planned batch): the AES-128 packets, then the AES-256 ones
+    if constexpr (AES != 14) quad_slices<false, 10>(keys, descs_out, perm, work, meta, arena, nullptr, status, 0u, ~0u, 0u);
+    if constexpr (AES != 10) quad_slices<false, 14>(keys, descs_out, perm, work, meta, arena, nullptr, status, 0u, ~0u, 0u);
 #if QPP_RX_TRACE
     RX_TS(7);
     if (threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1 || blockIdx.x == gridDim.x / 2))
@@ -666,17 +709,17 @@ void launch_quad(dim3 grid, hipStream_t s, const DevKey *keys, const qpp_pkt *de
 
 uint32_t quad_rx_max_keys() { return kRxHistMax; }
 
-hipError_t launch_aes_gcm_quad_rx(uint32_t nr, uint32_t grid, hipStream_t s, const DevKey *keys, uint32_t key_cap,
+hipError_t launch_aes_gcm_quad_rx(uint32_t aes, uint32_t grid, hipStream_t s, const DevKey *keys, uint32_t key_cap,
                                   const qpp_rx_pkt *rx, uint32_t n, uint8_t *arena, qpp_pkt *descs_out, int8_t *status,
-                                  uint32_t *scratch, uint32_t *perm, uint32_t *timeouts) {
+                                  uint32_t *scratch, uint32_t *perm, uint32_t *timeouts, bool chacha) {
     if (key_cap > kRxHistMax || (key_cap & 1u)) return hipErrorInvalidValue;
-    void *args[] = {&keys, &key_cap, &rx, &n, &arena, &descs_out, &status, &scratch, &perm, &timeouts};
+    uint32_t ch = chacha ? 1u : 0u;
+    void *args[] = {&keys, &key_cap, &rx, &n, &arena, &descs_out, &status, &scratch, &perm, &timeouts, &ch};
     // cooperative: the grid barriers need every workgroup resident (one per CU: grid <= the CUs it may use)
-    if (nr == 10)
-        return hipLaunchCooperativeKernel(reinterpret_cast<const void *>(&aes_gcm_quad_rx_kernel<10>), dim3(grid),
-                                          dim3(kQuadWG<10>), args, kLdsMax, s);
-    return hipLaunchCooperativeKernel(reinterpret_cast<const void *>(&aes_gcm_quad_rx_kernel<14>), dim3(grid),
-                                      dim3(kQuadWG<14>), args, kLdsMax, s);
+    const void *f = aes == 10   ? reinterpret_cast<const void *>(&aes_gcm_quad_rx_kernel<10>)
+                    : aes == 14 ? reinterpret_cast<const void *>(&aes_gcm_quad_rx_kernel<14>)
+                                : reinterpret_cast<const void *>(&aes_gcm_quad_rx_kernel<0>);
+    return hipLaunchCooperativeKernel(f, dim3(grid), dim3(kQuadWG<10>), args, kLdsMax, s);
 }
 
 // The quad-layout kernels behind launch_aes_gcm / launch_aes_gcm_single (aes_gcm.hip chooses).  single = 0xffffffff:

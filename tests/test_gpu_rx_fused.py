@@ -1,7 +1,7 @@
 """The fused receive kernel (quad.hip aes_gcm_quad_rx_kernel: unprotect -> PN expand -> key-phase choice -> group by
-key -> open, ONE cooperative launch, used when the live packet keys are all of one AES size, however many) against
-the multi-launch path (unprotect_kernel + plan + open, QPP_RX_FUSED=0) and against the oracle
-(orc_unprotect_open_batch).
+key -> open, ONE cooperative launch for any mix of live AES keys of both sizes, plus one ChaCha20 launch behind it on
+the same stream when ChaCha20 keys are live) against the multi-launch path (unprotect_kernel + plan + open,
+QPP_RX_FUSED=0) and against the oracle (orc_unprotect_open_batch).
 
 The batch is what a receiver sees during a key update (quic/s2n-quic-core/src/crypto/application/keyset.rs:113-143):
 short headers of both key phases and long headers, PNs truncated against the largest acknowledged PN, tampered tags,
@@ -244,5 +244,101 @@ def test_fused_chacha_rx_many_keys(monkeypatch):
             k0.free()
             if k1.handle:
                 k1.free()
+    finally:
+        ctx.close()
+
+
+@pytest.mark.parametrize("only_aes", [False, True])
+def test_fused_rx_mixed_suites(monkeypatch, only_aes):
+    """A server whose clients negotiated all three suites (cipher_suite/negotiated.rs:15-125): 18 connections, 6 per
+    suite, both key phases live, one connection per suite with its phase-1 key dropped; one GRO batch of their packets
+    at random.  The fused path (one cooperative launch for the AES packets of both sizes, the ChaCha20 packets opened by
+    one more launch on the stream) equals the multi-launch path bit for bit and the oracle on every packet.  With
+    QPP_ONLY_AES both paths leave the ChaCha20 packets' status alone (header unprotected, payload untouched); a packet
+    whose chosen key was dropped is INTERNAL_ERROR either way."""
+    rng = np.random.default_rng(120 + only_aes)
+    ctx = qpp.Context(0)
+    ctx.set_burst_max(0)
+    ctx.set_aes_kernel(qpp.AES_KERNEL_QUAD)  # the quad regime at test size (the fused path's condition)
+    try:
+        suites = [1, 2, 3] * 6
+        pairs = []
+        for s_ in suites:
+            k0 = ctx.key(s_, rng.integers(0, 256, qpp.HASH_LEN[s_], dtype=np.uint8).tobytes())
+            pairs.append((k0, k0.derive_next_key()))
+        mats = [(k.suite, *k.material()) for pair in pairs for k in pair]
+        slots = [(p[0].slot, p[1].slot) for p in pairs]
+        dropped_conn = [0, 1, 2]  # one connection of each suite dropped its phase-1 key
+        for c in dropped_conn:
+            pairs[c][1].free()
+        n = 6000
+        chunks, rx, orx = [], [], []
+        off = 0
+        for i in range(n):
+            c = int(rng.integers(0, len(pairs)))
+            largest = int(rng.integers(0, 2**40))
+            pn = largest + int(rng.integers(0, 300))
+            _, _, pn_len = orc.truncate_pn(pn, largest)
+            phase = int(rng.integers(0, 2))
+            header = bytes([0x40 | (phase << 2) | (pn_len - 1)]) + rng.integers(0, 256, 16, dtype=np.uint8).tobytes()
+            payload = rng.integers(0, 256, int(rng.integers(1, 1400)), dtype=np.uint8).tobytes()
+            s_, k, iv, hp = mats[2 * c + phase]
+            _, pkt = orc.protect_packet(s_, k, iv, hp, pn, header, pn_len, payload)
+            pkt = bytearray(pkt)
+            if i % 19 == 4:
+                pkt[-1 - i % 16] ^= 0x01  # tampered -> DECRYPT_ERROR
+            chunks.append(bytes(pkt) + bytes(int(rng.integers(0, 5))))
+            rx.append((largest, slots[c], off, len(header), len(pkt)))
+            orx.append((largest, (2 * c, 2 * c + 1), off, len(header), len(pkt)))
+            off += len(chunks[-1])
+        rx = np.array(rx, dtype=qpp.RX_DTYPE)
+        orx = np.array(orx, dtype=qpp.RX_DTYPE)
+        arena = np.frombuffer(b"".join(chunks) + bytes(64), dtype=np.uint8).copy()
+        flags = qpp.ONLY_AES if only_aes else 0
+
+        def run(fused):
+            monkeypatch.setenv("QPP_RX_FUSED", "1" if fused else "0")
+            d_rx, d_arena = ctx.alloc(rx.nbytes), ctx.alloc(arena.nbytes)
+            d_out, d_status = ctx.alloc(n * qpp.PKT_DTYPE.itemsize), ctx.alloc(n)
+            d_rx.upload(rx)
+            d_arena.upload(arena)
+            d_status.upload(np.full(n, 99, dtype=np.int8))
+            ctx.unprotect_open_batch(d_rx, n, d_arena, d_out, d_status, flags)
+            ctx.sync()
+            out = d_arena.download(), d_out.download(dtype=qpp.PKT_DTYPE), d_status.download(dtype=np.int8)
+            for b in (d_rx, d_arena, d_out, d_status):
+                b.free()
+            return out
+
+        a_f, o_f, s_f = run(True)
+        a_2, o_2, s_2 = run(False)
+        assert (s_f == s_2).all(), "status differs between the fused and the multi-launch path"
+        assert (a_f == a_2).all(), "arena differs between the fused and the multi-launch path"
+        assert (o_f.view(np.uint8) == o_2.view(np.uint8)).all(), "descriptors differ"
+        assert ctx.rx_timeouts() == 0
+        want_arena = arena.copy()
+        want_out, want_st = orc.unprotect_open_batch(orc.make_keys(mats), orx, want_arena)
+        want_st = np.array(want_st, dtype=np.int8)
+        conn = want_out["key_idx"] // 2
+        dropped = np.isin(want_out["key_idx"], [2 * c + 1 for c in dropped_conn])
+        chacha = np.array([suites[c] == 3 for c in conn])
+        # QPP_ONLY_AES: neither path opens a ChaCha20 packet (a dropped key is refused whatever the flags)
+        untouched = chacha & only_aes & ~dropped
+        assert dropped.sum() > 50 and (s_f[dropped] == qpp.INTERNAL_ERROR).all()
+        ok = ~dropped & ~untouched
+        assert (s_f[ok] == want_st[ok]).all()
+        assert (s_f[untouched] == 99).all()
+        for suite_ in (1, 2, 3):
+            sel = ok & (np.array([suites[c] for c in conn]) == suite_)
+            if only_aes and suite_ == 3:
+                continue
+            assert (s_f[sel] == 0).sum() > 1000 // 3, suite_
+        assert (s_f == qpp.DECRYPT_ERROR).any()
+        for i in np.flatnonzero(ok):
+            o, ln = int(rx[i]["off"]), int(rx[i]["len"])
+            assert (a_f[o:o + ln] == want_arena[o:o + ln]).all(), i
+        for i in np.flatnonzero(untouched):
+            o, ln, aad = int(rx[i]["off"]), int(rx[i]["len"]), int(want_out[i]["aad_len"])
+            assert (a_f[o:o + aad] == want_arena[o:o + aad]).all() and (a_f[o + aad:o + ln] == arena[o + aad:o + ln]).all()
     finally:
         ctx.close()

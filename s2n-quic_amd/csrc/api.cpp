@@ -2113,7 +2113,7 @@ static void txq_reset_batch(qpp_txq *q) {
     q->suites = 0;
 }
 
-// Persistent queue: posts slots[cur]'s packets (all AES, no FIPS key live) to the server.  The descriptors are copied
+// Persistent queue: posts slots[cur]'s packets (any suite, no FIPS key live) to the server.  The descriptors are copied
 // into the server's plan (key-sorted, items of <= one packet per wave), so the slot is free for the next pushes at
 // once; the previous posted flush must be done first (its plan is being rewritten).
 static int srv_submit(qpp_txq *q) {
@@ -2201,8 +2201,8 @@ static int txq_submit(qpp_txq *q) {
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     RC_TRY(flush_keys(ctx));
     if (q->persistent) {
-        if (!ctx->fips_live && !(q->suites & ~kAesSuites)) return srv_submit(q);
-        // FIPS gating and ChaCha20-Poly1305 packets take the launched path, behind the posted flush
+        if (!ctx->fips_live) return srv_submit(q);
+        // FIPS gating takes the launched path (its nonce-order gate), behind the posted flush
         RC_TRY(srv_wait(q, q->srv_posted));
     }
     q->n_launch++;

@@ -17,7 +17,7 @@
 // T_0 comes from the key record's V[m] = H x^m; T_{t+1}[e] = T_t[e] * P_t through T_t.
 //
 // LDS (dynamic, offsets): [0, 64 KiB) AES T0/T1 bank-replicated (as aes_gcm.hip); [64, 120 KiB) T_0 .. T_6.
-#include "device_common.h"
+#include "chacha_wave.h"
 
 namespace qpp {
 namespace {
@@ -102,24 +102,17 @@ __global__ __launch_bounds__(512) void pow_setup_kernel(const DevKey *__restrict
     for (uint32_t i = threadIdx.x; i < kPowBytes / 16; i += blockDim.x) dst[i] = lds_ld128(tab(1) + 16u * i);
 }
 
-__device__ __forceinline__ uint4 shfl4(uint4 v, int src) {
-    return make_uint4((uint32_t)__shfl((int)v.x, src, 64), (uint32_t)__shfl((int)v.y, src, 64),
-                      (uint32_t)__shfl((int)v.z, src, 64), (uint32_t)__shfl((int)v.w, src, 64));
-}
 __device__ __forceinline__ uint4 shfl4_down(uint4 v, unsigned d) {
     return make_uint4((uint32_t)__shfl_down((int)v.x, d, 64), (uint32_t)__shfl_down((int)v.y, d, 64),
                       (uint32_t)__shfl_down((int)v.z, d, 64), (uint32_t)__shfl_down((int)v.w, d, 64));
 }
-__device__ __forceinline__ uint32_t byte_of(uint4 v, uint32_t i) {  // byte i (< 16) of v
-    const uint32_t w = i < 4 ? v.x : i < 8 ? v.y : i < 12 ? v.z : v.w;
-    return (w >> (8 * (i & 3))) & 0xffu;
-}
-
 // The persistent txq server's per-workgroup copy of its cached key's iv | rk | hp_rk (LDS, after the tables and
-// the control words): no device-memory round trip per packet for them.
+// the control words): no device-memory round trip per packet for them; its record header (suite, nr, hp_nr, live) at
+// kTxsKeyHdr.
 constexpr uint32_t kTxsCtl = kBurstLds;         // LDS: the polled slot (288 B) and the exit flag, for every wave
 constexpr uint32_t kTxsStopFlag = kTxsCtl + 16 * kTxsPollLanes;
 constexpr uint32_t kTxsKey = kTxsCtl + 320;
+constexpr uint32_t kTxsKeyHdr = kTxsKey + 496;  // (iv | rk | hp_rk: 124 words)
 constexpr uint32_t kTxsTrace = kTxsKey + 512;  // QPP_TXS_TRACE: wave 0's stamps inside its packet (8 words)
 constexpr uint32_t kTxsLds = kTxsTrace + 32;
 static_assert(kTxsStopFlag + 4 <= kTxsKey && kTxsLds <= kLdsMax && kBurstWaves == (int)kTxsWaves, "server LDS");
@@ -387,6 +380,23 @@ __device__ __forceinline__ void txs_item(const AesLds &aes, const DevKey *key, c
         burst_packet<NR, true, true>(aes, key, rk, d, 0, ring, nullptr, nullptr, QPP_HP_APPLY);
 }
 
+// A ChaCha20-Poly1305 work item (cipher_suite.rs:270-284): one wave per packet (chacha_wave_packet, the burst kernel's
+// code), the key and HP key from the LDS copy, the header protected in place
+__device__ __forceinline__ void txs_item_chacha(const qpp_pkt &d, uint32_t wave, uint32_t count, uint8_t *ring,
+                                                uint32_t lane) {
+    uint32_t k[8], hk[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        k[i] = __builtin_amdgcn_readfirstlane(lds_ld32(kTxsKey + 16 + 4 * i));
+        hk[i] = __builtin_amdgcn_readfirstlane(lds_ld32(kTxsKey + 256 + 4 * i));
+    }
+    // Iv::nonce (src/iv.rs:27-39)
+    const uint32_t n0 = lds_ld32(kTxsKey), n1 = lds_ld32(kTxsKey + 4) ^ bswap32((uint32_t)(d.pn >> 32)),
+                   n2 = lds_ld32(kTxsKey + 8) ^ bswap32((uint32_t)d.pn);
+    if (wave < count && !(d.flags & QPP_PKT_SKIP))
+        chacha_wave_packet<true>(k, n0, n1, n2, hk, d, ring, nullptr, nullptr, QPP_HP_APPLY, lane);
+}
+
 // one 16-byte chunk of the slot (lane < kTxsPollLanes), in ONE load past every cache (sc0 sc1: the host writes it;
 // a chunk is read whole, so its tag vouches for its other words)
 __device__ __forceinline__ uint4 txs_poll(const TxsSlot *slot, uint32_t lane) {
@@ -501,13 +511,23 @@ __global__ __launch_bounds__(kBurstWG) void txq_server_kernel(const DevKey *keys
             const DevKey *key = keys_v + w.key;
             if (w.key != cached) {  // uniform
                 __syncthreads();  // every wave is done with the previous key's tables
-                // iv | rk | hp_rk: 124 consecutive words of the record (DevKey: iv at word 4)
-                if (threadIdx.x < 124) lds_st32(kTxsKey + 4 * threadIdx.x, ((const uint32_t *)key)[4 + threadIdx.x]);
-                burst_tables(key, w.key, pow);  // (ends with a barrier)
+                // iv | rk | hp_rk: 124 consecutive words of the record (DevKey: iv at word 4), then its header
+                const uint32_t *kw = (const uint32_t *)key;
+                if (threadIdx.x < 124) lds_st32(kTxsKey + 4 * threadIdx.x, kw[4 + threadIdx.x]);
+                else if (threadIdx.x < 128) lds_st32(kTxsKeyHdr + 4 * (threadIdx.x - 124), kw[threadIdx.x - 124]);
+                if (w.nr == 10 || w.nr == 14) burst_tables(key, w.key, pow);  // (ends with a barrier)
+                else __syncthreads();  // (ChaCha20: no GHASH tables)
                 cached = w.key;
             }
-            if (w.nr == 10) txs_item<10>(aes, key, d, wave, w.count, ring);
-            else txs_item<14>(aes, key, d, wave, w.count, ring);
+            // the record as installed (a key freed since the flush was planned: its packets are left alone, as the
+            // launched path's kernels refuse them)
+            const uint32_t k_suite = lds_ld32(kTxsKeyHdr), k_nr = lds_ld32(kTxsKeyHdr + 4),
+                           k_live = lds_ld32(kTxsKeyHdr + 12);
+            if (k_live == 1 && k_nr == w.nr) {
+                if (w.nr == 10) txs_item<10>(aes, key, d, wave, w.count, ring);
+                else if (w.nr == 14) txs_item<14>(aes, key, d, wave, w.count, ring);
+                else if (k_suite == QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256) txs_item_chacha(d, wave, w.count, ring, lane);
+            }
         }
         // completion: this workgroup's ring stores reach the host before its done word
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -185,15 +185,24 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
     const int a = has ? (int)((aad_len + 15) >> 4) : 0;
     auto at = [&](uint32_t off) { return arena + off; };
 
-    // AAD blocks of this lane: virtual slots t = 1 - a .. 0, t = s (mod 4).  The chain starts at w = 0: its first step
-    // multiplies zero (one product more per lane that has no AAD block, in exchange for no started-flag control flow)
+    // AAD blocks of this lane: virtual slots t = 1 - a .. 0, t = s (mod 4).  A lane's first AAD block starts its chain
+    // (w = rot(x): no product of zero); a lane with no AAD block starts at w = 0 and its first data step multiplies zero
+    // (one product more for those lanes, in exchange for no started-flag control flow in the group loop).  With the
+    // usual 1..2 AAD blocks no lane has a second one and the product loop is skipped by the whole wave.
     uint4 w = make_uint4(0, 0, 0, 0);
-    for (int t = (1 - a) + (((int)s - (1 - a)) & 3); t <= 0; t += 4) {
-        const uint32_t i = (uint32_t)(t + a - 1);
-        uint4 x = ld16(at(d.off + 16 * i));
-        const uint32_t r = aad_len - 16 * i;
-        if (r < 16) x = keep_bytes(x, r);
-        w = gh.mulx(w, x);
+    {
+        auto aad_block = [&](int t) {
+            const uint32_t i = (uint32_t)(t + a - 1);
+            uint4 x = ld16(at(d.off + 16 * i));
+            const uint32_t r = aad_len - 16 * i;
+            return r < 16 ? keep_bytes(x, r) : x;
+        };
+        int t = (1 - a) + (((int)s - (1 - a)) & 3);
+        if (t <= 0) {
+            w = gh.rot(aad_block(t));
+            t += 4;
+        }
+        for (; t <= 0; t += 4) w = gh.mulx(w, aad_block(t));
     }
 
     // Round keys: scalar loads where they are used (the key record stays in the scalar cache) instead of 44 / 60 SGPRs
@@ -308,13 +317,16 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
             const uint32_t b = pay + 16 * (uint32_t)(t0 - 1);
             // The 64-byte segment that straddles two groups' ciphertext gets its two parts from stores a whole group
             // apart, and in between L2 had often written the first part back on its own (a second partial write of
-            // the segment).  So between interior groups the last 64 bytes (blocks k = 3) wait for the next group and
-            // go out right after its first 64.
+            // the segment).  So the last 64 bytes (blocks k = 3) of an interior group wait for the next group -- an
+            // interior one, or the tail group when it runs <= 3 blocks per lane (1200-B packets: 3) -- and go out
+            // with its stores.  (Holding them across a 4-block edge group's keystream, or group 0's across group 1's,
+            // pushed the edge path past the register budget: its GHASH state went to scratch memory.)
             st_payload(at(b), out[0]);
             if (held_ok) st_payload(at(b - 64), held);
 #pragma unroll
             for (int k = 1; k < NBG - 1; k++) st_payload(at(b + 64 * k), out[k]);
-            held_ok = interior(g + 1) && (g + 1 < G - 1 || tail_slots > 12);  // uniform: the next group is interior
+            held_ok = (interior(g + 1) && (g + 1 < G - 1 || tail_slots > 12)) || (g + 1 == G - 1 && tail_slots <= 12);
+            // (uniform)
             if (held_ok) held = out[NBG - 1];
             else st_payload(at(b + 64 * (NBG - 1)), out[NBG - 1]);
 #pragma unroll
@@ -335,6 +347,9 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
                                                         : (SEAL ? out[k] : in[k]);
                 if (full || part || lenslot) w = gh.mulx(w, x);
                 len_done = len_done || lenslot;
+            }
+            if constexpr (NBG <= 3) {  // the tail group: the last interior group's blocks k = 3
+                if (held_ok) st_payload(at(pay + 16 * (uint32_t)(t0 - 1) - 64), held);
             }
         }
         if (SEAL && g == 0) hp_early(out[0]);
@@ -419,7 +434,7 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
 
 // One workgroup per CU (grid = CUs) over an equal slice of the key-sorted packets (plan meta,
 // same single-key mode), 256 packets per pass.
-template <bool SEAL, int NR>
+template <bool SEAL, int NR, int WG = kQuadWG<NR>>
 __device__ __forceinline__ void quad_slices(const DevKey *__restrict__ keys, const qpp_pkt *__restrict__ descs,
                                             const uint32_t *__restrict__ perm, const WorkItem *__restrict__ work,
                                             const uint32_t *__restrict__ meta, uint8_t *__restrict__ arena,
@@ -456,7 +471,7 @@ __device__ __forceinline__ void quad_slices(const DevKey *__restrict__ keys, con
         const DevKey *__restrict__ key = keys + w.key;
         __syncthreads();  // every wave is done with the previous segment's tables
         quad_tables(key);
-        for (uint32_t t0 = lo; t0 < end; t0 += kQuadWG<NR> / 4) {
+        for (uint32_t t0 = lo; t0 < end; t0 += WG / 4) {
             const uint32_t t = t0 + q;
             const bool real = t < end;
             const uint32_t pi = one ? (real ? t : lo) : perm[real ? t : lo];
@@ -542,10 +557,11 @@ __device__ __forceinline__ uint32_t rx_class(uint4 kw, bool chacha) {
 }
 
 // AES: 10 or 14 when the live AES packet keys are all of one size (that instance alone: no registers spent on the
-// other), 0 for both sizes in one launch
-static_assert(kQuadWG<10> == kQuadWG<14>, "the fused receive runs both round counts in one launch");
+// other), 0 for both sizes in one launch (the launch's workgroup size: kQuadWG<10>, or kQuadWG<14> for 14 alone)
 template <int AES>
-__global__ __launch_bounds__(kQuadWG<10>) void aes_gcm_quad_rx_kernel(const DevKey *__restrict__ keys,
+constexpr int kRxWG = AES == 14 ? kQuadWG<14> : kQuadWG<10>;
+template <int AES>
+__global__ __launch_bounds__(kRxWG<AES>) void aes_gcm_quad_rx_kernel(const DevKey *__restrict__ keys,
                                                                  uint32_t key_cap, const qpp_rx_pkt *__restrict__ rx,
                                                                  uint32_t n, uint8_t *arena, qpp_pkt *descs_out,
                                                                  int8_t *status, uint32_t *scratch, uint32_t *perm,
@@ -688,8 +704,9 @@ __global__ __launch_bounds__(kQuadWG<10>) void aes_gcm_quad_rx_kernel(const DevK
     if (!rx_grid_sync(scratch, 3 * gridDim.x)) return bail();
     RX_TS(6);
     // D: open, key-sorted slices (tables per key segment, as a planned batch): the AES-128 packets, then the AES-256 ones
-    if constexpr (AES != 14) quad_slices<false, 10>(keys, descs_out, perm, work, meta, arena, nullptr, status, 0u, ~0u, 0u);
-    if constexpr (AES != 10) quad_slices<false, 14>(keys, descs_out, perm, work, meta, arena, nullptr, status, 0u, ~0u, 0u);
+    constexpr int WG = kRxWG<AES>;
+    if constexpr (AES != 14) quad_slices<false, 10, WG>(keys, descs_out, perm, work, meta, arena, nullptr, status, 0u, ~0u, 0u);
+    if constexpr (AES != 10) quad_slices<false, 14, WG>(keys, descs_out, perm, work, meta, arena, nullptr, status, 0u, ~0u, 0u);
 #if QPP_RX_TRACE
     RX_TS(7);
     if (threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1 || blockIdx.x == gridDim.x / 2))
@@ -719,7 +736,7 @@ hipError_t launch_aes_gcm_quad_rx(uint32_t aes, uint32_t grid, hipStream_t s, co
     const void *f = aes == 10   ? reinterpret_cast<const void *>(&aes_gcm_quad_rx_kernel<10>)
                     : aes == 14 ? reinterpret_cast<const void *>(&aes_gcm_quad_rx_kernel<14>)
                                 : reinterpret_cast<const void *>(&aes_gcm_quad_rx_kernel<0>);
-    return hipLaunchCooperativeKernel(f, dim3(grid), dim3(kQuadWG<10>), args, kLdsMax, s);
+    return hipLaunchCooperativeKernel(f, dim3(grid), dim3(aes == 14 ? kRxWG<14> : kRxWG<10>), args, kLdsMax, s);
 }
 
 // The quad-layout kernels behind launch_aes_gcm / launch_aes_gcm_single (aes_gcm.hip chooses).  single = 0xffffffff:

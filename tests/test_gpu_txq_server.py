@@ -3,8 +3,8 @@
 The queue's flushes are posted through a doorbell in pinned memory to a resident kernel instead of launched
 (quic/s2n-quic-platform/src/socket/io/tx.rs:204-268 flushes the GSO segments; endpoint/mod.rs:158 calls it per
 wakeup).  Every flushed packet must equal crypto::encrypt + crypto::protect of the oracle
-(quic/s2n-quic-core/src/crypto/packet_protection.rs), whatever path sealed it: the server, or the launched kernels
-that take FIPS-gated and ChaCha20-Poly1305 flushes.  The lifecycle cases cover what a resident kernel adds: the idle
+(quic/s2n-quic-core/src/crypto/packet_protection.rs), whatever path sealed it: the server (every suite; ChaCha20-Poly1305
+packets one wave each, chacha_wave.h), or the launched kernels that take FIPS-gated flushes.  The lifecycle cases cover what a resident kernel adds: the idle
 exit and restart, key installs between flushes (cached GHASH tables), a key-table growth and a context
 synchronisation while the server runs, and the queue's destruction with it running.
 """
@@ -70,7 +70,7 @@ def test_server_bursts_bit_exact(ctx, monkeypatch):
 
 def test_server_many_keys_both_sizes(ctx):
     """AES-128 and AES-256 keys interleaved, 700 packets of 1..1200 B in one flush (several items per workgroup,
-    key changes inside a workgroup), then a ChaCha20-Poly1305 packet in the next flush: launched path, same bytes"""
+    key changes inside a workgroup), then ChaCha20-Poly1305 packets among them in the next flush: the server too"""
     rng = np.random.default_rng(72)
     keys = [ctx.key(s, rng.integers(0, 256, qpp.HASH_LEN[s], dtype=np.uint8).tobytes()) for s in (1, 2, 1, 2, 1)]
     q = qpp.TxQueue(ctx, 700 * STRIDE, 700, persistent=True)
@@ -83,9 +83,45 @@ def test_server_many_keys_both_sizes(ctx):
     want = _fill(q, rng, keys[:2] + [ck], 90, largest + 701, largest + 700)
     q.flush()
     _check(q, want)
-    assert q.info()[:2] == (1, 1)
+    assert q.info()[:2] == (2, 0)
     q.close()
     for k in keys + [ck]:
+        k.free()
+
+
+@pytest.mark.parametrize("sizes", [(1000, 1200), (1, 3000)])
+def test_server_chacha_bursts_bit_exact(ctx, monkeypatch, sizes):
+    """64-packet ChaCha20-Poly1305 bursts (one connection's key; then three keys of all suites interleaved), 20 flushes
+    on one server launch, bit-exact against the oracle's encrypt + protect; ragged sizes 1..3000 B (one to four
+    64-block passes of the wave, the HP sample reaching into the tag)"""
+    monkeypatch.setenv("QPP_TXQ_SERVER_IDLE_MS", "4000")
+    rng = np.random.default_rng(78 + sizes[0])
+    ck = ctx.key(3, rng.integers(0, 256, 32, dtype=np.uint8).tobytes())
+    mixed = [ck, ctx.key(1, rng.integers(0, 256, 32, dtype=np.uint8).tobytes()),
+             ctx.key(2, rng.integers(0, 256, 48, dtype=np.uint8).tobytes())]
+    q = qpp.TxQueue(ctx, 64 * 3200, 64, persistent=True)
+    largest = int(rng.integers(0, 2**40))
+    for f in range(20):
+        keys = [ck] if f < 10 else mixed
+        want = []
+        for i in range(64):
+            k = keys[i % len(keys)]
+            pn = largest + 1 + 64 * f + i
+            trunc, pn_len = qpp.pn_truncate(pn, largest + 64 * f)
+            header = bytes([0x40 | (pn_len - 1)]) + rng.integers(0, 256, 16, dtype=np.uint8).tobytes()
+            payload = rng.integers(0, 256, int(rng.integers(max(sizes[0], 4 - pn_len), sizes[1])), dtype=np.uint8).tobytes()
+            pkt = header + trunc.to_bytes(pn_len, "big") + payload
+            off = i * 3200
+            q.ring[off:off + len(pkt)] = np.frombuffer(pkt, dtype=np.uint8)
+            q.push(k, pn, off, len(header), pn_len, len(payload))
+            kk, iv, hp = k.material()
+            want.append((off, orc.protect_packet(k.suite, kk, iv, hp, pn, header, pn_len, payload)[1]))
+        q.flush()
+        _check(q, want)
+    served, launched, starts = q.info()
+    assert (served, launched, starts) == (20, 0, 1)
+    q.close()
+    for k in mixed:
         k.free()
 
 

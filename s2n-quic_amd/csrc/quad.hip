@@ -48,9 +48,9 @@ using QPage = CtrPageQ4;
 __device__ __forceinline__ QAes make_qaes() { return AesQ4::make(); }
 __device__ __forceinline__ void build_qaes() { build_aes_tables_q4(kLdsAes); }
 template <int NR, int NB, int STRIDE>
-__device__ __forceinline__ void qkeystream(const QAes &a, const QPage &pg, const uint32_t *rk, uint32_t c0,
+__device__ __forceinline__ void qkeystream(const QAes &a, const QPage &pg, const uint4 *rkp, uint32_t c0,
                                            uint4 (&ks)[NB]) {
-    ctr_keystream_q4<NR, NB, STRIDE>(a, pg, rk, c0, ks);
+    ctr_keystream_q4<NR, NB, STRIDE>(a, pg, rkp, c0, ks);
 }
 #else
 using QAes = AesLds;
@@ -58,8 +58,14 @@ using QPage = CtrPage;
 __device__ __forceinline__ QAes make_qaes() { return make_aes(kLdsAes); }
 __device__ __forceinline__ void build_qaes() { build_aes_tables(kLdsAes); }
 template <int NR, int NB, int STRIDE>
-__device__ __forceinline__ void qkeystream(const QAes &a, const QPage &pg, const uint32_t *rk, uint32_t c0,
+__device__ __forceinline__ void qkeystream(const QAes &a, const QPage &pg, const uint4 *rkp, uint32_t c0,
                                            uint4 (&ks)[NB]) {
+    uint32_t rk[4 * (NR + 1)];
+#pragma unroll
+    for (int r = 0; r <= NR; r++) {
+        const uint4 v = rkp[r];
+        rk[4 * r] = v.x; rk[4 * r + 1] = v.y; rk[4 * r + 2] = v.z; rk[4 * r + 3] = v.w;
+    }
     ctr_keystream_inplace<NR, NB, STRIDE>(a, pg, rk, c0, ks);
 }
 #endif
@@ -205,24 +211,16 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
         for (; t <= 0; t += 4) w = gh.mulx(w, aad_block(t));
     }
 
-    // Round keys: scalar loads where they are used (the key record stays in the scalar cache) instead of 44 / 60 SGPRs
-    // held for the whole kernel, which pushed other uniform values into VGPR lanes (a v_readlane per use in the loop)
-    auto round_keys = [&](uint32_t (&k)[4 * (NR + 1)]) {
+    // Round keys: scalar loads where they are used (the key record stays in the scalar cache), through a pointer
+    // laundered per group so that no load is hoisted out of the group loop: held for the whole loop, 44 / 60 words
+    // exhausted the SGPRs and went to VGPRs (the keystream loads each round's words one round ahead)
+    auto round_keys = [&]() {
         uint64_t a = (uint64_t)key->rk;
         asm volatile("" : "+s"(a));  // reloaded here, not hoisted into SGPRs for the whole loop
-        const uint4 *p = (const uint4 *)a;
-#pragma unroll
-        for (int r = 0; r <= NR; r++) {
-            const uint4 v = p[r];
-            k[4 * r] = v.x; k[4 * r + 1] = v.y; k[4 * r + 2] = v.z; k[4 * r + 3] = v.w;
-        }
+        return (const uint4 *)a;
     };
     QPage pg;
-    {
-        uint32_t rk[4 * (NR + 1)];
-        round_keys(rk);
-        pg.build(aes, rk, n0, n1, n2, 0);
-    }
+    pg.build(aes, round_keys(), n0, n1, n2, 0);
     const int ngroups = has ? (m + 1 + 15) >> 4 : 0;  // counter slots 0 (J0) .. m
     const int G = (int)wave_max((uint32_t)ngroups);
     const int min_full = (int)__builtin_amdgcn_readfirstlane(wave_min(has ? (uint32_t)nfull : 0u));
@@ -269,8 +267,7 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
     auto group = [&](auto nbc, int g) {
         constexpr int NBG = decltype(nbc)::value;
         const bool inner = NBG == 4 && interior(g);  // uniform
-        uint32_t rk[4 * (NR + 1)];
-        round_keys(rk);
+        const uint4 *rkp = round_keys();
         const int t0 = 16 * g + (int)s;
         uint4 ks[NBG];
         const uint32_t c0 = (uint32_t)t0 + 1u;
@@ -281,11 +278,17 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
         if ((g & 15) != 15) {  // uniform: no lane's counters straddle a 256-block page
             if ((c0 >> 8) != pg.page) {
                 asm volatile("" : "+v"(m0), "+v"(m1), "+v"(m2));
-                pg.build(aes, rk, m0, m1, m2, c0 >> 8);
+                pg.build(aes, rkp, m0, m1, m2, c0 >> 8);
             }
-            qkeystream<NR, NBG, 4>(aes, pg, rk, c0, ks);
+            qkeystream<NR, NBG, 4>(aes, pg, rkp, c0, ks);
         } else {
             asm volatile("" : "+v"(m0), "+v"(m1), "+v"(m2));
+            uint32_t rk[4 * (NR + 1)];
+#pragma unroll
+            for (int r = 0; r <= NR; r++) {
+                const uint4 v = rkp[r];
+                rk[4 * r] = v.x; rk[4 * r + 1] = v.y; rk[4 * r + 2] = v.z; rk[4 * r + 3] = v.w;
+            }
             static_for<NBG>([&](auto kc) {
                 constexpr int k = decltype(kc)::value;
                 ks[k] = aes.encrypt<NR>(make_uint4(m0, m1, m2, bswap32(c0 + 4 * k)), rk);

@@ -2,7 +2,7 @@
 # crashed at exit in round 3 (run once after the ordered-teardown fix), and the PMC profile of the AesQ4 build
 set -o pipefail
 cd $GRAFT_REPO_ROOT; export TMPDIR=/tmp; o=gpurun_out/r04b; mkdir -p $o
-timeout -k 10 500 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > $o/pytest.log 2>&1; rc=$?
+timeout -k 10 500 python -u -m pytest ${R04B_TESTS:-tests} -m gpu -q --timeout 120 --timeout-method thread > $o/pytest.log 2>&1; rc=$?
 tail -3 $o/pytest.log
 [ $rc -eq 0 ] || exit 1
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $o/smoke.log 2>&1 && cat $o/smoke.log && \

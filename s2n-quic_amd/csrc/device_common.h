@@ -453,6 +453,14 @@ __device__ __forceinline__ void build_aes_tables_q4(uint32_t base) {
     }
 }
 
+// Round keys read through the constant address space (scalar loads into SGPRs; the key records are not written while
+// a kernel reads them).  The host pass of this code sees a plain pointer (it never runs there).
+#ifdef __HIP_DEVICE_COMPILE__
+typedef const __attribute__((address_space(4))) uint4 *RkPtr;
+#else
+typedef const uint4 *RkPtr;
+#endif
+
 // CtrPage in the AesQ4 convention (every constant rotated by 8 q; the counter byte x3 natural)
 struct CtrPageQ4 {
     uint32_t k0, k1, k2, k3;  // round-1 output (k0 without the varying slot-3 term)
@@ -460,9 +468,9 @@ struct CtrPageQ4 {
     uint32_t x3;              // rk[3] byte 3 (xored with the counter's low byte)
     uint32_t page;            // c >> 8 these constants belong to
 
-    // from round keys in memory (uniform pointer: scalar loads of rounds 0..2 only)
-    __device__ __forceinline__ void build(const AesQ4 &a, const uint4 *__restrict__ rkp, uint32_t n0, uint32_t n1,
-                                          uint32_t n2, uint32_t pg) {
+    // from round keys in memory (rounds 0..2 only; RK: a pointer type, e.g. into the constant address space)
+    template <typename RK>
+    __device__ __forceinline__ void build(const AesQ4 &a, RK rkp, uint32_t n0, uint32_t n1, uint32_t n2, uint32_t pg) {
         const uint4 r0 = rkp[0], r1 = rkp[1], r2 = rkp[2];
         const uint32_t rk[12] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w};
         build(a, rk, n0, n1, n2, pg);
@@ -495,15 +503,12 @@ struct CtrPageQ4 {
 };
 
 // ctr_keystream_inplace on AesQ4 (same unit order and pipeline; the round's 4 key words rotated once per round for
-// all NB blocks).  The round keys come from memory one round ahead (rkp: a uniform pointer, so scalar loads; round r's
-// words are requested at the start of round r - 1): 8 SGPRs in flight instead of 4 (NR + 1) held for the whole group
-// loop -- held, they exhausted the SGPRs and the compiler kept 40+ of them in VGPRs (the quad kernel's register
-// budget, i.e. its waves per SIMD).
+// all NB blocks).  Reads rk[12 ..] only (rounds 3..NR: rounds 1 and 2 are the page's).
 #ifndef QPP_Q4_DEPTH
 #define QPP_Q4_DEPTH 3  // units (4 lookups each) issued ahead of the one combined (<= NB - 1)
 #endif
 template <int NR, int NB, int STRIDE = 1>
-__device__ __forceinline__ void ctr_keystream_q4(const AesQ4 &a, const CtrPageQ4 &pg, const uint4 *__restrict__ rkp,
+__device__ __forceinline__ void ctr_keystream_q4(const AesQ4 &a, const CtrPageQ4 &pg, const uint32_t *__restrict__ rk,
                                                  uint32_t c0, uint4 (&ks)[NB]) {
     static_assert(NB >= 1 && NB <= 4, "pipeline depth NB - 1 lookups groups of 4 within the 15-read counter");
     constexpr int D = NB - 1 < QPP_Q4_DEPTH ? NB - 1 : QPP_Q4_DEPTH;
@@ -511,7 +516,6 @@ __device__ __forceinline__ void ctr_keystream_q4(const AesQ4 &a, const CtrPageQ4
     uint32_t st[NB][4];
     uint32_t nw[4];
     uint32_t kr[4];
-    uint4 kcur = rkp[3], knext = kcur;  // round r's key words, and round r + 1's in flight
     uint32_t ld[D + 1][4];
 #pragma unroll
     for (int j = 0; j < NB; j++) pg.two_rounds(a, c0 + STRIDE * j, st[j]);
@@ -529,14 +533,9 @@ __device__ __forceinline__ void ctr_keystream_q4(const AesQ4 &a, const CtrPageQ4
         constexpr int u = decltype(uc)::value;
         constexpr int r = 3 + u / (4 * NB), j = (u / 4) % NB, c = u % 4;
         const uint32_t *l = ld[u % (D + 1)];
-        if constexpr (u % (4 * NB) == 0) {  // the round's first unit: its keys in use, the next round's requested
-            if constexpr (r > 3) kcur = knext;
-            if constexpr (r < NR) knext = rkp[r + 1];
-            if constexpr (r < NR) {
-                kr[0] = a.rot(kcur.x); kr[1] = a.rot(kcur.y); kr[2] = a.rot(kcur.z); kr[3] = a.rot(kcur.w);
-            } else {
-                kr[0] = kcur.x; kr[1] = kcur.y; kr[2] = kcur.z; kr[3] = kcur.w;
-            }
+        if constexpr (u % (4 * NB) == 0) {  // the round's first unit: its key words (rotated but in the last round)
+#pragma unroll
+            for (int i = 0; i < 4; i++) kr[i] = r < NR ? a.rot(rk[4 * r + i]) : rk[4 * r + i];
         }
         if constexpr (r < NR) {
             nw[c] = AesQ4::comb(l[0], l[1], l[2], l[3], kr[c]);

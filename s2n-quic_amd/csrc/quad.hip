@@ -24,6 +24,8 @@
 //   [64K, 128K)  AES tables (AesQ4: T0..T3, 8 copies each, in the lower 128 B of 256 rows; AesLds: T0/T1 x 32)
 //   [128K, 160K) 4-bit GHASH tables of H^1..H^4 (Ghash4 layout, power e at 128K + 8K (e - 1))
 // While a key's tables are built, [64K, 72K) holds V_e[m] = H^e x^m (e = 1..4), before the AES tables overwrite it.
+#include <stdlib.h>
+
 #include "device_common.h"
 #include "ghash.h"
 
@@ -48,9 +50,16 @@ using QPage = CtrPageQ4;
 __device__ __forceinline__ QAes make_qaes() { return AesQ4::make(); }
 __device__ __forceinline__ void build_qaes() { build_aes_tables_q4(kLdsAes); }
 template <int NR, int NB, int STRIDE>
-__device__ __forceinline__ void qkeystream(const QAes &a, const QPage &pg, const uint4 *rkp, uint32_t c0,
+__device__ __forceinline__ void qkeystream(const QAes &a, const QPage &pg, RkPtr rkp, uint32_t c0,
                                            uint4 (&ks)[NB]) {
-    ctr_keystream_q4<NR, NB, STRIDE>(a, pg, rkp, c0, ks);
+    // rounds 3..NR only: 32 / 48 words at the group's start (the page build reads rounds 0..2 itself, when it runs)
+    uint32_t rk[4 * (NR + 1)];
+#pragma unroll
+    for (int r = 3; r <= NR; r++) {
+        const uint4 v = rkp[r];
+        rk[4 * r] = v.x; rk[4 * r + 1] = v.y; rk[4 * r + 2] = v.z; rk[4 * r + 3] = v.w;
+    }
+    ctr_keystream_q4<NR, NB, STRIDE>(a, pg, rk, c0, ks);
 }
 #else
 using QAes = AesLds;
@@ -58,7 +67,7 @@ using QPage = CtrPage;
 __device__ __forceinline__ QAes make_qaes() { return make_aes(kLdsAes); }
 __device__ __forceinline__ void build_qaes() { build_aes_tables(kLdsAes); }
 template <int NR, int NB, int STRIDE>
-__device__ __forceinline__ void qkeystream(const QAes &a, const QPage &pg, const uint4 *rkp, uint32_t c0,
+__device__ __forceinline__ void qkeystream(const QAes &a, const QPage &pg, RkPtr rkp, uint32_t c0,
                                            uint4 (&ks)[NB]) {
     uint32_t rk[4 * (NR + 1)];
 #pragma unroll
@@ -212,12 +221,15 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
     }
 
     // Round keys: scalar loads where they are used (the key record stays in the scalar cache), through a pointer
-    // laundered per group so that no load is hoisted out of the group loop: held for the whole loop, 44 / 60 words
-    // exhausted the SGPRs and went to VGPRs (the keystream loads each round's words one round ahead)
+    // laundered per group so that no load is hoisted out of the group loop (held for the whole loop, 44 / 60 words
+    // exhausted the SGPRs and went to VGPRs); a group's keystream loads rounds 3..NR, the page build rounds 0..2
     auto round_keys = [&]() {
         uint64_t a = (uint64_t)key->rk;
         asm volatile("" : "+s"(a));  // reloaded here, not hoisted into SGPRs for the whole loop
-        return (const uint4 *)a;
+        // Through the constant address space: a uniform load from a global pointer is a scalar load only when the
+        // compiler can prove no store of the kernel clobbers it, which the laundering hides -- the round keys were
+        // FLAT loads into 32-44 VGPRs (uniform values in vector registers, the register budget of the waves)
+        return (RkPtr)a;
     };
     QPage pg;
     pg.build(aes, round_keys(), n0, n1, n2, 0);
@@ -267,7 +279,7 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
     auto group = [&](auto nbc, int g) {
         constexpr int NBG = decltype(nbc)::value;
         const bool inner = NBG == 4 && interior(g);  // uniform
-        const uint4 *rkp = round_keys();
+        const RkPtr rkp = round_keys();
         const int t0 = 16 * g + (int)s;
         uint4 ks[NBG];
         const uint32_t c0 = (uint32_t)t0 + 1u;
@@ -739,7 +751,19 @@ hipError_t launch_aes_gcm_quad_rx(uint32_t aes, uint32_t grid, hipStream_t s, co
     const void *f = aes == 10   ? reinterpret_cast<const void *>(&aes_gcm_quad_rx_kernel<10>)
                     : aes == 14 ? reinterpret_cast<const void *>(&aes_gcm_quad_rx_kernel<14>)
                                 : reinterpret_cast<const void *>(&aes_gcm_quad_rx_kernel<0>);
-    return hipLaunchCooperativeKernel(f, dim3(grid), dim3(aes == 14 ? kRxWG<14> : kRxWG<10>), args, kLdsMax, s);
+    const dim3 block(aes == 14 ? kRxWG<14> : kRxWG<10>);
+    // A plain launch: the grid is at most the CUs the context's resident servers leave and a workgroup takes a whole
+    // CU's LDS, so on a device this context owns every workgroup is resident at once -- the guarantee the grid
+    // barriers need (and hipLaunchCooperativeKernel gives no more than that against another context's kernels; the
+    // barriers' timeout covers that case).  QPP_RX_COOP=1: the cooperative launch API instead (under rocprofv3 a
+    // process that had made cooperative launches crashed in exit(), after the profiler's finalization: round 3 and
+    // round 4, profiles/r04b).
+    static const bool coop = [] {
+        const char *e = getenv("QPP_RX_COOP");
+        return e && e[0] == '1';
+    }();
+    if (coop) return hipLaunchCooperativeKernel(f, dim3(grid), block, args, kLdsMax, s);
+    return hipLaunchKernel(f, dim3(grid), block, args, kLdsMax, s);
 }
 
 // The quad-layout kernels behind launch_aes_gcm / launch_aes_gcm_single (aes_gcm.hip chooses).  single = 0xffffffff:

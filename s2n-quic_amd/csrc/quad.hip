@@ -79,8 +79,12 @@ __device__ __forceinline__ void qkeystream(const QAes &a, const QPage &pg, RkPtr
 }
 #endif
 __device__ __forceinline__ uint4 ld_payload(const uint8_t *p) { return ld16(p); }
+#ifndef QPP_QUAD_NT
+#define QPP_QUAD_NT 1  // payload stores streaming (nt); 0: plain stores (write-traffic A/B)
+#endif
 __device__ __forceinline__ void st_payload(uint8_t *p, uint4 v) {
-    st16_nt(p, v);  // streaming: the sealed / opened bytes are not read again
+    if (QPP_QUAD_NT) st16_nt(p, v);  // streaming: the sealed / opened bytes are not read again
+    else st16(p, v);
 }
 template <int NR>
 constexpr int kQuadWG = NR == 10 ? QPP_QUAD_WG : QPP_QUAD_WG256;
@@ -332,16 +336,15 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
             const uint32_t b = pay + 16 * (uint32_t)(t0 - 1);
             // The 64-byte segment that straddles two groups' ciphertext gets its two parts from stores a whole group
             // apart, and in between L2 had often written the first part back on its own (a second partial write of
-            // the segment).  So the last 64 bytes (blocks k = 3) of an interior group wait for the next group -- an
-            // interior one, or the tail group when it runs <= 3 blocks per lane (1200-B packets: 3) -- and go out
-            // with its stores.  (Holding them across a 4-block edge group's keystream, or group 0's across group 1's,
-            // pushed the edge path past the register budget: its GHASH state went to scratch memory.)
+            // the segment).  So between interior groups the last 64 bytes (blocks k = 3) wait for the next group and
+            // go out right after its first 64.  (Holding them into the tail group as well measured no fewer HBM
+            // writes -- 1.473 vs 1.492 MB WRITE_SIZE per launch, profiles/r04d -- and holding group 0's across group
+            // 1's keystream pushed the edge path past the register budget: its GHASH state went to scratch memory.)
             st_payload(at(b), out[0]);
             if (held_ok) st_payload(at(b - 64), held);
 #pragma unroll
             for (int k = 1; k < NBG - 1; k++) st_payload(at(b + 64 * k), out[k]);
-            held_ok = (interior(g + 1) && (g + 1 < G - 1 || tail_slots > 12)) || (g + 1 == G - 1 && tail_slots <= 12);
-            // (uniform)
+            held_ok = interior(g + 1) && (g + 1 < G - 1 || tail_slots > 12);  // uniform: the next group is interior
             if (held_ok) held = out[NBG - 1];
             else st_payload(at(b + 64 * (NBG - 1)), out[NBG - 1]);
 #pragma unroll
@@ -362,9 +365,6 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
                                                         : (SEAL ? out[k] : in[k]);
                 if (full || part || lenslot) w = gh.mulx(w, x);
                 len_done = len_done || lenslot;
-            }
-            if constexpr (NBG <= 3) {  // the tail group: the last interior group's blocks k = 3
-                if (held_ok) st_payload(at(pay + 16 * (uint32_t)(t0 - 1) - 64), held);
             }
         }
         if (SEAL && g == 0) hp_early(out[0]);

@@ -30,7 +30,7 @@ import qpp  # noqa: E402
 
 qpp.lib()  # load the engine (and its HIP runtime) before anything else touches the GPU
 
-SUITES = {"aes128gcm": 1, "aes256gcm": 2, "chacha20poly1305": 3}
+SUITES = {"aes128gcm": 1, "aes256gcm": 2, "chacha20poly1305": 3, "mixed": 0}  # mixed: key i of suite 1 + i % 3
 WARMUP_MIN_S = 0.25  # see the warmup loop in main()
 METRIC = "GiB/s AEAD seal+open, device-resident, 1200 B packets at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s; 6.29 measured copy)
@@ -69,6 +69,20 @@ def aes_lds_cycles_per_packet(pt, aad, nr, hp=True):
 
 
 VALU_PEAK_PER_NS = 540.0  # wave-instructions/ns chip-wide for xor/add/alignbit/bitop3/perm/mul_lo (tools/ubench/issue.hip)
+
+
+def aes_valu_per_packet(pt, aad, nr):
+    """VALU wave-instructions aes_gcm_quad_kernel<seal> issues per packet: per wave-block (64 lane-slots: 16 packets x 4
+    lanes) of counter slots as in aes_lds_cycles_per_packet, plus a per-packet part (page build, AAD, HP on the quad,
+    final GHASH), calibrated on SQ_INSTS_VALU of the 1 Mi x 1200 B AES-128 seal (round 4, profiles/r04f: 402.7 per
+    packet at 76 counter slots); AES-256 scales the AES share (213 of the 322 per wave-block) by 14/10 rounds' lookups."""
+    m = (pt + 15) // 16
+    slots = m + 1
+    groups = -(-(slots + 1) // 16)
+    tail = slots + 1 - 16 * (groups - 1)
+    ctr = 16 * (groups - 1) + (12 if tail <= 12 else 16)
+    per_block = 322.0 if nr == 10 else 322.0 + 213.0 * (197.0 / 133.0 - 1.0)
+    return ctr * per_block / 64.0 + 20.3
 
 
 def chacha_valu_per_packet(pt):
@@ -200,10 +214,13 @@ def main():
     barrier, max_over_ranks = ctl.barrier, ctl.max
 
     suite = SUITES[args.suite]
+    if suite == 0 and args.mode not in ("device", "rx"):
+        raise SystemExit("--suite mixed: device and rx modes only")
     # QPP_SHARE_DEVICE=1: every rank on GPU 0 (rehearsing the torchrun path on a one-GPU box; never set by the driver)
     ctx = qpp.Context(0 if os.environ.get("QPP_SHARE_DEVICE") == "1" else local_rank)
     rng = np.random.default_rng(0x5eed0000 + 1)
-    keys = [ctx.key(suite, rng.integers(0, 256, qpp.HASH_LEN[suite], dtype=np.uint8).tobytes()) for _ in range(args.keys)]
+    key_suites = [suite or 1 + i % 3 for i in range(args.keys)]  # mixed: a server whose clients chose every suite
+    keys = [ctx.key(ks, rng.integers(0, 256, qpp.HASH_LEN[ks], dtype=np.uint8).tobytes()) for ks in key_suites]
     n, pt, aad = args.packets, args.pt, args.aad
     if args.mode == "keys":
         return keys_churn(args, ctx, suite, rank, world, barrier, max_over_ranks)
@@ -215,7 +232,7 @@ def main():
     sh["pn_base"] = args.pn_first
     descs, arena = qpp.make_batch(n, pt, [k.slot for k in keys], seed=sh["seed"], aad_len=aad, pn_base=sh["pn_base"],
                                   run=args.key_run, stride=args.stride or None)
-    flags = (0 if args.no_hp else qpp.HP_MASK_OUT) | (qpp.ONLY_CHACHA if suite == 3 else qpp.ONLY_AES)
+    flags = (0 if args.no_hp else qpp.HP_MASK_OUT) | (qpp.ONLY_CHACHA if suite == 3 else qpp.ONLY_AES if suite else 0)
     d_desc, d_mask, d_status = ctx.alloc(descs.nbytes), ctx.alloc(5 * n), ctx.alloc(n)
     d_desc.upload(descs)
     s = ctx.stream
@@ -293,7 +310,7 @@ def main():
             "scaling": "strong" if args.total_packets else "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic (seeded PCG64 payload bytes, 21 B short-header AAD, PN = base + i)",
             "config": {
-                "workload": (f"{qpp.SUITE_NAMES[suite]} seal(+HP mask)+open, " +
+                "workload": (f"{qpp.SUITE_NAMES[suite] if suite else 'mixed-suite'} seal(+HP mask)+open, " +
                              (f"{args.total_packets} x {pt} B packets split over {world} GPU(s), " if args.total_packets
                               else f"{n} x {pt} B packets per GPU, ") + f"{args.keys} key(s)" + (" (BASELINE configs[1])" if suite == 1 and pt == 1200 and
                                                      args.keys == 1 and n == 1 << 20 else "")),
@@ -305,7 +322,8 @@ def main():
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic["bytes"] if traffic else None,
                 "traffic_detail": traffic,
-                "kernel": ("chacha_burst_kernel<seal>" if suite == 3 and n <= burst_max else
+                "kernel": ("plan + aes_gcm_quad_kernel<seal> + chacha_kernel<seal>" if suite == 0 else
+                           "chacha_burst_kernel<seal>" if suite == 3 and n <= burst_max else
                            "chacha_kernel<seal>" if suite == 3 else
                            "aes_gcm_burst_kernel<seal>" if n <= burst_max else
                            "aes_gcm_quad_kernel<seal>" + (" + plan (per seal call)" if args.keys > 1 else "")),
@@ -320,16 +338,22 @@ def main():
                 "unit": "G wave-instructions/s", "frac": round(ins / (seal_avg / 1e3) / (VALU_PEAK_PER_NS * 1e9), 4),
                 "model": "bench.chacha_valu_per_packet (SQ_INSTS_VALU); peak measured by tools/ubench/issue.hip",
             }
-        if suite != 3 and n > burst_max:
-            # the quad kernel's own bound: the CU's LDS array (T-table + GHASH-table lookups), not HBM
-            cyc = n * aes_lds_cycles_per_packet(pt, aad, 10 if suite == 1 else 14)
+        if suite in (1, 2) and n > burst_max and args.keys * 1024 <= n:
+            # the quad kernel's own bounds: the CU's LDS array (T-table + GHASH-table lookups) and VALU issue, not HBM
+            nr = 10 if suite == 1 else 14
+            cyc = n * aes_lds_cycles_per_packet(pt, aad, nr)
+            ins = n * aes_valu_per_packet(pt, aad, nr)
             out["kernel_roofline"] = {
                 "bound": "lds", "achieved": round(cyc / (seal_avg / 1e3) / 1e9, 1), "peak": LDS_PEAK_CYCLES / 1e9,
                 "unit": "G LDS-array cycles/s", "frac": round(cyc / (seal_avg / 1e3) / LDS_PEAK_CYCLES, 4),
                 "model": "bench.aes_lds_cycles_per_packet (quad layout), checked against SQ_LDS_IDX_ACTIVE; "
                          "peak = 256 CUs x 2.4 GHz",
+                "valu": {"achieved": round(ins / (seal_avg / 1e3) / 1e9, 1), "peak": VALU_PEAK_PER_NS,
+                         "unit": "G wave-instructions/s", "frac": round(ins / (seal_avg / 1e3) / (VALU_PEAK_PER_NS * 1e9), 4),
+                         "model": "bench.aes_valu_per_packet, calibrated on SQ_INSTS_VALU; peak measured by "
+                                  "tools/ubench/issue.hip"},
             }
-        if world == 1 and not args.no_cpu:
+        if world == 1 and not args.no_cpu and suite:
             out["cpu_baseline"] = cpu_baseline(suite, pt, aad, args.cpu_seconds)
         print(json.dumps(out), flush=True)
     ctx.close()

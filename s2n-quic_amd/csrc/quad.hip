@@ -41,10 +41,8 @@ constexpr uint32_t kQLdsVe = 65536;    // V_e during the build
 #ifndef QPP_QUAD_WG256
 #define QPP_QUAD_WG256 768  // AES-256 (60 round-key words, 14 rounds of pipeline state)
 #endif
-#ifndef QPP_QUAD_Q4
-#define QPP_QUAD_Q4 1  // AES on four quarter-split T-tables (AesQ4); 0: two tables + rotl16 (AesLds)
-#endif
-#if QPP_QUAD_Q4
+// AES on four quarter-split T-tables (AesQ4, device_common.h; the two-table AesLds + rotl16 form measured 2 % slower
+// in the quad kernel, round 4, profiles/r04a)
 using QAes = AesQ4;
 using QPage = CtrPageQ4;
 __device__ __forceinline__ QAes make_qaes() { return AesQ4::make(); }
@@ -61,24 +59,10 @@ __device__ __forceinline__ void qkeystream(const QAes &a, const QPage &pg, RkPtr
     }
     ctr_keystream_q4<NR, NB, STRIDE>(a, pg, rk, c0, ks);
 }
-#else
-using QAes = AesLds;
-using QPage = CtrPage;
-__device__ __forceinline__ QAes make_qaes() { return make_aes(kLdsAes); }
-__device__ __forceinline__ void build_qaes() { build_aes_tables(kLdsAes); }
-template <int NR, int NB, int STRIDE>
-__device__ __forceinline__ void qkeystream(const QAes &a, const QPage &pg, RkPtr rkp, uint32_t c0,
-                                           uint4 (&ks)[NB]) {
-    uint32_t rk[4 * (NR + 1)];
-#pragma unroll
-    for (int r = 0; r <= NR; r++) {
-        const uint4 v = rkp[r];
-        rk[4 * r] = v.x; rk[4 * r + 1] = v.y; rk[4 * r + 2] = v.z; rk[4 * r + 3] = v.w;
-    }
-    ctr_keystream_inplace<NR, NB, STRIDE>(a, pg, rk, c0, ks);
-}
-#endif
 __device__ __forceinline__ uint4 ld_payload(const uint8_t *p) { return ld16(p); }
+#ifndef QPP_QUAD_PREFETCH
+#define QPP_QUAD_PREFETCH 1  // interior groups load the next interior group's payload before hashing their own
+#endif
 #ifndef QPP_QUAD_NT
 #define QPP_QUAD_NT 1  // payload stores streaming (nt); 0: plain stores (write-traffic A/B)
 #endif
@@ -279,6 +263,9 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
         hp_done = true;
     };
 
+    // the next interior group's payload, loaded while this group hashes (QPP_QUAD_PREFETCH)
+    uint4 pre[4] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
+    bool pre_ok = false;  // (uniform)
     // one group: slots t = 16 g + 4 k + s, k < NBG; slot t holds counter t + 1 and ciphertext block t - 1
     auto group = [&](auto nbc, int g) {
         constexpr int NBG = decltype(nbc)::value;
@@ -310,13 +297,13 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
                 ks[k] = aes.encrypt<NR>(make_uint4(m0, m1, m2, bswap32(c0 + 4 * k)), rk);
             });
         }
-        // payload loads after the keystream: held across the AES pipeline they cost 16 VGPRs at its peak (spills at
-        // 128); the other 3 waves of the SIMD cover their latency
+        // payload: an interior group's was loaded while the previous group hashed (QPP_QUAD_PREFETCH), else it is loaded
+        // after the keystream
         uint4 in[NBG];
         if (inner) {
             const uint32_t b = pay + 16 * (uint32_t)(t0 - 1);
 #pragma unroll
-            for (int k = 0; k < NBG; k++) in[k] = ld_payload(at(b + 64 * k));
+            for (int k = 0; k < NBG; k++) in[k] = pre_ok ? pre[k < 4 ? k : 0] : ld_payload(at(b + 64 * k));
         } else {
 #pragma unroll
             for (int k = 0; k < NBG; k++) {
@@ -347,6 +334,14 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
             held_ok = interior(g + 1) && (g + 1 < G - 1 || tail_slots > 12);  // uniform: the next group is interior
             if (held_ok) held = out[NBG - 1];
             else st_payload(at(b + 64 * (NBG - 1)), out[NBG - 1]);
+            // The next interior group's payload now: its latency passes under this group's GHASH and the next
+            // keystream instead of stalling the wave right after that keystream (round 4: with the round keys out of
+            // the VGPRs the 16 registers fit)
+            pre_ok = QPP_QUAD_PREFETCH && held_ok;
+            if (pre_ok) {
+#pragma unroll
+                for (int k = 0; k < 4; k++) pre[k] = ld_payload(at(b + 256 + 64 * k));
+            }
 #pragma unroll
             for (int k = 0; k < NBG; k++) w = gh.mulx(w, SEAL ? out[k] : in[k]);
         } else {

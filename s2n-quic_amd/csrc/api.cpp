@@ -191,6 +191,8 @@ uint32_t servers_cu(const qpp_ctx *ctx);
 // CUs a full-chip kernel (one workgroup per CU) should size its grid for: those of running servers are taken
 uint32_t cu_avail(const qpp_ctx *ctx) {
     const uint32_t r = servers_cu(ctx);
+    static const bool dbg = getenv("QPP_DEBUG_CU") != nullptr;
+    if (dbg) fprintf(stderr, "qpp cu_avail: n_cu %u servers %zu cu taken %u\n", ctx->n_cu, ctx->servers.size(), r);
     return ctx->n_cu > r ? ctx->n_cu - r : 1u;
 }
 // hipFree / hipHostFree wait for every stream of the device, a running server's too -- and a server only ends on its
@@ -2365,7 +2367,14 @@ int qpp_txq_create_persistent(qpp_ctx *ctx, size_t ring_bytes, size_t max_packet
         return QPP_DEVICE_ERROR;
     q->v_sdesc = (qpp_pkt *)v;
     memset(q->h_sdesc, 0, sizeof(qpp_pkt) * max_packets * W);
-    if (bad(hipStreamCreateWithFlags(&q->srv_stream, hipStreamNonBlocking), "txq server stream"))
+    // The server's stream at the device's greatest priority: the runtime maps streams onto at most GPU_MAX_HW_QUEUES
+    // hardware queues per priority level, round-robin, and a kernel queued behind a persistent one on the same hardware
+    // queue waits for its idle exit -- found by tests/test_gpu_txrx.py: after another context's streams had come and
+    // gone, the context's batch stream shared the server's queue and its seal started 30 s late.  A priority level of
+    // its own keeps the servers off the batch streams' queues (at most GPU_MAX_HW_QUEUES servers per process).
+    int prio_least = 0, prio_greatest = 0;
+    if (bad(hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest), "stream priorities") ||
+        bad(hipStreamCreateWithPriority(&q->srv_stream, hipStreamNonBlocking, prio_greatest), "txq server stream"))
         return QPP_DEVICE_ERROR;
     uint32_t wgs = 16, idle_ms = 200;
     if (const char *e = getenv("QPP_TXQ_SERVER_WGS")) wgs = (uint32_t)strtoul(e, nullptr, 10);

@@ -61,7 +61,7 @@ __device__ __forceinline__ void qkeystream(const QAes &a, const QPage &pg, RkPtr
 }
 __device__ __forceinline__ uint4 ld_payload(const uint8_t *p) { return ld16(p); }
 #ifndef QPP_QUAD_PREFETCH
-#define QPP_QUAD_PREFETCH 1  // interior groups load the next interior group's payload before hashing their own
+#define QPP_QUAD_PREFETCH 0  // 1: interior groups load the next interior group's payload before hashing their own (A/B)
 #endif
 #ifndef QPP_QUAD_NT
 #define QPP_QUAD_NT 1  // payload stores streaming (nt); 0: plain stores (write-traffic A/B)
@@ -264,7 +264,8 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
     };
 
     // the next interior group's payload, loaded while this group hashes (QPP_QUAD_PREFETCH)
-    uint4 pre[4] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
+    // (four scalars, not an array: an array written under a condition in the group lambda stayed in scratch memory)
+    uint4 pre0 = make_uint4(0, 0, 0, 0), pre1 = pre0, pre2 = pre0, pre3 = pre0;
     bool pre_ok = false;  // (uniform)
     // one group: slots t = 16 g + 4 k + s, k < NBG; slot t holds counter t + 1 and ciphertext block t - 1
     auto group = [&](auto nbc, int g) {
@@ -303,7 +304,8 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
         if (inner) {
             const uint32_t b = pay + 16 * (uint32_t)(t0 - 1);
 #pragma unroll
-            for (int k = 0; k < NBG; k++) in[k] = pre_ok ? pre[k < 4 ? k : 0] : ld_payload(at(b + 64 * k));
+            for (int k = 0; k < NBG; k++)
+                in[k] = pre_ok ? (k == 0 ? pre0 : k == 1 ? pre1 : k == 2 ? pre2 : pre3) : ld_payload(at(b + 64 * k));
         } else {
 #pragma unroll
             for (int k = 0; k < NBG; k++) {
@@ -339,8 +341,10 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
             // the VGPRs the 16 registers fit)
             pre_ok = QPP_QUAD_PREFETCH && held_ok;
             if (pre_ok) {
-#pragma unroll
-                for (int k = 0; k < 4; k++) pre[k] = ld_payload(at(b + 256 + 64 * k));
+                pre0 = ld_payload(at(b + 256));
+                pre1 = ld_payload(at(b + 320));
+                pre2 = ld_payload(at(b + 384));
+                pre3 = ld_payload(at(b + 448));
             }
 #pragma unroll
             for (int k = 0; k < NBG; k++) w = gh.mulx(w, SEAL ? out[k] : in[k]);

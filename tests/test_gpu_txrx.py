@@ -122,16 +122,24 @@ def test_tx_and_rx_with_resident_server(monkeypatch):
 
         flush()  # the server is resident from here on
         starts = q.info()[2]
+        trail = []  # (step, server launches so far, seconds since the first flush)
+        t_0 = time.perf_counter()
+        note = lambda what: trail.append((what, q.info()[2], round(time.perf_counter() - t_0, 3)))
         ctx.seal_batch(d_desc, n, d_arena, d_mask, d_status, qpp.HP_MASK_OUT)  # asynchronous: runs beside the flushes
+        note("seal_batch")
         flush()
+        note("flush 2")
         ctx.unprotect_open_batch(d_rx, nrx, d_rxa, d_out, d_rst)  # same stream: after the seal
+        note("unprotect_open_batch")
         flush()
+        note("flush 3")
         ctx.sync()
         flush()
+        note("flush 4")
         # the same server launch sealed every flush beside the batches (checked before the slow oracle work below: a
         # queue idle for a quarter of QPP_TXQ_SERVER_IDLE_MS restarts its server on the next flush, by design)
         served, launched, starts_now = q.info()
-        assert launched == 0 and starts_now == starts, "the server was stopped while the batches ran"
+        assert launched == 0 and starts_now == starts, f"the server was stopped while the batches ran: {trail}"
         sealed, masks = d_arena.download(), d_mask.download()
         assert (d_status.download(dtype=np.int8) == 0).all()
         assert orc.check_full_seal(okeys, slots, descs, arena, sealed, masks, qpp.HP_MASK_OUT) == n  # every packet

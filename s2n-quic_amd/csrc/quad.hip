@@ -268,7 +268,7 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
     uint4 pre0 = make_uint4(0, 0, 0, 0), pre1 = pre0, pre2 = pre0, pre3 = pre0;
     bool pre_ok = false;  // (uniform)
     // one group: slots t = 16 g + 4 k + s, k < NBG; slot t holds counter t + 1 and ciphertext block t - 1
-    auto group = [&](auto nbc, int g) {
+    auto group = [&](auto nbc, int g) __attribute__((always_inline)) {
         constexpr int NBG = decltype(nbc)::value;
         const bool inner = NBG == 4 && interior(g);  // uniform
         const RkPtr rkp = round_keys();
@@ -303,9 +303,14 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
         uint4 in[NBG];
         if (inner) {
             const uint32_t b = pay + 16 * (uint32_t)(t0 - 1);
+            if constexpr (NBG == 4) {
+                if (pre_ok) {
+                    in[0] = pre0; in[1] = pre1; in[2] = pre2; in[3] = pre3;
+                } else {
 #pragma unroll
-            for (int k = 0; k < NBG; k++)
-                in[k] = pre_ok ? (k == 0 ? pre0 : k == 1 ? pre1 : k == 2 ? pre2 : pre3) : ld_payload(at(b + 64 * k));
+                    for (int k = 0; k < NBG; k++) in[k] = ld_payload(at(b + 64 * k));
+                }
+            }
         } else {
 #pragma unroll
             for (int k = 0; k < NBG; k++) {
@@ -340,11 +345,14 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
             // keystream instead of stalling the wave right after that keystream (round 4: with the round keys out of
             // the VGPRs the 16 registers fit)
             pre_ok = QPP_QUAD_PREFETCH && held_ok;
-            if (pre_ok) {
-                pre0 = ld_payload(at(b + 256));
-                pre1 = ld_payload(at(b + 320));
-                pre2 = ld_payload(at(b + 384));
-                pre3 = ld_payload(at(b + 448));
+            if constexpr (QPP_QUAD_PREFETCH != 0) {
+                // (loaded unconditionally, clamped inside the packet when no interior group follows: a conditionally
+                // assigned set of registers was kept in scratch memory by the compiler)
+                const uint32_t lim = pay + len - 16u, bn = b + 256u;
+                pre0 = ld_payload(at(min(bn, lim)));
+                pre1 = ld_payload(at(min(bn + 64u, lim)));
+                pre2 = ld_payload(at(min(bn + 128u, lim)));
+                pre3 = ld_payload(at(min(bn + 192u, lim)));
             }
 #pragma unroll
             for (int k = 0; k < NBG; k++) w = gh.mulx(w, SEAL ? out[k] : in[k]);

@@ -60,9 +60,6 @@ __device__ __forceinline__ void qkeystream(const QAes &a, const QPage &pg, RkPtr
     ctr_keystream_q4<NR, NB, STRIDE>(a, pg, rk, c0, ks);
 }
 __device__ __forceinline__ uint4 ld_payload(const uint8_t *p) { return ld16(p); }
-#ifndef QPP_QUAD_PREFETCH
-#define QPP_QUAD_PREFETCH 0  // 1: interior groups load the next interior group's payload before hashing their own (A/B)
-#endif
 #ifndef QPP_QUAD_NT
 #define QPP_QUAD_NT 1  // payload stores streaming (nt); 0: plain stores (write-traffic A/B)
 #endif
@@ -263,10 +260,6 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
         hp_done = true;
     };
 
-    // the next interior group's payload, loaded while this group hashes (QPP_QUAD_PREFETCH)
-    // (four scalars, not an array: an array written under a condition in the group lambda stayed in scratch memory)
-    uint4 pre0 = make_uint4(0, 0, 0, 0), pre1 = pre0, pre2 = pre0, pre3 = pre0;
-    bool pre_ok = false;  // (uniform)
     // one group: slots t = 16 g + 4 k + s, k < NBG; slot t holds counter t + 1 and ciphertext block t - 1
     auto group = [&](auto nbc, int g) __attribute__((always_inline)) {
         constexpr int NBG = decltype(nbc)::value;
@@ -298,19 +291,13 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
                 ks[k] = aes.encrypt<NR>(make_uint4(m0, m1, m2, bswap32(c0 + 4 * k)), rk);
             });
         }
-        // payload: an interior group's was loaded while the previous group hashed (QPP_QUAD_PREFETCH), else it is loaded
-        // after the keystream
+        // payload after the keystream (loading the next interior group's payload while this group hashes measured 8 %
+        // slower: 1.248 vs 1.152 ms seal, 8 VGPRs spilled, profiles/r04h_ab)
         uint4 in[NBG];
         if (inner) {
             const uint32_t b = pay + 16 * (uint32_t)(t0 - 1);
-            if constexpr (NBG == 4) {
-                if (pre_ok) {
-                    in[0] = pre0; in[1] = pre1; in[2] = pre2; in[3] = pre3;
-                } else {
 #pragma unroll
-                    for (int k = 0; k < NBG; k++) in[k] = ld_payload(at(b + 64 * k));
-                }
-            }
+            for (int k = 0; k < NBG; k++) in[k] = ld_payload(at(b + 64 * k));
         } else {
 #pragma unroll
             for (int k = 0; k < NBG; k++) {
@@ -341,19 +328,6 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
             held_ok = interior(g + 1) && (g + 1 < G - 1 || tail_slots > 12);  // uniform: the next group is interior
             if (held_ok) held = out[NBG - 1];
             else st_payload(at(b + 64 * (NBG - 1)), out[NBG - 1]);
-            // The next interior group's payload now: its latency passes under this group's GHASH and the next
-            // keystream instead of stalling the wave right after that keystream (round 4: with the round keys out of
-            // the VGPRs the 16 registers fit)
-            pre_ok = QPP_QUAD_PREFETCH && held_ok;
-            if constexpr (QPP_QUAD_PREFETCH != 0) {
-                // (loaded unconditionally, clamped inside the packet when no interior group follows: a conditionally
-                // assigned set of registers was kept in scratch memory by the compiler)
-                const uint32_t lim = pay + len - 16u, bn = b + 256u;
-                pre0 = ld_payload(at(min(bn, lim)));
-                pre1 = ld_payload(at(min(bn + 64u, lim)));
-                pre2 = ld_payload(at(min(bn + 128u, lim)));
-                pre3 = ld_payload(at(min(bn + 192u, lim)));
-            }
 #pragma unroll
             for (int k = 0; k < NBG; k++) w = gh.mulx(w, SEAL ? out[k] : in[k]);
         } else {

@@ -199,6 +199,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-hp", action="store_true", help="seal without the HP mask (diagnostic)")
     ap.add_argument("--no-check", action="store_true", help="skip the warmup open-status check (diagnostic builds)")
+    ap.add_argument("--no-server", action="store_true", help="--mode packet: one launch per call (no packet server)")
     args = ap.parse_args()
 
     rank, world, local_rank = multigpu.env_rank()
@@ -703,30 +704,36 @@ def txq_bursts(args, ctx, keys, rank, world, max_over_ranks, burst=64):
     ctx.close()
 
 
-def per_packet(args, ctx, keys, rank, world, max_over_ranks, calls=300):
+def per_packet(args, ctx, keys, rank, world, max_over_ranks, calls=2000):
     """The trait-shaped per-packet face (Key::encrypt -> qpp_seal, Key::decrypt -> qpp_open): one packet per call,
-    as quic/s2n-quic-transport calls it today.  Reports the median call latency (zero-copy, one launch per call)."""
+    as quic/s2n-quic-transport calls it today.  Reports the median call latency, timed around each call in C
+    (tools/txqdrive.c packet_latency), through the context's packet server (qpp_ctx_set_packet_server; --no-server:
+    one launch per call)."""
     rng = np.random.default_rng(10)
     hdr = bytes([0x43]) + bytes(args.aad - 1)
     pt = rng.integers(0, 256, args.pt, dtype=np.uint8).tobytes()
     k = keys[0]
-    ts, to = [], []
-    for i in range(args.warmup + calls):
-        t0 = time.perf_counter()
-        ct = k.encrypt(i, hdr, pt)
-        t1 = time.perf_counter()
-        if k.decrypt(i, hdr, ct) != pt:
-            raise SystemExit("per-packet round trip failed")
-        t2 = time.perf_counter()
-        if i >= args.warmup:
-            ts.append(t1 - t0)
-            to.append(t2 - t1)
-    t = max_over_ranks(float(np.median(ts)))
+    if args.no_server:
+        ctx.set_packet_server(False)
+    drv = ctypes.CDLL(os.path.join(ROOT, "tools", "libtxqdrive.so")).packet_latency
+    drv.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t,
+                    ctypes.c_size_t, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
+    n = args.warmup + calls
+    ts, to = np.zeros(n), np.zeros(n)
+    rc = drv(k.handle, hdr, len(hdr), pt, len(pt), n, 0, ts.ctypes.data, to.ctypes.data)
+    if rc:
+        raise SystemExit(f"per-packet driver failed: {rc}")
+    ts, to = ts[args.warmup:], to[args.warmup:]
+    t = max_over_ranks(float(np.median(ts)) * 1e-6)
+    calls_srv, starts = ctx.packet_server_info()
     if rank == 0:
         print(json.dumps({
-            "metric": f"per-packet Key::encrypt latency ({args.pt} B, qpp_seal), median", "value": round(1e6 * t, 1),
+            "metric": f"per-packet Key::encrypt latency ({args.pt} B, qpp_seal), median", "value": round(1e6 * t, 2),
             "unit": "us", "higher_is_better": False, "n_gpus": world, "suite": args.suite,
-            "decrypt_us": round(1e6 * float(np.median(to)), 1), "calls": calls,
+            "p10_us": round(float(np.percentile(ts, 10)), 2), "p90_us": round(float(np.percentile(ts, 90)), 2),
+            "decrypt_us": round(float(np.median(to)), 2), "decrypt_p90_us": round(float(np.percentile(to, 90)), 2),
+            "calls": calls, "path": "launch per call" if args.no_server else "packet server",
+            "server_calls_starts": [calls_srv, starts], "driver": "tools/txqdrive.c packet_latency (timed in C)",
         }), flush=True)
     ctx.close()
 

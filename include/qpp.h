@@ -67,6 +67,14 @@ int qpp_ctx_synchronize(qpp_ctx *ctx);
  * (latency: a 64-packet GSO burst); larger ones by the throughput kernels (quad / wave-item; qpp_ctx_set_aes_kernel).  ChaCha20-Poly1305 batches switch
  * at max_packets / 4.  0 = never one wave per packet.  Outputs are identical either way. */
 int qpp_ctx_set_burst_max(qpp_ctx *ctx, size_t max_packets);
+/* Per-packet calls (qpp_seal, qpp_seal_scatter, qpp_open, qpp_dc_*) through the context's packet server (on by default;
+ * env QPP_PACKET_SERVER=0 turns it off): a persistent kernel of 4 workgroups, started by the first such call, that
+ * seals / opens one packet posted through pinned memory without a kernel launch, and leaves after
+ * QPP_TXQ_SERVER_IDLE_MS (200) without a call.  Packets of more than 16 KiB (header + payload + tag) and FIPS seals
+ * take the launched path.  Outputs are identical either way.  on = 0 stops and frees the server. */
+int qpp_ctx_set_packet_server(qpp_ctx *ctx, int on);
+/* Per-packet calls the packet server has taken so far, and its kernel launches (it leaves when idle). */
+int qpp_ctx_packet_server_info(const qpp_ctx *ctx, uint64_t *calls, uint64_t *starts);
 /* AES-GCM batches larger than burst_max: the quad kernel (four lanes per packet, one workgroup per CU over a slice of
  * the key-sorted packets) serves batches with at least 1024 packets per live AES key, the wave-item kernel (one key
  * per 64-packet wave) batches with fewer (many keys, few packets each: key-update churn).  This forces one of them

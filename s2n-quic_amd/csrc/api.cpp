@@ -133,6 +133,11 @@ struct qpp_ctx {
     int kstage_next = 0;
     HostPipe *pipe = nullptr;
     std::vector<qpp_txq *> servers;  // transmit queues with a persistent server kernel (qpp_txq_create_persistent)
+    // The packet server: a persistent queue of the context's own (kPktWgs workgroups, created on the first per-packet
+    // call) through which qpp_seal / qpp_open run without a kernel launch; qpp_ctx_set_packet_server, QPP_PACKET_SERVER
+    qpp_txq *pkt_q = nullptr;
+    bool pkt_server = true;
+    uint64_t pkt_calls = 0, pkt_starts = 0;  // qpp_ctx_packet_server_info (starts of freed servers in pkt_starts)
     uint32_t *d_connmap = nullptr;    // qpp_ctx_set_conn_keys: connection -> key slot (device)
     size_t connmap_cap = 0, connmap_n = 0;
     // its pinned staging copy (the caller's array is pageable: HIP does not promise an async copy from it has read it
@@ -188,11 +193,14 @@ bool fail(qpp_ctx *ctx, hipError_t e, const char *what) {
 int servers_stop(qpp_ctx *ctx);
 int servers_quiesce(qpp_ctx *ctx);
 uint32_t servers_cu(const qpp_ctx *ctx);
+// Key::encrypt / Key::decrypt of one packet through the context's packet server (defined with qpp_txq below);
+// *handled = false: the call is not one the server takes (FIPS seal, packet over kPktRing, server off) -- launch it
+int packet_server_run(const qpp_key *k, bool seal, uint64_t pn, const uint8_t *header, size_t header_len,
+                      const uint8_t *payload, size_t payload_len, uint8_t *out, uint8_t *tag_out, int8_t *status_out,
+                      bool *handled);
 // CUs a full-chip kernel (one workgroup per CU) should size its grid for: those of running servers are taken
 uint32_t cu_avail(const qpp_ctx *ctx) {
     const uint32_t r = servers_cu(ctx);
-    static const bool dbg = getenv("QPP_DEBUG_CU") != nullptr;
-    if (dbg) fprintf(stderr, "qpp cu_avail: n_cu %u servers %zu cu taken %u\n", ctx->n_cu, ctx->servers.size(), r);
     return ctx->n_cu > r ? ctx->n_cu - r : 1u;
 }
 // hipFree / hipHostFree wait for every stream of the device, a running server's too -- and a server only ends on its
@@ -677,6 +685,9 @@ int run_one(const qpp_key *k, bool seal, uint64_t pn, const uint8_t *header, siz
     qpp_ctx *ctx = k->ctx;
     if (header_len > 0xffff || payload_len > 0xffff) return QPP_INTERNAL_ERROR;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
+    bool handled = false;
+    RC_TRY(packet_server_run(k, seal, pn, header, header_len, payload, payload_len, out, tag_out, status_out, &handled));
+    if (handled) return QPP_OK;
     const size_t total = kOnePkt + 16 + header_len + payload_len + 16;
     RC_TRY(ensure_stage(ctx, total));
     RC_TRY(flush_keys(ctx));
@@ -901,6 +912,7 @@ int qpp_ctx_create(int device, qpp_ctx **out) {
     ctx->device = device;
     ctx->n_cu = (uint32_t)prop.multiProcessorCount;
     if (const char *e = getenv("QPP_BURST_MAX")) ctx->burst_max = (uint32_t)strtoul(e, nullptr, 10);
+    if (const char *e = getenv("QPP_PACKET_SERVER")) ctx->pkt_server = strcmp(e, "0") != 0;
     if (const char *e = getenv("QPP_AES_KERNEL"))
         ctx->aes_kernel = !strcmp(e, "quad") || !strcmp(e, "lane") ? QPP_AES_KERNEL_QUAD
                         : !strcmp(e, "wave")                     ? QPP_AES_KERNEL_WAVE
@@ -956,6 +968,8 @@ int qpp_ctx_set_burst_max(qpp_ctx *ctx, size_t max_packets) {
 void qpp_ctx_destroy(qpp_ctx *ctx) {
     if (!ctx) return;
     hipSetDevice(ctx->device);
+    qpp_txq_destroy(ctx->pkt_q);
+    ctx->pkt_q = nullptr;
     if (ctx->d_keys) flush_retire(ctx);  // pending zeroizations, while the table and the stream states still exist
     servers_stop(ctx);
     hipDeviceSynchronize();
@@ -1901,7 +1915,11 @@ int qpp_txq_create(qpp_ctx *ctx, size_t ring_bytes, size_t max_packets, qpp_txq 
     return qpp_txq_create_async(ctx, ring_bytes, max_packets, 1, out);
 }
 
-int qpp_txq_create_async(qpp_ctx *ctx, size_t ring_bytes, size_t max_packets, size_t in_flight, qpp_txq **out) {
+}  // extern "C"
+
+// ring_flags: hipHostMallocDefault (launched flushes), or coherent + mapped (a server's ring, see txq_make_server)
+static int txq_create(qpp_ctx *ctx, size_t ring_bytes, size_t max_packets, size_t in_flight, unsigned ring_flags,
+                      qpp_txq **out) {
     if (!ctx || !out || !ring_bytes || !max_packets || ring_bytes > UINT32_MAX || max_packets > UINT32_MAX ||
         !in_flight || in_flight > 64)
         return QPP_INTERNAL_ERROR;
@@ -1917,7 +1935,7 @@ int qpp_txq_create_async(qpp_ctx *ctx, size_t ring_bytes, size_t max_packets, si
         qpp_txq_destroy(q);
         return true;
     };
-    if (bad(hipHostMalloc(&q->h_ring, ring_bytes, hipHostMallocDefault), "txq ring") ||
+    if (bad(hipHostMalloc(&q->h_ring, ring_bytes, ring_flags), "txq ring") ||
         bad(hipMalloc(&q->d_ring, ring_bytes), "txq ring") || bad(hipHostGetDevicePointer(&v, q->h_ring, 0), "ring view"))
         return QPP_DEVICE_ERROR;
     q->v_ring = (uint8_t *)v;
@@ -1955,6 +1973,12 @@ int qpp_txq_create_async(qpp_ctx *ctx, size_t ring_bytes, size_t max_packets, si
     memset(q->h_ring, 0, ring_bytes);
     *out = q;
     return QPP_OK;
+}
+
+extern "C" {
+
+int qpp_txq_create_async(qpp_ctx *ctx, size_t ring_bytes, size_t max_packets, size_t in_flight, qpp_txq **out) {
+    return txq_create(ctx, ring_bytes, max_packets, in_flight, hipHostMallocDefault, out);
 }
 
 void qpp_txq_destroy(qpp_txq *q) {
@@ -2118,10 +2142,10 @@ static void txq_reset_batch(qpp_txq *q) {
 // Persistent queue: posts slots[cur]'s packets (any suite, no FIPS key live) to the server.  The descriptors are copied
 // into the server's plan (key-sorted, items of <= one packet per wave), so the slot is free for the next pushes at
 // once; the previous posted flush must be done first (its plan is being rewritten).
-static int srv_submit(qpp_txq *q) {
+// Before a post: the previous one done, key records installed since visible to the server (and a new key epoch), the
+// server on the current key table and not possibly leaving on its idle timeout
+static int srv_prepare(qpp_txq *q, std::chrono::steady_clock::time_point now) {
     qpp_ctx *ctx = q->ctx;
-    TxqSlot &sl = q->slots[q->cur];
-    const uint32_t n = (uint32_t)q->count;
     RC_TRY(srv_wait(q, q->srv_posted));
     if (ctx->key_gen != q->srv_key_gen) {
         // records installed since the last post are in HBM before the server reads them (host wait, only after key
@@ -2132,8 +2156,16 @@ static int srv_submit(qpp_txq *q) {
     }
     if (q->srv_running && q->srv_keys != ctx->d_keys) RC_TRY(srv_stop(q));  // (grow_keys stops servers already)
     // a server idle for long may be leaving on its own timeout: never post to it (part of it could miss the flush)
-    const auto now = std::chrono::steady_clock::now();
     if (q->srv_running && now - q->srv_last_post > q->srv_host_idle) RC_TRY(srv_stop(q));
+    return QPP_OK;
+}
+
+static int srv_submit(qpp_txq *q) {
+    qpp_ctx *ctx = q->ctx;
+    TxqSlot &sl = q->slots[q->cur];
+    const uint32_t n = (uint32_t)q->count;
+    const auto now = std::chrono::steady_clock::now();
+    RC_TRY(srv_prepare(q, now));
     const uint32_t W = kTxsWaves;
     std::vector<uint32_t> &ord = q->order;
     ord.resize(n);
@@ -2329,9 +2361,16 @@ int qpp_txq_wait(qpp_txq *q, uint64_t ticket) {
     return txq_refused(*sl);
 }
 
-int qpp_txq_create_persistent(qpp_ctx *ctx, size_t ring_bytes, size_t max_packets, qpp_txq **out) {
+}  // extern "C"
+
+// A queue with a persistent server of `wgs` workgroups.  Fine-grained (coherent) pinned memory for everything the
+// server touches: polled over PCIe while the host writes it, and read and written by a kernel that does not end
+// between flushes (no cached copy may outlive a flush) -- the ring too.
+static int txq_create_server(qpp_ctx *ctx, size_t ring_bytes, size_t max_packets, uint32_t wgs, uint32_t idle_ms,
+                             qpp_txq **out) {
     if (!ctx || !out || max_packets >= kTxsItemsMask) return QPP_INTERNAL_ERROR;
-    RC_TRY(qpp_txq_create_async(ctx, ring_bytes, max_packets, 1, out));
+    const unsigned fl = hipHostMallocCoherent | hipHostMallocMapped;
+    RC_TRY(txq_create(ctx, ring_bytes, max_packets, 1, fl, out));
     qpp_txq *q = *out;
     auto bad = [&](hipError_t e, const char *what) {
         if (!fail(ctx, e, what)) return false;
@@ -2342,17 +2381,7 @@ int qpp_txq_create_persistent(qpp_ctx *ctx, size_t ring_bytes, size_t max_packet
     q->persistent = true;
     ctx->servers.push_back(q);
     const size_t W = kTxsWaves;
-    // fine-grained (coherent) pinned memory: polled by the server over PCIe while the host writes it, and read and
-    // written by a kernel that does not end between flushes (no cached copy may outlive a flush) -- the ring too
-    const unsigned fl = hipHostMallocCoherent | hipHostMallocMapped;
     void *v = nullptr;
-    hipHostFree(q->h_ring);
-    q->h_ring = nullptr;
-    if (bad(hipHostMalloc(&q->h_ring, ring_bytes, fl), "txq server ring") ||
-        bad(hipHostGetDevicePointer(&v, q->h_ring, 0), "ring view"))
-        return QPP_DEVICE_ERROR;
-    q->v_ring = (uint8_t *)v;
-    memset(q->h_ring, 0, ring_bytes);
     if (bad(hipHostMalloc(&q->h_mail, sizeof(TxsMail), fl), "txq server mailbox") ||
         bad(hipHostGetDevicePointer(&v, q->h_mail, 0), "mailbox view"))
         return QPP_DEVICE_ERROR;
@@ -2376,9 +2405,6 @@ int qpp_txq_create_persistent(qpp_ctx *ctx, size_t ring_bytes, size_t max_packet
     if (bad(hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest), "stream priorities") ||
         bad(hipStreamCreateWithPriority(&q->srv_stream, hipStreamNonBlocking, prio_greatest), "txq server stream"))
         return QPP_DEVICE_ERROR;
-    uint32_t wgs = 16, idle_ms = 200;
-    if (const char *e = getenv("QPP_TXQ_SERVER_WGS")) wgs = (uint32_t)strtoul(e, nullptr, 10);
-    if (const char *e = getenv("QPP_TXQ_SERVER_IDLE_MS")) idle_ms = (uint32_t)strtoul(e, nullptr, 10);
     q->srv_wgs = std::max(1u, std::min(wgs, ctx->n_cu));
     if (bad(hipHostMalloc(&q->h_slots, sizeof(TxsSlot) * q->srv_wgs, fl), "txq server slots") ||
         bad(hipHostGetDevicePointer(&v, q->h_slots, 0), "slots view"))
@@ -2389,6 +2415,19 @@ int qpp_txq_create_persistent(qpp_ctx *ctx, size_t ring_bytes, size_t max_packet
     q->srv_idle_ticks = idle_ms * 100000u;  // s_memrealtime: 100 MHz
     q->srv_host_idle = std::chrono::microseconds(250u * idle_ms);
     return QPP_OK;
+}
+
+static uint32_t srv_idle_ms() {
+    const char *e = getenv("QPP_TXQ_SERVER_IDLE_MS");
+    return e ? (uint32_t)strtoul(e, nullptr, 10) : 200u;
+}
+
+extern "C" {
+
+int qpp_txq_create_persistent(qpp_ctx *ctx, size_t ring_bytes, size_t max_packets, qpp_txq **out) {
+    uint32_t wgs = 16;
+    if (const char *e = getenv("QPP_TXQ_SERVER_WGS")) wgs = (uint32_t)strtoul(e, nullptr, 10);
+    return txq_create_server(ctx, ring_bytes, max_packets, wgs, srv_idle_ms(), out);
 }
 
 int qpp_txq_server_time(const qpp_txq *q, double *us) {
@@ -2418,6 +2457,98 @@ int qpp_txq_flush(qpp_txq *q) {
     uint64_t t = 0;
     RC_TRY(qpp_txq_flush_async(q, &t));
     return qpp_txq_wait(q, t);
+}
+
+}  // extern "C"
+
+namespace {
+
+// Key::encrypt / Key::decrypt (crypto/src/packet_protection.rs; cipher_suite.rs:86-160) of one packet through the
+// context's packet server: the header and payload (and the tag, to open) are copied into its pinned ring, posted as
+// one work item to workgroup slot % kPktWgs (so a connection's sealer and opener keep their GHASH tables in different
+// workgroups' LDS), sealed without header protection or opened in place there, and copied back.  No launch, no
+// runtime call: the cost is the post's PCIe round trip, the packet's own read / AES / GHASH / write chain and the copies.
+constexpr size_t kPktRing = 16384;  // header + payload + tag; longer packets take the launched path
+constexpr uint32_t kPktWgs = 4;
+int packet_server_run(const qpp_key *k, bool seal, uint64_t pn, const uint8_t *header, size_t header_len,
+                      const uint8_t *payload, size_t payload_len, uint8_t *out, uint8_t *tag_out, int8_t *status_out,
+                      bool *handled) {
+    qpp_ctx *ctx = k->ctx;
+    *handled = false;
+    const DevKey &rec = ctx->h_keys[k->slot];
+    const size_t total = header_len + payload_len + 16;
+    // FIPS seals keep the launched path (its nonce-order gate)
+    if (!ctx->pkt_server || (seal && rec.fips) || total > kPktRing) return QPP_OK;
+    if (!ctx->pkt_q) RC_TRY(txq_create_server(ctx, kPktRing, 1, kPktWgs, srv_idle_ms(), &ctx->pkt_q));
+    qpp_txq *q = ctx->pkt_q;
+    RC_TRY(flush_keys(ctx));
+    const auto now = std::chrono::steady_clock::now();
+    RC_TRY(srv_prepare(q, now));
+    uint8_t *r = q->h_ring;
+    if (header_len) memcpy(r, header, header_len);
+    if (payload_len) memcpy(r + header_len, payload, payload_len);
+    if (!seal) memcpy(r + header_len + payload_len, tag_out, 16);
+    RC_TRY(srv_start(q));
+    q->srv_seq = srv_next(q->srv_seq);
+    const uint32_t seq = q->srv_seq, wg = k->slot % q->srv_wgs;
+    const uint32_t word = (q->srv_epoch << 24) | q->srv_wgs;  // item b for workgroup b; all but one empty
+    for (uint32_t b = 0; b < q->srv_wgs; b++) {
+        TxsSlot &sl = q->h_slots[b];
+        sl.word = word;
+        if (b == wg) {
+            sl.status[0] = (int8_t)QPP_INTERNAL_ERROR;  // (stays so if the record is not live as planned)
+            TxsSlotDesc &sd = sl.desc[0];
+            sd.pn = pn;
+            sd.key_idx = k->slot;
+            __atomic_store_n(&sd.tag0, seq, __ATOMIC_RELEASE);
+            sd.off = 0;
+            sd.lens = (uint32_t)header_len | (uint32_t)payload_len << 16;
+            sd.misc = (uint32_t)(seal ? kTxsPktNoHp : kTxsPktOpen) << 8;
+            __atomic_store_n(&sd.tag1, seq, __ATOMIC_RELEASE);
+        }
+        sl.it_key = b == wg ? k->slot : 0u;
+        sl.it_count = b == wg ? 1u : 0u;
+        sl.it_nr = b == wg ? rec.nr : 0u;
+        __atomic_store_n(&sl.it_tag, seq, __ATOMIC_RELEASE);
+        __atomic_store_n(&sl.seq, seq, __ATOMIC_RELEASE);
+    }
+    q->srv_last_post = now;
+    q->srv_posted = seq;
+    q->srv_first = q->srv_last = 0;  // (no ticket: nothing of the transmit-queue API refers to this post)
+    q->n_server++;
+    ctx->pkt_calls++;
+    RC_TRY(srv_wait(q, seq));
+    *status_out = __atomic_load_n(&q->h_slots[wg].status[0], __ATOMIC_ACQUIRE);
+    *handled = true;
+    if (!(seal && *status_out != QPP_OK)) {  // (a refused seal leaves the caller's buffer untouched)
+        memcpy(out, r + header_len, payload_len);
+        if (seal) memcpy(tag_out, r + header_len + payload_len, 16);
+    }
+    secure_zero(r, total);
+    return QPP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int qpp_ctx_set_packet_server(qpp_ctx *ctx, int on) {
+    if (!ctx) return QPP_INTERNAL_ERROR;
+    ctx->pkt_server = on != 0;
+    if (!on && ctx->pkt_q) {
+        HIP_TRY(ctx, hipSetDevice(ctx->device));
+        ctx->pkt_starts += ctx->pkt_q->n_starts;
+        qpp_txq_destroy(ctx->pkt_q);
+        ctx->pkt_q = nullptr;
+    }
+    return QPP_OK;
+}
+
+int qpp_ctx_packet_server_info(const qpp_ctx *ctx, uint64_t *calls, uint64_t *starts) {
+    if (!ctx) return QPP_INTERNAL_ERROR;
+    if (calls) *calls = ctx->pkt_calls;
+    if (starts) *starts = ctx->pkt_starts + (ctx->pkt_q ? ctx->pkt_q->n_starts : 0);
+    return QPP_OK;
 }
 
 }  // extern "C"

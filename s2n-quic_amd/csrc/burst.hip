@@ -370,20 +370,28 @@ __global__ __launch_bounds__(kBurstWG) void aes_gcm_burst_kernel(const DevKey *_
 //   a new one first (api.cpp srv_submit), so a flush is seen by every workgroup or by none (the idle exit is for a
 //   host that went away).
 
+// A transmit flush's packet is sealed and header-protected; a per-packet request (kTxsPktNoHp: Key::encrypt,
+// kTxsPktOpen: Key::decrypt) is sealed without header protection or opened, its status into the slot (status[wave]).
 template <int NR>
 __device__ __forceinline__ void txs_item(const AesLds &aes, const DevKey *key, const qpp_pkt &d,
-                                         uint32_t wave, uint32_t count, uint8_t *ring) {
+                                         uint32_t wave, uint32_t count, uint8_t *ring, int8_t *status) {
     uint32_t rk[4 * (NR + 1)];
 #pragma unroll
     for (int i = 0; i < 4 * (NR + 1); i++) rk[i] = __builtin_amdgcn_readfirstlane(lds_ld32(kTxsKey + 16 + 4 * i));
-    if (wave < count && !(d.flags & QPP_PKT_SKIP))
-        burst_packet<NR, true, true>(aes, key, rk, d, 0, ring, nullptr, nullptr, QPP_HP_APPLY);
+    if (wave < count && !(d.flags & QPP_PKT_SKIP)) {
+        if (d.flags & kTxsPktOpen)
+            burst_packet<NR, false, true>(aes, key, rk, d, wave, ring, nullptr, status, 0);
+        else if (d.flags & kTxsPktNoHp)
+            burst_packet<NR, true, true>(aes, key, rk, d, wave, ring, nullptr, status, 0);
+        else
+            burst_packet<NR, true, true>(aes, key, rk, d, 0, ring, nullptr, nullptr, QPP_HP_APPLY);
+    }
 }
 
 // A ChaCha20-Poly1305 work item (cipher_suite.rs:270-284): one wave per packet (chacha_wave_packet, the burst kernel's
 // code), the key and HP key from the LDS copy, the header protected in place
 __device__ __forceinline__ void txs_item_chacha(const qpp_pkt &d, uint32_t wave, uint32_t count, uint8_t *ring,
-                                                uint32_t lane) {
+                                                int8_t *status, uint32_t lane) {
     uint32_t k[8], hk[8];
 #pragma unroll
     for (int i = 0; i < 8; i++) {
@@ -393,8 +401,14 @@ __device__ __forceinline__ void txs_item_chacha(const qpp_pkt &d, uint32_t wave,
     // Iv::nonce (src/iv.rs:27-39)
     const uint32_t n0 = lds_ld32(kTxsKey), n1 = lds_ld32(kTxsKey + 4) ^ bswap32((uint32_t)(d.pn >> 32)),
                    n2 = lds_ld32(kTxsKey + 8) ^ bswap32((uint32_t)d.pn);
-    if (wave < count && !(d.flags & QPP_PKT_SKIP))
-        chacha_wave_packet<true>(k, n0, n1, n2, hk, d, ring, nullptr, nullptr, QPP_HP_APPLY, lane);
+    if (wave < count && !(d.flags & QPP_PKT_SKIP)) {
+        if (d.flags & kTxsPktOpen)
+            chacha_wave_packet<false>(k, n0, n1, n2, hk, d, ring, nullptr, status + wave, 0, lane);
+        else if (d.flags & kTxsPktNoHp)
+            chacha_wave_packet<true>(k, n0, n1, n2, hk, d, ring, nullptr, status + wave, 0, lane);
+        else
+            chacha_wave_packet<true>(k, n0, n1, n2, hk, d, ring, nullptr, nullptr, QPP_HP_APPLY, lane);
+    }
 }
 
 // one 16-byte chunk of the slot (lane < kTxsPollLanes), in ONE load past every cache (sc0 sc1: the host writes it;
@@ -509,6 +523,7 @@ __global__ __launch_bounds__(kBurstWG) void txq_server_kernel(const DevKey *keys
             const WorkItem w = first ? w0 : items_v[it];
             const qpp_pkt d = first ? d0 : sdesc_v[it * kBurstWaves + wave];
             const DevKey *key = keys_v + w.key;
+            if (w.count == 0) continue;  // (a per-packet request posts one packet to one workgroup, none to the others)
             if (w.key != cached) {  // uniform
                 __syncthreads();  // every wave is done with the previous key's tables
                 // iv | rk | hp_rk: 124 consecutive words of the record (DevKey: iv at word 4), then its header
@@ -524,9 +539,10 @@ __global__ __launch_bounds__(kBurstWG) void txq_server_kernel(const DevKey *keys
             const uint32_t k_suite = lds_ld32(kTxsKeyHdr), k_nr = lds_ld32(kTxsKeyHdr + 4),
                            k_live = lds_ld32(kTxsKeyHdr + 12);
             if (k_live == 1 && k_nr == w.nr) {
-                if (w.nr == 10) txs_item<10>(aes, key, d, wave, w.count, ring);
-                else if (w.nr == 14) txs_item<14>(aes, key, d, wave, w.count, ring);
-                else if (k_suite == QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256) txs_item_chacha(d, wave, w.count, ring, lane);
+                if (w.nr == 10) txs_item<10>(aes, key, d, wave, w.count, ring, slot->status);
+                else if (w.nr == 14) txs_item<14>(aes, key, d, wave, w.count, ring, slot->status);
+                else if (k_suite == QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256)
+                    txs_item_chacha(d, wave, w.count, ring, slot->status, lane);
             }
         }
         // completion: this workgroup's ring stores reach the host before its done word

@@ -151,6 +151,10 @@ hipError_t launch_aes_gcm_burst(bool seal, const DevKey *keys, const qpp_pkt *de
 constexpr uint32_t kTxsWaves = 8;  // server workgroup = 8 waves, one packet per wave per work item
 constexpr uint32_t kTxsItemsMask = 0xffffffu;
 constexpr uint32_t kTxsStop = 0xffffffu;
+// Descriptor flags of the per-packet requests (qpp_seal / qpp_open through the context's packet server, api.cpp
+// run_one_server): never set by the transport (qpp_txq_push_descs refuses any flag)
+constexpr uint8_t kTxsPktNoHp = 0x40;  // seal without header protection (Key::encrypt), status written
+constexpr uint8_t kTxsPktOpen = 0x80;  // open (Key::decrypt), status written
 // Every 16-byte chunk carries the flush's seq as its last word (the host stores it after the chunk's other words):
 // the server reads each chunk with ONE 16-byte load, so a chunk whose tag matches is wholly this flush's.  (With the
 // tag in only one chunk of a descriptor, a poll could combine a stale first half -- the previous flush's pn, key and
@@ -170,7 +174,8 @@ struct alignas(64) TxsSlot {
     uint32_t it_key, it_count, it_nr, it_tag;  // this workgroup's first work item (count 0: none)
     TxsSlotDesc desc[kTxsWaves];
     alignas(64) uint32_t done;  // written by the server: the seq whose packets this workgroup has sealed
-    uint32_t pad2[15];
+    int8_t status[kTxsWaves];   // per-packet requests (kTxsPktOpen / kTxsPktNoHp): wave q's packet status, before done
+    uint32_t pad2[13];
 };
 static_assert(sizeof(TxsSlot) == 384 && offsetof(TxsSlot, desc) == 32 && offsetof(TxsSlot, done) == 320, "TxsSlot");
 constexpr uint32_t kTxsPollLanes = 18;  // 16-byte chunks of [seq .. desc[7]] = 288 bytes

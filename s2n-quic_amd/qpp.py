@@ -63,6 +63,7 @@ EXPORTS = [
     "qpp_header_key_new", "qpp_header_key_new_raw", "qpp_header_key_free", "qpp_header_key_slot",
     "qpp_header_key_suite", "qpp_header_key_sample_len", "qpp_header_key_mask", "qpp_host_batch_submit",
     "qpp_host_batch_query", "qpp_host_batch_wait", "qpp_ctx_set_host_pipe", "qpp_ctx_set_fips", "qpp_key_fips",
+    "qpp_ctx_set_packet_server", "qpp_ctx_packet_server_info",
 ]
 OP_SEAL, OP_OPEN = 0x1, 0x2
 
@@ -160,6 +161,8 @@ def lib():
             "qpp_txq_pending": (sz, [vp]),
             "qpp_memcpy_d2d": (ctypes.c_int, [vp, vp, vp, sz, vp]),
             "qpp_ctx_set_burst_max": (ctypes.c_int, [vp, sz]),
+            "qpp_ctx_set_packet_server": (ctypes.c_int, [vp, ctypes.c_int]),
+            "qpp_ctx_packet_server_info": (ctypes.c_int, [vp, ctypes.POINTER(u64), ctypes.POINTER(u64)]),
             "qpp_dc_key_new": (ctypes.c_int, [vp, ctypes.c_int, vp, sz, vp, ctypes.POINTER(vp)]),
             "qpp_dc_seal": (ctypes.c_int, [vp, u64, vp, sz, vp, sz, vp, sz]),
             "qpp_dc_open": (ctypes.c_int, [vp, ctypes.c_int, u64, vp, sz, vp, vp, sz, vp, sz]),
@@ -274,6 +277,17 @@ class Context:
     def set_burst_max(self, max_packets):
         """AES batches of <= max_packets run one wave per packet (burst kernel); 0 = always lane per packet."""
         self._check(lib().qpp_ctx_set_burst_max(self.handle, int(max_packets)), "set_burst_max")
+
+    def set_packet_server(self, on=True):
+        """Per-packet seal / open through the context's resident packet server (default on) or one launch per call."""
+        self._check(lib().qpp_ctx_set_packet_server(self.handle, int(bool(on))), "set_packet_server")
+
+    def packet_server_info(self):
+        """(per-packet calls the packet server took, its kernel launches)"""
+        calls, starts = ctypes.c_uint64(), ctypes.c_uint64()
+        self._check(lib().qpp_ctx_packet_server_info(self.handle, ctypes.byref(calls), ctypes.byref(starts)),
+                    "packet_server_info")
+        return calls.value, starts.value
 
     def set_aes_kernel(self, kernel):
         """AES_KERNEL_AUTO / _QUAD / _WAVE for batches above burst_max (identical outputs; A/B and tests)."""

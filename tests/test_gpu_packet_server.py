@@ -1,0 +1,109 @@
+"""Per-packet Key::encrypt / Key::decrypt (crypto/src/cipher_suite.rs:86-160, the packet_protection.rs trait face)
+through the context's packet server (api.cpp packet_server_run; burst.hip txq_server_kernel, kTxsPktNoHp /
+kTxsPktOpen items): bit-exact against the oracle and against the launched path, for every suite, header and payload
+lengths from empty to the server's 16 KiB ring, tampered tags, keys spread over the server's workgroups, the server
+stopped and restarted between calls, FIPS seals and long packets on the launched path."""
+import time
+
+import numpy as np
+import pytest
+
+import _oracle as orc
+import qpp
+
+pytestmark = pytest.mark.gpu
+
+SUITES = (1, 2, 3)  # AES-128-GCM, AES-256-GCM, ChaCha20-Poly1305
+
+
+def _lengths(rng):
+    return [0, 1, 15, 16, 17, 63, 64, 65, 1000, 1184, 1200, 1452, 4096, 16384 - 64 - 16] + \
+        [int(x) for x in rng.integers(0, 3000, 10)]
+
+
+@pytest.mark.parametrize("suite", SUITES)
+def test_server_seal_open_bit_exact(suite):
+    rng = np.random.default_rng(7100 + suite)
+    ctx = qpp.Context(0)
+    try:
+        keys = [ctx.key(suite, rng.integers(0, 256, qpp.HASH_LEN[suite], dtype=np.uint8).tobytes())
+                for _ in range(6)]  # slots over all 4 server workgroups, two sharing one (key switches in its LDS)
+        for i, ln in enumerate(_lengths(rng)):
+            k = keys[i % len(keys)]
+            kk, iv, _ = k.material()
+            pn = int(rng.integers(0, 2**62))
+            header = rng.integers(0, 256, int(rng.integers(1, 64)), dtype=np.uint8).tobytes()
+            payload = rng.integers(0, 256, ln, dtype=np.uint8).tobytes()
+            want = b"".join(orc.seal(suite, kk, orc.nonce(iv, pn), header, payload))
+            got = k.encrypt(pn, header, payload)
+            assert got == want, (suite, ln)
+            assert k.decrypt(pn, header, got) == payload
+            bad = bytearray(got)
+            bad[int(rng.integers(0, len(bad)))] ^= 0x10
+            with pytest.raises(qpp.DecryptError):
+                k.decrypt(pn, header, bytes(bad))
+        served, starts = ctx.packet_server_info()
+        assert served >= 3 * len(_lengths(rng)) and starts >= 1
+    finally:
+        ctx.close()
+
+
+def test_server_matches_launched_path():
+    rng = np.random.default_rng(7200)
+    on, off = qpp.Context(0), qpp.Context(0)
+    try:
+        off.set_packet_server(False)
+        for suite in SUITES:
+            secret = rng.integers(0, 256, qpp.HASH_LEN[suite], dtype=np.uint8).tobytes()
+            a, b = on.key(suite, secret), off.key(suite, secret)
+            for ln in (0, 5, 300, 1200, 3000):
+                pn = int(rng.integers(0, 2**40))
+                header = rng.integers(0, 256, 21, dtype=np.uint8).tobytes()
+                payload = rng.integers(0, 256, ln, dtype=np.uint8).tobytes()
+                ct = a.encrypt(pn, header, payload)
+                assert ct == b.encrypt(pn, header, payload)
+                assert a.decrypt(pn, header, ct) == b.decrypt(pn, header, ct) == payload
+        assert on.packet_server_info()[0] > 0 and off.packet_server_info() == (0, 0)
+    finally:
+        on.close()
+        off.close()
+
+
+def test_server_restarts_and_long_packets(monkeypatch):
+    """the server leaves on its idle time and is stopped by a free (hipFree waits for every stream); the next call
+    restarts it.  A packet over the
+    ring (16 KiB) and a FIPS seal take the launched path, identical bytes."""
+    monkeypatch.setenv("QPP_TXQ_SERVER_IDLE_MS", "20")
+    rng = np.random.default_rng(7300)
+    ctx = qpp.Context(0)
+    try:
+        k = ctx.key(1, rng.integers(0, 256, 32, dtype=np.uint8).tobytes())
+        kk, iv, _ = k.material()
+        header = bytes(21)
+
+        def one(pn, ln):
+            payload = rng.integers(0, 256, ln, dtype=np.uint8).tobytes()
+            ct = k.encrypt(pn, header, payload)
+            assert ct == b"".join(orc.seal(1, kk, orc.nonce(iv, pn), header, payload))
+            assert k.decrypt(pn, header, ct) == payload
+
+        one(1, 1200)
+        s0 = ctx.packet_server_info()[1]
+        time.sleep(0.1)  # past the idle time: the server left
+        one(2, 1200)
+        ctx.alloc(4096).free()  # a free stops the context's servers
+        one(3, 1200)
+        assert ctx.packet_server_info()[1] >= s0 + 2
+        served = ctx.packet_server_info()[0]
+        one(4, 20000)  # over the ring: launched
+        assert ctx.packet_server_info()[0] == served
+        ctx.set_fips(True)
+        f = ctx.key(1, rng.integers(0, 256, 32, dtype=np.uint8).tobytes())
+        fk, fiv, _ = f.material()
+        payload = bytes(range(200))
+        assert f.encrypt(10, header, payload) == b"".join(orc.seal(1, fk, orc.nonce(fiv, 10), header, payload))
+        assert ctx.packet_server_info()[0] == served  # FIPS seal: launched (nonce-order gate)
+        with pytest.raises(qpp.QppError):
+            f.encrypt(10, header, payload)  # the same packet number again: refused
+    finally:
+        ctx.close()

@@ -5,3 +5,8 @@ export QPP_LIB=ab/sT.so
 timeout -k 10 120 python tools/diag/server_trace.py 1 1200 2>&1 | tee $o/trace_1.txt && \
 timeout -k 10 120 python tools/diag/server_trace.py 64 1200 2>&1 | tee $o/trace_64.txt && \
 timeout -k 10 120 python tools/diag/server_trace.py 1 100 2>&1 | tee $o/trace_1_100.txt
+# the 300-B row on each AES kernel
+for kern in quad wave; do
+  QPP_LIB= QPP_AES_KERNEL=$kern timeout -k 10 120 python bench.py --pt 300 --packets 4194304 --no-cpu > $o/c4_300_$kern.json 2> $o/c4_300_$kern.err || exit 1
+  echo "$kern: $(head -c 400 $o/c4_300_$kern.json)"
+done

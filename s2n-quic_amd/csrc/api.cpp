@@ -198,6 +198,8 @@ uint32_t servers_cu(const qpp_ctx *ctx);
 int packet_server_run(const qpp_key *k, bool seal, uint64_t pn, const uint8_t *header, size_t header_len,
                       const uint8_t *payload, size_t payload_len, uint8_t *out, uint8_t *tag_out, int8_t *status_out,
                       bool *handled);
+// HeaderKey::*_header_protection_mask of one sample through the packet server (*handled = false: server off)
+int packet_server_mask(qpp_ctx *ctx, uint32_t slot, const uint8_t *sample, uint8_t mask[5], bool *handled);
 // CUs a full-chip kernel (one workgroup per CU) should size its grid for: those of running servers are taken
 uint32_t cu_avail(const qpp_ctx *ctx) {
     const uint32_t r = servers_cu(ctx);
@@ -750,6 +752,9 @@ int run_one(const qpp_key *k, bool seal, uint64_t pn, const uint8_t *header, siz
 // descriptor @0, sample @64 (+4), mask @96.
 int mask_one(qpp_ctx *ctx, uint32_t slot, const uint8_t *sample, uint8_t mask[5]) {
     HIP_TRY(ctx, hipSetDevice(ctx->device));
+    bool handled = false;
+    RC_TRY(packet_server_mask(ctx, slot, sample, mask, &handled));
+    if (handled) return QPP_OK;
     RC_TRY(ensure_stage(ctx, 128));
     RC_TRY(flush_keys(ctx));
     StreamState *st = nullptr;
@@ -2470,6 +2475,49 @@ namespace {
 // runtime call: the cost is the post's PCIe round trip, the packet's own read / AES / GHASH / write chain and the copies.
 constexpr size_t kPktRing = 16384;  // header + payload + tag; longer packets take the launched path
 constexpr uint32_t kPktWgs = 4;
+
+// Posts one work item of one packet (ring offset 0) to workgroup wg of the packet server -- every other workgroup an
+// empty item -- and waits for it.  The slot's status byte is preset to INTERNAL_ERROR (left so if the record is not
+// what the item names).
+int srv_post_one(qpp_txq *q, std::chrono::steady_clock::time_point now, uint32_t wg, uint32_t slot, uint32_t nr,
+                 uint64_t pn, uint32_t lens, uint32_t misc) {
+    RC_TRY(srv_start(q));
+    q->srv_seq = srv_next(q->srv_seq);
+    const uint32_t seq = q->srv_seq;
+    const uint32_t word = (q->srv_epoch << 24) | q->srv_wgs;  // item b for workgroup b; all but one empty
+    for (uint32_t b = 0; b < q->srv_wgs; b++) {
+        TxsSlot &sl = q->h_slots[b];
+        sl.word = word;
+        if (b == wg) {
+            sl.status[0] = (int8_t)QPP_INTERNAL_ERROR;
+            TxsSlotDesc &sd = sl.desc[0];
+            sd.pn = pn;
+            sd.key_idx = slot;
+            __atomic_store_n(&sd.tag0, seq, __ATOMIC_RELEASE);
+            sd.off = 0;
+            sd.lens = lens;
+            sd.misc = misc;
+            __atomic_store_n(&sd.tag1, seq, __ATOMIC_RELEASE);
+        }
+        sl.it_key = b == wg ? slot : 0u;
+        sl.it_count = b == wg ? 1u : 0u;
+        sl.it_nr = b == wg ? nr : 0u;
+        __atomic_store_n(&sl.it_tag, seq, __ATOMIC_RELEASE);
+        __atomic_store_n(&sl.seq, seq, __ATOMIC_RELEASE);
+    }
+    q->srv_last_post = now;
+    q->srv_posted = seq;
+    q->srv_first = q->srv_last = 0;  // (no ticket: nothing of the transmit-queue API refers to this post)
+    q->n_server++;
+    q->ctx->pkt_calls++;
+    return srv_wait(q, seq);
+}
+
+int packet_server_get(qpp_ctx *ctx, qpp_txq **out) {
+    if (!ctx->pkt_q) RC_TRY(txq_create_server(ctx, kPktRing, 1, kPktWgs, srv_idle_ms(), &ctx->pkt_q));
+    *out = ctx->pkt_q;
+    return QPP_OK;
+}
 int packet_server_run(const qpp_key *k, bool seal, uint64_t pn, const uint8_t *header, size_t header_len,
                       const uint8_t *payload, size_t payload_len, uint8_t *out, uint8_t *tag_out, int8_t *status_out,
                       bool *handled) {
@@ -2479,8 +2527,8 @@ int packet_server_run(const qpp_key *k, bool seal, uint64_t pn, const uint8_t *h
     const size_t total = header_len + payload_len + 16;
     // FIPS seals keep the launched path (its nonce-order gate)
     if (!ctx->pkt_server || (seal && rec.fips) || total > kPktRing) return QPP_OK;
-    if (!ctx->pkt_q) RC_TRY(txq_create_server(ctx, kPktRing, 1, kPktWgs, srv_idle_ms(), &ctx->pkt_q));
-    qpp_txq *q = ctx->pkt_q;
+    qpp_txq *q = nullptr;
+    RC_TRY(packet_server_get(ctx, &q));
     RC_TRY(flush_keys(ctx));
     const auto now = std::chrono::steady_clock::now();
     RC_TRY(srv_prepare(q, now));
@@ -2488,36 +2536,9 @@ int packet_server_run(const qpp_key *k, bool seal, uint64_t pn, const uint8_t *h
     if (header_len) memcpy(r, header, header_len);
     if (payload_len) memcpy(r + header_len, payload, payload_len);
     if (!seal) memcpy(r + header_len + payload_len, tag_out, 16);
-    RC_TRY(srv_start(q));
-    q->srv_seq = srv_next(q->srv_seq);
-    const uint32_t seq = q->srv_seq, wg = k->slot % q->srv_wgs;
-    const uint32_t word = (q->srv_epoch << 24) | q->srv_wgs;  // item b for workgroup b; all but one empty
-    for (uint32_t b = 0; b < q->srv_wgs; b++) {
-        TxsSlot &sl = q->h_slots[b];
-        sl.word = word;
-        if (b == wg) {
-            sl.status[0] = (int8_t)QPP_INTERNAL_ERROR;  // (stays so if the record is not live as planned)
-            TxsSlotDesc &sd = sl.desc[0];
-            sd.pn = pn;
-            sd.key_idx = k->slot;
-            __atomic_store_n(&sd.tag0, seq, __ATOMIC_RELEASE);
-            sd.off = 0;
-            sd.lens = (uint32_t)header_len | (uint32_t)payload_len << 16;
-            sd.misc = (uint32_t)(seal ? kTxsPktNoHp : kTxsPktOpen) << 8;
-            __atomic_store_n(&sd.tag1, seq, __ATOMIC_RELEASE);
-        }
-        sl.it_key = b == wg ? k->slot : 0u;
-        sl.it_count = b == wg ? 1u : 0u;
-        sl.it_nr = b == wg ? rec.nr : 0u;
-        __atomic_store_n(&sl.it_tag, seq, __ATOMIC_RELEASE);
-        __atomic_store_n(&sl.seq, seq, __ATOMIC_RELEASE);
-    }
-    q->srv_last_post = now;
-    q->srv_posted = seq;
-    q->srv_first = q->srv_last = 0;  // (no ticket: nothing of the transmit-queue API refers to this post)
-    q->n_server++;
-    ctx->pkt_calls++;
-    RC_TRY(srv_wait(q, seq));
+    const uint32_t wg = k->slot % q->srv_wgs;
+    RC_TRY(srv_post_one(q, now, wg, k->slot, rec.nr, pn, (uint32_t)header_len | (uint32_t)payload_len << 16,
+                        (uint32_t)(seal ? kTxsPktNoHp : kTxsPktOpen) << 8));
     *status_out = __atomic_load_n(&q->h_slots[wg].status[0], __ATOMIC_ACQUIRE);
     *handled = true;
     if (!(seal && *status_out != QPP_OK)) {  // (a refused seal leaves the caller's buffer untouched)
@@ -2525,6 +2546,30 @@ int packet_server_run(const qpp_key *k, bool seal, uint64_t pn, const uint8_t *h
         if (seal) memcpy(tag_out, r + header_len + payload_len, 16);
     }
     secure_zero(r, total);
+    return QPP_OK;
+}
+
+}  // namespace
+
+namespace {
+
+// HeaderKey::*_header_protection_mask of one sample (header_key.rs:52-56) through the packet server: the sample at
+// ring offset 0, the mask written at 16 by a mask item (kTxsMaskNr) on workgroup slot % kPktWgs
+int packet_server_mask(qpp_ctx *ctx, uint32_t slot, const uint8_t *sample, uint8_t mask[5], bool *handled) {
+    *handled = false;
+    if (!ctx->pkt_server || slot >= ctx->key_cap || !ctx->h_keys[slot].live) return QPP_OK;
+    qpp_txq *q = nullptr;
+    RC_TRY(packet_server_get(ctx, &q));
+    RC_TRY(flush_keys(ctx));
+    const auto now = std::chrono::steady_clock::now();
+    RC_TRY(srv_prepare(q, now));
+    uint8_t *r = q->h_ring;
+    memcpy(r, sample, 16);
+    memset(r + 16, 0, 16);
+    RC_TRY(srv_post_one(q, now, slot % q->srv_wgs, slot, kTxsMaskNr, 0, 16, 0));
+    memcpy(mask, r + 16, 5);
+    secure_zero(r, 32);
+    *handled = true;
     return QPP_OK;
 }
 

@@ -39,16 +39,27 @@ __device__ __forceinline__ uint32_t tab(int t) { return kBurstGh + (uint32_t)t *
 
 // Z * P_t through T_t: nibble pos 2k = high nibble of byte k, 2k + 1 = its low nibble (GCM bit order: the byte's
 // 0x80 bit is the lowest power of x).
+// At most D byte positions (2 D reads) in flight: left to itself the compiler issued all 32 reads first -- 128 VGPRs
+// for one product, which pushed the persistent server kernel (this code plus its polling state) into scratch memory,
+// and on the pinned ring every scratch reload after the first payload stores waited for their PCIe round trip.
+// 8 positions in flight still keep the LDS pipe busy (16 b128 reads issue in 64 cycles, about its latency).
 __device__ __forceinline__ uint4 gmul(uint32_t base, uint4 z) {
+    constexpr int D = 8;
     const uint32_t w[4] = {z.x, z.y, z.z, z.w};
-    uint4 acc[4];
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
+    uint4 hi[D], lo[D], acc[4];
+    auto issue = [&](auto kc) {
+        constexpr int k = decltype(kc)::value;
         const uint32_t byte = w[k >> 2] >> (8 * (k & 3));
-        const uint4 hi = lds_ld128(base + 512u * k + (byte & 0xf0u));
-        const uint4 lo = lds_ld128(base + 512u * k + 256u + ((byte & 0x0fu) << 4));
-        acc[k & 3] = k < 4 ? hi ^ lo : xor3(acc[k & 3], hi, lo);
-    }
+        hi[k % D] = lds_ld128(base + 512u * k + (byte & 0xf0u));
+        lo[k % D] = lds_ld128(base + 512u * k + 256u + ((byte & 0x0fu) << 4));
+    };
+    static_for<D>([&](auto kc) { issue(kc); });
+    static_for<16>([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        __builtin_amdgcn_sched_barrier(0);
+        acc[k & 3] = k < 4 ? hi[k % D] ^ lo[k % D] : xor3(acc[k & 3], hi[k % D], lo[k % D]);
+        if constexpr (k + D < 16) issue(std::integral_constant<int, k + D>{});
+    });
     return xor3(acc[0], acc[1], acc[2] ^ acc[3]);
 }
 
@@ -114,7 +125,10 @@ constexpr uint32_t kTxsStopFlag = kTxsCtl + 16 * kTxsPollLanes;
 constexpr uint32_t kTxsKey = kTxsCtl + 320;
 constexpr uint32_t kTxsKeyHdr = kTxsKey + 496;  // (iv | rk | hp_rk: 124 words)
 constexpr uint32_t kTxsTrace = kTxsKey + 512;  // QPP_TXS_TRACE: wave 0's stamps inside its packet (8 words)
-constexpr uint32_t kTxsLds = kTxsTrace + 32;
+// header-protection mask items (kTxsMaskNr): their key's record header (suite, nr, hp_nr, live) and HP round keys,
+// apart from the packet key above so that a mask between two seals of one key costs that key nothing
+constexpr uint32_t kTxsMaskKey = kTxsTrace + 32;
+constexpr uint32_t kTxsLds = kTxsMaskKey + 256;
 static_assert(kTxsStopFlag + 4 <= kTxsKey && kTxsLds <= kLdsMax && kBurstWaves == (int)kTxsWaves, "server LDS");
 #ifndef QPP_TXS_TRACE
 #define QPP_TXS_TRACE 0  // 1: workgroup 0 stamps its phases into the mailbox (tools/diag/server_trace.py)
@@ -169,6 +183,10 @@ __device__ __forceinline__ void burst_packet(const AesLds &aes, const DevKey *__
     HpPrefetch<HNR> hpk;
     constexpr uint32_t hp_lds = LDSKEY ? kTxsKey + 16 + 240 : kBurstHpRk;  // the HP round keys in LDS
     if (hp_on && lane == 0 && p.pn_len >= 1 && p.pn_len <= 4) hpk.load_hdr(p.base, p.aad_len - p.pn_len, flags);
+    // open: the received tag, read now with the payload (read after the plaintext stores, it waited for their
+    // round trip: stores and loads share one counter)
+    uint4 want = make_uint4(0, 0, 0, 0);
+    if (!SEAL && lane == 0) want = ld16(pay + p.len);
     uint4 acc = make_uint4(0, 0, 0, 0), ct0 = acc, ct1 = acc;  // ct0/ct1: ciphertext blocks 0/1 where owned
     uint4 ek = acc;  // E_K(J0), computed in pass 0 by the idle lane pad - 1 inside the data lanes' AES stream
     // counter block of this lane in pass k (data block b uses counter b + 2; J0 = counter 1 for everything else)
@@ -206,8 +224,18 @@ __device__ __forceinline__ void burst_packet(const AesLds &aes, const DevKey *__
         }
         acc = k ? gmul(tab(6), acc) ^ x : x;
     };
+    // LDSKEY: the round keys from the server's LDS copy, one broadcast read per round (held in SGPRs for the whole
+    // packet, 44 / 60 words, they crowded the server kernel's registers into scratch memory, and every reload after
+    // the first ring stores waited for those stores' PCIe round trip)
     auto rkey = [&](int r, uint32_t (&k)[4]) {
-        k[0] = rk[4 * r]; k[1] = rk[4 * r + 1]; k[2] = rk[4 * r + 2]; k[3] = rk[4 * r + 3];
+        if constexpr (LDSKEY) {
+            uint32_t o = kTxsKey + 16u + 16u * (uint32_t)r;
+            asm volatile("" : "+v"(o));  // read where used, not hoisted out of the pass loop into 44-60 VGPRs
+            const uint4 v = lds_ld128(o);
+            k[0] = v.x; k[1] = v.y; k[2] = v.z; k[3] = v.w;
+        } else {
+            k[0] = rk[4 * r]; k[1] = rk[4 * r + 1]; k[2] = rk[4 * r + 2]; k[3] = rk[4 * r + 3];
+        }
     };
     // Passes in pairs: the two passes' AES chains are independent, so they run interleaved (one chain of dependent
     // LDS rounds for both instead of one each); a pass past the packet (K odd) computes a discarded block.
@@ -258,7 +286,9 @@ __device__ __forceinline__ void burst_packet(const AesLds &aes, const DevKey *__
     if (pad) {
         ek0 = shfl4(ek, (int)pad - 1);
     } else {  // (pad == 0: no idle lane in pass 0)
-        ek0 = aes.encrypt<NR>(make_uint4(p.n0, p.n1, p.n2, bswap32(1u)), rk);
+        const uint4 j0 = make_uint4(p.n0, p.n1, p.n2, bswap32(1u));
+        if constexpr (LDSKEY) ek0 = aes.encrypt_lrk<NR>(j0, kTxsKey + 16u);
+        else ek0 = aes.encrypt<NR>(j0, rk);
     }
     const uint4 tag = shfl4(gmul(tab(0), acc), 0) ^ ek0;  // Y = Q * H, from lane 0
 
@@ -290,8 +320,7 @@ __device__ __forceinline__ void burst_packet(const AesLds &aes, const DevKey *__
         TXS_STAMP(4);
         if (status && lane == 0) status[pi] = st;
     } else {
-        const uint4 want = ld16(pay + p.len);
-        const uint4 diff = tag ^ want;
+        const uint4 diff = tag ^ shfl4(want, 0);
         const bool ok = (diff.x | diff.y | diff.z | diff.w) == 0;  // all 16 bytes compared, no early exit
         if (!ok) {
             // never release unauthenticated plaintext: each lane zeroes the blocks it wrote (same-lane order)
@@ -375,9 +404,7 @@ __global__ __launch_bounds__(kBurstWG) void aes_gcm_burst_kernel(const DevKey *_
 template <int NR>
 __device__ __forceinline__ void txs_item(const AesLds &aes, const DevKey *key, const qpp_pkt &d,
                                          uint32_t wave, uint32_t count, uint8_t *ring, int8_t *status) {
-    uint32_t rk[4 * (NR + 1)];
-#pragma unroll
-    for (int i = 0; i < 4 * (NR + 1); i++) rk[i] = __builtin_amdgcn_readfirstlane(lds_ld32(kTxsKey + 16 + 4 * i));
+    const uint32_t *rk = nullptr;  // (the round keys come from LDS: burst_packet<.., LDSKEY = true>)
     if (wave < count && !(d.flags & QPP_PKT_SKIP)) {
         if (d.flags & kTxsPktOpen)
             burst_packet<NR, false, true>(aes, key, rk, d, wave, ring, nullptr, status, 0);
@@ -411,6 +438,31 @@ __device__ __forceinline__ void txs_item_chacha(const qpp_pkt &d, uint32_t wave,
     }
 }
 
+// A header-protection mask item (HeaderKey::*_header_protection_mask, header_key.rs:52-56): the 16-byte sample at
+// ring offset d.off, the 5 mask bytes written at d.off + 16, by lane 0 of wave 0 (every lane computes the block)
+__device__ __forceinline__ void txs_mask_item(const AesLds &aes, const qpp_pkt &d, uint32_t wave, uint32_t count,
+                                              uint8_t *ring, uint32_t lane) {
+    if (!(wave < count)) return;
+    const uint4 smp = ld16(ring + d.off);
+    const uint32_t suite = lds_ld32(kTxsMaskKey), hp_nr = lds_ld32(kTxsMaskKey + 8);
+    uint32_t m0 = 0, m1 = 0;
+    if (suite == QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256) {
+        uint32_t hk[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) hk[i] = lds_ld32(kTxsMaskKey + 16 + 4 * i);
+        m0 = chacha_hp_word(hk, smp, &m1);
+    } else {
+        const uint4 m = hp_nr == 14 ? aes.encrypt_lrk<14>(smp, kTxsMaskKey + 16) : aes.encrypt_lrk<10>(smp, kTxsMaskKey + 16);
+        m0 = m.x;
+        m1 = m.y;
+    }
+    if (lane == 0) {
+        uint8_t *o = ring + d.off + 16;
+        o[0] = (uint8_t)m0; o[1] = (uint8_t)(m0 >> 8); o[2] = (uint8_t)(m0 >> 16); o[3] = (uint8_t)(m0 >> 24);
+        o[4] = (uint8_t)m1;
+    }
+}
+
 // one 16-byte chunk of the slot (lane < kTxsPollLanes), in ONE load past every cache (sc0 sc1: the host writes it;
 // a chunk is read whole, so its tag vouches for its other words)
 __device__ __forceinline__ uint4 txs_poll(const TxsSlot *slot, uint32_t lane) {
@@ -432,7 +484,7 @@ __global__ __launch_bounds__(kBurstWG) void txq_server_kernel(const DevKey *keys
     const AesLds aes = make_aes(kBurstAes);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
     TxsSlot *slot = slots + blockIdx.x;
-    uint32_t seen = seq0, cached = 0xffffffffu, epoch = 0xffffffffu;
+    uint32_t seen = seq0, cached = 0xffffffffu, mcached = 0xffffffffu, epoch = 0xffffffffu;
     {
         // A server relaunched behind a posted flush (seq0 = posted - 1: the previous one left on its idle timeout
         // before every workgroup had seen it) must not seal it again in the workgroups that did: the ring is sealed in
@@ -480,7 +532,9 @@ __global__ __launch_bounds__(kBurstWG) void txq_server_kernel(const DevKey *keys
                 // Every flush: the CU's vector cache (and L2's non-coherent lines) dropped, so that this flush's ring
                 // bytes are read from the host, not the lines the previous flush left for the same offsets (the ring
                 // is reused flush after flush; without it, every flush after the first of one server launch sealed
-                // stale plaintext: tools/diag/server_mismatch.py), and key records installed since are visible
+                // stale plaintext: tools/diag/server_mismatch.py), and key records installed since are visible.
+                // (Reading the ring past the caches instead -- volatile loads, then system-scope buffer loads --
+                // measured slower, and the buffer-load build faulted the GPU on a many-key flush: round 4, r04k.)
                 if (!stop) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
             }
         }
@@ -510,7 +564,7 @@ __global__ __launch_bounds__(kBurstWG) void txq_server_kernel(const DevKey *keys
         asm volatile("" : "+v"(items_v), "+v"(sdesc_v), "+v"(keys_v));
         if (ep != epoch) {
             epoch = ep;
-            cached = 0xffffffffu;
+            cached = mcached = 0xffffffffu;
         }
         uint64_t tr[4] = {0, 0, 0, 0}, clk0 = 0;
         if (QPP_TXS_TRACE && threadIdx.x == 0) {
@@ -524,6 +578,18 @@ __global__ __launch_bounds__(kBurstWG) void txq_server_kernel(const DevKey *keys
             const qpp_pkt d = first ? d0 : sdesc_v[it * kBurstWaves + wave];
             const DevKey *key = keys_v + w.key;
             if (w.count == 0) continue;  // (a per-packet request posts one packet to one workgroup, none to the others)
+            if (w.nr == kTxsMaskNr) {  // uniform: a mask item -- its key's header and HP round keys, cached apart
+                if (w.key != mcached) {
+                    __syncthreads();
+                    const uint32_t *kw = (const uint32_t *)key;
+                    if (threadIdx.x < 4) lds_st32(kTxsMaskKey + 4 * threadIdx.x, kw[threadIdx.x]);
+                    else if (threadIdx.x < 64) lds_st32(kTxsMaskKey + 16 + 4 * (threadIdx.x - 4), kw[64 + threadIdx.x]);
+                    __syncthreads();
+                    mcached = w.key;
+                }
+                if (lds_ld32(kTxsMaskKey + 12) != 0) txs_mask_item(aes, d, wave, w.count, ring, lane);  // (live 1 or 2)
+                continue;
+            }
             if (w.key != cached) {  // uniform
                 __syncthreads();  // every wave is done with the previous key's tables
                 // iv | rk | hp_rk: 124 consecutive words of the record (DevKey: iv at word 4), then its header

@@ -68,13 +68,19 @@ struct Poly1305 {
     }
 };
 
+// hb: the header bytes hdr_load read (read before any store of the packet by the wave-per-packet code)
 __device__ __forceinline__ void apply_mask(uint8_t *base, uint32_t hdr_len, uint32_t pn_len, uint32_t m0, uint32_t m1,
-                                           uint8_t *mask_out, uint32_t flags) {
+                                           uint8_t *mask_out, uint32_t flags, HdrBytes hb) {
     if (flags & QPP_HP_MASK_OUT) {
         mask_out[0] = (uint8_t)m0; mask_out[1] = (uint8_t)(m0 >> 8); mask_out[2] = (uint8_t)(m0 >> 16);
         mask_out[3] = (uint8_t)(m0 >> 24); mask_out[4] = (uint8_t)m1;
     }
-    if (flags & QPP_HP_APPLY) hdr_apply(base, hdr_len, pn_len, hdr_load(base, hdr_len), m0, m1);  // header_crypto.rs:80-95
+    if (flags & QPP_HP_APPLY) hdr_apply(base, hdr_len, pn_len, hb, m0, m1);  // header_crypto.rs:80-95
+}
+__device__ __forceinline__ void apply_mask(uint8_t *base, uint32_t hdr_len, uint32_t pn_len, uint32_t m0, uint32_t m1,
+                                           uint8_t *mask_out, uint32_t flags) {
+    apply_mask(base, hdr_len, pn_len, m0, m1, mask_out, flags,
+               (flags & QPP_HP_APPLY) ? hdr_load(base, hdr_len) : HdrBytes{0, 0});
 }
 
 // ---------------------------------------------------------------- one WAVE per packet
@@ -138,7 +144,8 @@ __device__ __forceinline__ uint32_t byte_of(uint4 v, uint32_t i) {  // byte i (<
 // plaintext in place (zeroed on a bad tag, all 16 tag bytes compared), *status_out = OK / DECRYPT_ERROR.  status_out
 // and mask_out are written by lane 0 only (status_out may be null when sealing).
 // Each lane's block of pass kk + 1 is loaded before pass kk's ChaCha20 block and Poly1305 step: a packet pays one
-// memory round trip, not one per pass (the transmit-queue server reads the ring over PCIe).
+// memory round trip, not one per pass (the transmit-queue server reads the ring over PCIe).  Nothing is read after
+// the first store (stores and loads share one counter: a read after them waits for their PCIe round trip).
 template <bool SEAL>
 __device__ __forceinline__ void chacha_wave_packet(const uint32_t (&k)[8], uint32_t n0, uint32_t n1, uint32_t n2,
                                                    const uint32_t *hk, const qpp_pkt &d, uint8_t *arena,
@@ -162,6 +169,12 @@ __device__ __forceinline__ void chacha_wave_packet(const uint32_t (&k)[8], uint3
     uint4 pk0 = ct0, pk1 = ct0;                       // the one-time Poly1305 key (r, s), in lane pad - 1
     P130 rp[7];                                       // r^(2^t), from pass 1 on (pass 0 needs no power of r)
     uint4 nxt = load(0);
+    // the header bytes the HP mask is applied to (seal) / the received tag (open), read with the first blocks
+    const bool hdr_want = SEAL && (flags & QPP_HP_APPLY) && d.pn_len >= 1 && d.pn_len <= 4;
+    HdrBytes hb{0, 0};
+    if (hdr_want && lane == 0) hb = hdr_load(base, aad_len - d.pn_len);
+    uint4 want = make_uint4(0, 0, 0, 0);
+    if (!SEAL && lane == 0) want = ld16(pay + len);
     for (uint32_t kk = 0; kk < K; kk++) {
         const int i = (int)(lane + 64u * kk) - (int)pad;
         const bool data = i >= (int)a && i < (int)(a + c);
@@ -260,12 +273,12 @@ __device__ __forceinline__ void chacha_wave_packet(const uint32_t (&k)[8], uint3
 #pragma unroll
                 for (int i = 0; i < 8; i++) hkr[i] = hk[i];
                 uint32_t m1, m0 = chacha_hp_word(hkr, smp, &m1);
-                if (lane == 0) apply_mask(base, aad_len - d.pn_len, d.pn_len, m0, m1, mask_out, flags);
+                if (lane == 0) apply_mask(base, aad_len - d.pn_len, d.pn_len, m0, m1, mask_out, flags, hb);
             }
         }
         if (status_out && lane == 0) *status_out = st8;
     } else {
-        const uint4 diff = tag ^ ld16(pay + len);
+        const uint4 diff = tag ^ shfl4(want, 0);
         const bool ok = (diff.x | diff.y | diff.z | diff.w) == 0;
         if (!ok) {  // each lane zeroes the plaintext blocks it wrote (same-lane order)
             for (uint32_t kk = 0; kk < K; kk++) {

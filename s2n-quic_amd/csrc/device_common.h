@@ -591,6 +591,7 @@ __device__ __forceinline__ HdrBytes hdr_load(const uint8_t *base, uint32_t hdr_l
     __builtin_memcpy(&h.pnw, base + hdr_len, 4);
     return h;
 }
+
 __device__ __forceinline__ void hdr_apply(uint8_t *base, uint32_t hdr_len, uint32_t pn_len, HdrBytes h, uint32_t m0,
                                           uint32_t m1) {
     const uint32_t nb0 = h.b0 ^ (m0 & ((h.b0 & 0x80) ? 0x0fu : 0x1fu));

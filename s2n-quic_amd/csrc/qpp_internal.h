@@ -155,6 +155,7 @@ constexpr uint32_t kTxsStop = 0xffffffu;
 // run_one_server): never set by the transport (qpp_txq_push_descs refuses any flag)
 constexpr uint8_t kTxsPktNoHp = 0x40;  // seal without header protection (Key::encrypt), status written
 constexpr uint8_t kTxsPktOpen = 0x80;  // open (Key::decrypt), status written
+constexpr uint32_t kTxsMaskNr = 0xffu;  // WorkItem.nr of a header-protection mask item (qpp_hp_mask, qpp_header_key_mask)
 // Every 16-byte chunk carries the flush's seq as its last word (the host stores it after the chunk's other words):
 // the server reads each chunk with ONE 16-byte load, so a chunk whose tag matches is wholly this flush's.  (With the
 // tag in only one chunk of a descriptor, a poll could combine a stale first half -- the previous flush's pn, key and

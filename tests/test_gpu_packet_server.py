@@ -107,3 +107,29 @@ def test_server_restarts_and_long_packets(monkeypatch):
             f.encrypt(10, header, payload)  # the same packet number again: refused
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize("suite", SUITES)
+def test_server_header_protection_masks(suite):
+    """HeaderKey::*_header_protection_mask (header_key.rs:52-56) of packet keys and header-key-only records through the
+    server's mask items, interleaved with seals of the same packet key (the mask's key words are cached apart from the
+    packet key's in the workgroup's LDS): every mask and every seal bit-exact"""
+    rng = np.random.default_rng(7400 + suite)
+    ctx = qpp.Context(0)
+    try:
+        k = ctx.key(suite, rng.integers(0, 256, qpp.HASH_LEN[suite], dtype=np.uint8).tobytes())
+        kk, iv, hp = k.material()
+        hp2 = rng.integers(0, 256, len(hp), dtype=np.uint8).tobytes()
+        hk = ctx.header_key(suite, hp=hp2)
+        calls0 = ctx.packet_server_info()[0]
+        for i in range(24):
+            sample = rng.integers(0, 256, 16, dtype=np.uint8).tobytes()
+            assert k.header_protection_mask(sample) == orc.hp_mask(suite, hp, sample)[:5]
+            assert hk.header_protection_mask(sample) == orc.hp_mask(suite, hp2, sample)[:5]
+            payload = rng.integers(0, 256, int(rng.integers(0, 1500)), dtype=np.uint8).tobytes()
+            header = rng.integers(0, 256, 21, dtype=np.uint8).tobytes()
+            assert k.encrypt(i, header, payload) == b"".join(orc.seal(suite, kk, orc.nonce(iv, i), header, payload))
+        assert ctx.packet_server_info()[0] - calls0 == 3 * 24
+        hk.free()
+    finally:
+        ctx.close()

@@ -245,18 +245,22 @@ __device__ __forceinline__ void burst_packet(const AesLds &aes, const DevKey *__
         if (k + 3 < K) nx1 = block(k + 3);
         if (k == 0) TXS_STAMP(1);
         const uint4 c0 = ctr(k), c1 = ctr(k + 1);
-        uint32_t kk[4];
+        // (round r + 1's key words read while round r runs: read right before its round, an LDS key read added its
+        // latency to every round of the chain)
+        uint32_t kk[4], kn[4];
         rkey(0, kk);
+        rkey(1, kn);
         uint32_t s0[4] = {c0.x ^ kk[0], c0.y ^ kk[1], c0.z ^ kk[2], c0.w ^ kk[3]};
         uint32_t s1[4] = {c1.x ^ kk[0], c1.y ^ kk[1], c1.z ^ kk[2], c1.w ^ kk[3]};
 #pragma unroll
         for (int r = 1; r < NR; r++) {
-            rkey(r, kk);
+#pragma unroll
+            for (int i = 0; i < 4; i++) kk[i] = kn[i];
+            rkey(r + 1, kn);
             aes.round(s0, kk);
             aes.round(s1, kk);
         }
-        rkey(NR, kk);
-        const uint4 ks0 = aes.final(s0, kk), ks1 = aes.final(s1, kk);
+        const uint4 ks0 = aes.final(s0, kn), ks1 = aes.final(s1, kn);
         pass(k, r0, ks0);
         if (k + 1 < K) pass(k + 1, r1, ks1);
     }

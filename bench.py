@@ -717,13 +717,13 @@ def per_packet(args, ctx, keys, rank, world, max_over_ranks, calls=2000):
         ctx.set_packet_server(False)
     drv = ctypes.CDLL(os.path.join(ROOT, "tools", "libtxqdrive.so")).packet_latency
     drv.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t,
-                    ctypes.c_size_t, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
+                    ctypes.c_size_t, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     n = args.warmup + calls
-    ts, to = np.zeros(n), np.zeros(n)
-    rc = drv(k.handle, hdr, len(hdr), pt, len(pt), n, 0, ts.ctypes.data, to.ctypes.data)
+    ts, to, tm = np.zeros(n), np.zeros(n), np.zeros(n)
+    rc = drv(k.handle, hdr, len(hdr), pt, len(pt), n, 0, ts.ctypes.data, to.ctypes.data, tm.ctypes.data)
     if rc:
         raise SystemExit(f"per-packet driver failed: {rc}")
-    ts, to = ts[args.warmup:], to[args.warmup:]
+    ts, to, tm = ts[args.warmup:], to[args.warmup:], tm[args.warmup:]
     t = max_over_ranks(float(np.median(ts)) * 1e-6)
     calls_srv, starts = ctx.packet_server_info()
     if rank == 0:
@@ -732,6 +732,7 @@ def per_packet(args, ctx, keys, rank, world, max_over_ranks, calls=2000):
             "unit": "us", "higher_is_better": False, "n_gpus": world, "suite": args.suite,
             "p10_us": round(float(np.percentile(ts, 10)), 2), "p90_us": round(float(np.percentile(ts, 90)), 2),
             "decrypt_us": round(float(np.median(to)), 2), "decrypt_p90_us": round(float(np.percentile(to, 90)), 2),
+            "hp_mask_us": round(float(np.median(tm)), 2),
             "calls": calls, "path": "launch per call" if args.no_server else "packet server",
             "server_calls_starts": [calls_srv, starts], "driver": "tools/txqdrive.c packet_latency (timed in C)",
         }), flush=True)

@@ -25,7 +25,8 @@ def ctx():
 
 @pytest.fixture(params=["burst", "quad", "wave"])
 def path(request, ctx):
-    """AES-GCM kernel path: wave per packet (small batches), lane per packet with one key per 1024-packet workgroup,
+    """AES-GCM kernel path: wave per packet (small batches), the quad kernel (four lanes per packet, one workgroup per
+    CU over a key-sorted slice),
     or lane per packet with one key per 64-packet wave (many keys); same outputs."""
     ctx.set_burst_max(1 << 30 if request.param == "burst" else 0)
     ctx.set_aes_kernel({"burst": qpp.AES_KERNEL_AUTO, "quad": qpp.AES_KERNEL_QUAD,

@@ -6,33 +6,16 @@
  *                    size_t bursts, uint64_t pn0)  -> seconds for `bursts` bursts (all waited for), < 0 on error
  *   int txq_latency(qpp_txq *q, const qpp_pkt *proto, size_t burst, size_t bursts, uint64_t pn0, double *lat_us)
  *        -> one burst at a time: push, then qpp_txq_flush (seal and wait); lat_us[k] = that call's duration
- *   int packet_latency(qpp_key *k, const uint8_t *header, size_t header_len, const uint8_t *payload, size_t payload_len,
-                   size_t calls, uint64_t pn0, double *seal_us, double *open_us) {
-    uint8_t *buf = (uint8_t *)malloc(payload_len + 16);
-    if (!buf) return -1;
-    for (size_t c = 0; c < calls; c++) {
-        memcpy(buf, payload, payload_len);
-        double t0 = now_s();
-        if (qpp_seal(k, pn0 + c, header, header_len, buf, payload_len, payload_len + 16) != QPP_OK) return -2;
-        double t1 = now_s();
-        if (qpp_open(k, pn0 + c, header, header_len, buf, payload_len + 16) != QPP_OK) return -3;
-        double t2 = now_s();
-        if (memcmp(buf, payload, payload_len) != 0) return -5;
-        seal_us[c] = 1e6 * (t1 - t0);
-        open_us[c] = 1e6 * (t2 - t1);
-    }
-    free(buf);
-    return 0;
-}
-
-int rotate_keys(qpp_ctx *ctx, qpp_key **keys, size_t n, uint32_t *slots)
+ *   int rotate_keys(qpp_ctx *ctx, qpp_key **keys, size_t n, uint32_t *slots)
  *        -> a KeySet rotation of every connection (BASELINE configs[4]): keys[i] <- its next-phase key
  *           (qpp_key_update_batch), the old keys freed (qpp_key_free_batch), slots[i] = the new slots, and the
  *           connection table repointed (qpp_ctx_set_conn_keys), as the transport would call it
  *   int packet_latency(qpp_key *k, const uint8_t *header, size_t header_len, const uint8_t *payload,
- *                      size_t payload_len, size_t calls, uint64_t pn0, double *seal_us, double *open_us)
- *        -> Key::encrypt then Key::decrypt of one packet per call (qpp_seal, qpp_open), each call timed; the opened
- *           bytes checked against the payload (returns -5 on a mismatch)
+ *                      size_t payload_len, size_t calls, uint64_t pn0, double *seal_us, double *open_us,
+ *                      double *mask_us)
+ *        -> Key::encrypt, the sealing HeaderKey mask of a sample of the sealed packet, then Key::decrypt of one packet
+ *           per call (qpp_seal, qpp_hp_mask, qpp_open), each call timed; the opened bytes checked against the payload
+ *           (returns -5 on a mismatch)
  */
 #include <stdint.h>
 #include <stdlib.h>
@@ -90,7 +73,7 @@ int txq_latency(qpp_txq *q, const qpp_pkt *proto, size_t burst, size_t bursts, u
 }
 
 int packet_latency(qpp_key *k, const uint8_t *header, size_t header_len, const uint8_t *payload, size_t payload_len,
-                   size_t calls, uint64_t pn0, double *seal_us, double *open_us) {
+                   size_t calls, uint64_t pn0, double *seal_us, double *open_us, double *mask_us) {
     uint8_t *buf = (uint8_t *)malloc(payload_len + 16);
     if (!buf) return -1;
     for (size_t c = 0; c < calls; c++) {
@@ -98,11 +81,15 @@ int packet_latency(qpp_key *k, const uint8_t *header, size_t header_len, const u
         double t0 = now_s();
         if (qpp_seal(k, pn0 + c, header, header_len, buf, payload_len, payload_len + 16) != QPP_OK) return -2;
         double t1 = now_s();
-        if (qpp_open(k, pn0 + c, header, header_len, buf, payload_len + 16) != QPP_OK) return -3;
+        uint8_t mask[5];
+        if (payload_len + 16 >= 20 && qpp_hp_mask(k, buf + 4, 16, mask) != QPP_OK) return -4;  /* sample: pn_len 0 */
         double t2 = now_s();
+        if (qpp_open(k, pn0 + c, header, header_len, buf, payload_len + 16) != QPP_OK) return -3;
+        double t3 = now_s();
         if (memcmp(buf, payload, payload_len) != 0) return -5;
         seal_us[c] = 1e6 * (t1 - t0);
-        open_us[c] = 1e6 * (t2 - t1);
+        mask_us[c] = 1e6 * (t2 - t1);
+        open_us[c] = 1e6 * (t3 - t2);
     }
     free(buf);
     return 0;

@@ -454,7 +454,7 @@ __device__ __forceinline__ void txs_mask_item(const AesLds &aes, const qpp_pkt &
         uint32_t hk[8];
 #pragma unroll
         for (int i = 0; i < 8; i++) hk[i] = lds_ld32(kTxsMaskKey + 16 + 4 * i);
-        m0 = chacha_hp_word(hk, smp, &m1);
+        m0 = chacha_hp_quad(hk, smp, lane & 3u, &m1);
     } else {
         const uint4 m = hp_nr == 14 ? aes.encrypt_lrk<14>(smp, kTxsMaskKey + 16) : aes.encrypt_lrk<10>(smp, kTxsMaskKey + 16);
         m0 = m.x;

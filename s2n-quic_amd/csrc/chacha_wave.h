@@ -138,6 +138,36 @@ __device__ __forceinline__ uint32_t byte_of(uint4 v, uint32_t i) {  // byte i (<
     return (w >> (8 * (i & 3))) & 0xffu;
 }
 
+// quad_perm DPP: lane l reads lane 4 (l / 4) + sel[l % 4]
+template <int CTRL>
+__device__ __forceinline__ uint32_t cq_perm(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, false);
+}
+// The ChaCha20 block of the header-protection key (header_key.rs:52-56: counter = sample[0..4], nonce =
+// sample[4..16]; RFC 9001 §5.4.4) split over the 4 lanes of a quad: lane s holds column s (words s, 4 + s, 8 + s,
+// 12 + s), a column round is one quarter-round per lane, and a diagonal round one quarter-round on (a_s, b_s+1,
+// c_s+2, d_s+3) with those words moved in and back out by DPP -- a quarter of a whole block's VALU per lane (the
+// block is on the latency chain of every sealed packet of the wave-per-packet code).  Every lane of every quad must
+// be active.  Returns mask word 0 (bytes 0..3) and *w1 = word 1 (byte 4), in every lane.
+__device__ __forceinline__ uint32_t chacha_hp_quad(const uint32_t hk[8], uint4 smp, uint32_t s, uint32_t *w1) {
+    constexpr uint32_t k0 = 0x61707865u, k1 = 0x3320646eu, k2 = 0x79622d32u, k3 = 0x6b206574u;
+    const uint32_t a0 = s == 0 ? k0 : s == 1 ? k1 : s == 2 ? k2 : k3;
+    const uint32_t b0 = s == 0 ? hk[0] : s == 1 ? hk[1] : s == 2 ? hk[2] : hk[3];
+    const uint32_t c0 = s == 0 ? hk[4] : s == 1 ? hk[5] : s == 2 ? hk[6] : hk[7];
+    const uint32_t d0 = s == 0 ? smp.x : s == 1 ? smp.y : s == 2 ? smp.z : smp.w;
+    uint32_t a = a0, b = b0, c = c0, d = d0;
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+        QR(a, b, c, d);  // column round
+        b = cq_perm<0x39>(b); c = cq_perm<0x4e>(c); d = cq_perm<0x93>(d);  // (a_s, b_s+1, c_s+2, d_s+3)
+        QR(a, b, c, d);  // diagonal round
+        b = cq_perm<0x93>(b); c = cq_perm<0x4e>(c); d = cq_perm<0x39>(d);  // back to their columns
+    }
+    const uint32_t w = a + a0;  // keystream word s
+    *w1 = cq_perm<0x55>(w);
+    return cq_perm<0x00>(w);
+}
+
 // One packet, one wave (every lane calls it with the same d).  k: the ChaCha20 key, n0..n2: the packet's nonce words
 // (Iv::nonce, iv.rs:27-39), hk: the header-protection key (read only when sealing with an HP flag).  Seal: ciphertext
 // and tag in place, HP mask out / applied per flags, *status_out = OK / DECODE_ERROR (no room for the sample).  Open:
@@ -272,7 +302,7 @@ __device__ __forceinline__ void chacha_wave_packet(const uint32_t (&k)[8], uint3
                 uint32_t hkr[8];
 #pragma unroll
                 for (int i = 0; i < 8; i++) hkr[i] = hk[i];
-                uint32_t m1, m0 = chacha_hp_word(hkr, smp, &m1);
+                uint32_t m1, m0 = chacha_hp_quad(hkr, smp, lane & 3u, &m1);
                 if (lane == 0) apply_mask(base, aad_len - d.pn_len, d.pn_len, m0, m1, mask_out, flags, hb);
             }
         }

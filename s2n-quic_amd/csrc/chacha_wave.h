@@ -168,6 +168,40 @@ __device__ __forceinline__ uint32_t chacha_hp_quad(const uint32_t hk[8], uint4 s
     return cq_perm<0x00>(w);
 }
 
+// ChaCha20 block cb (equal within a quad) over the 4 lanes of the quad, as chacha_hp_quad: lane s computes column s
+// and returns ROW s after a 4 x 4 transpose through DPP -- keystream words 4 s .. 4 s + 3, the 16 bytes of the block's
+// quarter s.  Every lane of every quad must be active.
+__device__ __forceinline__ uint4 chacha_row_quad(const uint32_t (&k)[8], uint32_t cb, uint32_t n0, uint32_t n1,
+                                                 uint32_t n2, uint32_t s) {
+    constexpr uint32_t k0 = 0x61707865u, k1 = 0x3320646eu, k2 = 0x79622d32u, k3 = 0x6b206574u;
+    const uint32_t a0 = s == 0 ? k0 : s == 1 ? k1 : s == 2 ? k2 : k3;
+    const uint32_t b0 = s == 0 ? k[0] : s == 1 ? k[1] : s == 2 ? k[2] : k[3];
+    const uint32_t c0 = s == 0 ? k[4] : s == 1 ? k[5] : s == 2 ? k[6] : k[7];
+    const uint32_t d0 = s == 0 ? cb : s == 1 ? n0 : s == 2 ? n1 : n2;
+    uint32_t a = a0, b = b0, c = c0, d = d0;
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+        QR(a, b, c, d);
+        b = cq_perm<0x39>(b); c = cq_perm<0x4e>(c); d = cq_perm<0x93>(d);
+        QR(a, b, c, d);
+        b = cq_perm<0x93>(b); c = cq_perm<0x4e>(c); d = cq_perm<0x39>(d);
+    }
+    const uint32_t w[4] = {a + a0, b + b0, c + c0, d + d0};  // column s, rows 0..3
+    // lane s wants row s: word 4 s + t = row s of column t, i.e. register w[s] of lane t.  For a rotation rho, lane t
+    // offers w[(t - rho) & 3] and lane s reads lane (s + rho) & 3: it receives word 4 s + ((s + rho) & 3).
+    auto pick = [&](uint32_t j) { return j == 0 ? w[0] : j == 1 ? w[1] : j == 2 ? w[2] : w[3]; };
+    const uint32_t r0 = pick(s);
+    const uint32_t r1 = cq_perm<0x39>(pick((s - 1u) & 3u));
+    const uint32_t r2 = cq_perm<0x4e>(pick((s - 2u) & 3u));
+    const uint32_t r3 = cq_perm<0x93>(pick((s - 3u) & 3u));
+    // component t came with rho = (t - s) & 3
+    auto comp = [&](uint32_t t) {
+        const uint32_t rho = (t - s) & 3u;
+        return rho == 0 ? r0 : rho == 1 ? r1 : rho == 2 ? r2 : r3;
+    };
+    return make_uint4(comp(0), comp(1), comp(2), comp(3));
+}
+
 // One packet, one wave (every lane calls it with the same d).  k: the ChaCha20 key, n0..n2: the packet's nonce words
 // (Iv::nonce, iv.rs:27-39), hk: the header-protection key (read only when sealing with an HP flag).  Seal: ciphertext
 // and tag in place, HP mask out / applied per flags, *status_out = OK / DECODE_ERROR (no room for the sample).  Open:
@@ -199,6 +233,13 @@ __device__ __forceinline__ void chacha_wave_packet(const uint32_t (&k)[8], uint3
     uint4 pk0 = ct0, pk1 = ct0;                       // the one-time Poly1305 key (r, s), in lane pad - 1
     P130 rp[7];                                       // r^(2^t), from pass 1 on (pass 0 needs no power of r)
     uint4 nxt = load(0);
+    // Keystream by quads: quad j of pass kk computes ChaCha block 1 + (base_b + 4 j) / 4 split over its four lanes
+    // (chacha_row_quad: a quarter of a block's VALU per lane, where every lane computing its own data block's whole
+    // ChaCha block did 4x the work -- the 4 lanes of a block computed it 4 times), so lane L holds the keystream of
+    // data block base_b + L; the data block of lane l is base_b + l - delta (delta aligns the MAC layout's data blocks
+    // to quads), read from lane l - delta, or for l < delta from lane 64 + l - delta of the previous pass.
+    const uint32_t delta = (pad + a) & 3u;
+    uint4 prev_row = make_uint4(0, 0, 0, 0);
     // the header bytes the HP mask is applied to (seal) / the received tag (open), read with the first blocks
     const bool hdr_want = SEAL && (flags & QPP_HP_APPLY) && d.pn_len >= 1 && d.pn_len <= 4;
     HdrBytes hb{0, 0};
@@ -208,15 +249,29 @@ __device__ __forceinline__ void chacha_wave_packet(const uint32_t (&k)[8], uint3
     for (uint32_t kk = 0; kk < K; kk++) {
         const int i = (int)(lane + 64u * kk) - (int)pad;
         const bool data = i >= (int)a && i < (int)(a + c);
-        const bool key0 = kk == 0 && i == -1;  // ChaCha block 0 (the Poly1305 key) rides in an idle lane of pass 0
         const uint32_t b = (uint32_t)i - a;
         uint4 in = nxt;
         if (kk + 1 < K) nxt = load(kk + 1);
-        uint32_t ks[16];
-        if (data || key0) chacha_block(k, data ? 1u + (b >> 2) : 0u, n0, n1, n2, ks);
-        if (key0) {
-            pk0 = make_uint4(ks[0], ks[1], ks[2], ks[3]);
-            pk1 = make_uint4(ks[4], ks[5], ks[6], ks[7]);
+        const int base_b = 64 * (int)kk - (int)pad - (int)a + (int)delta;  // a multiple of 4
+        const int cbq = 1 + (base_b >> 2) + (int)(lane >> 2);
+        const uint4 row = chacha_row_quad(k, cbq > 0 ? (uint32_t)cbq : 0u, n0, n1, n2, lane & 3u);
+        uint4 kq = row;
+        if (delta) {  // (uniform)
+            const int src = (int)((lane - delta) & 63u);
+            const uint4 cur = shfl4(row, src), prv = shfl4(prev_row, src);
+            kq = lane >= delta ? cur : prv;
+        }
+        prev_row = row;
+        if (kk == 0) {  // the Poly1305 key: ChaCha block 0, rows 0 and 1, from the quad that computed it
+            const int j0 = -(base_b >> 2) - 1;  // (uniform)
+            if (j0 >= 0 && j0 < 16) {
+                pk0 = shfl4(row, 4 * j0);
+                pk1 = shfl4(row, 4 * j0 + 1);
+            } else {
+                const uint4 r0 = chacha_row_quad(k, 0u, n0, n1, n2, lane & 3u);
+                pk0 = shfl4(r0, 0);
+                pk1 = shfl4(r0, 1);
+            }
         }
         uint4 x = make_uint4(0, 0, 0, 0);
         uint32_t hib = 1u << 24;  // the 2^128 bit of every (padded, full) MAC block
@@ -226,11 +281,7 @@ __device__ __forceinline__ void chacha_wave_packet(const uint32_t (&k)[8], uint3
             const uint32_t off = 16u * (uint32_t)i;
             x = aad_len - off < 16u ? keep_bytes(in, aad_len - off) : in;
         } else if (data) {
-            const uint32_t r = len - 16u * b, q = b & 3u;
-            const uint4 kq = make_uint4(q == 0 ? ks[0] : q == 1 ? ks[4] : q == 2 ? ks[8] : ks[12],
-                                        q == 0 ? ks[1] : q == 1 ? ks[5] : q == 2 ? ks[9] : ks[13],
-                                        q == 0 ? ks[2] : q == 1 ? ks[6] : q == 2 ? ks[10] : ks[14],
-                                        q == 0 ? ks[3] : q == 1 ? ks[7] : q == 2 ? ks[11] : ks[15]);
+            const uint32_t r = len - 16u * b;
             uint4 out = in ^ kq;
             if (r >= 16u) {
                 st16(pay + 16u * b, out);
@@ -248,15 +299,6 @@ __device__ __forceinline__ void chacha_wave_packet(const uint32_t (&k)[8], uint3
         const P130 xb = p_block(x, hib);
         if (kk == 0) {
             acc = xb;
-            // Poly1305 key to every lane (pad == 0: no idle lane in pass 0, so every lane computes block 0)
-            if (pad) {
-                pk0 = shfl4(pk0, (int)pad - 1);
-                pk1 = shfl4(pk1, (int)pad - 1);
-            } else {
-                chacha_block(k, 0, n0, n1, n2, ks);
-                pk0 = make_uint4(ks[0], ks[1], ks[2], ks[3]);
-                pk1 = make_uint4(ks[4], ks[5], ks[6], ks[7]);
-            }
             Poly1305 key_r;
             key_r.init(pk0.x, pk0.y, pk0.z, pk0.w);
             rp[0] = P130{key_r.r0, key_r.r1, key_r.r2, key_r.r3, key_r.r4};

@@ -280,7 +280,11 @@ __device__ __forceinline__ void burst_packet(const AesLds &aes, const DevKey *__
         const uint4 smp = make_uint4(__builtin_amdgcn_alignbyte(c0.y, c0.x, sh), __builtin_amdgcn_alignbyte(c0.z, c0.y, sh),
                                      __builtin_amdgcn_alignbyte(c0.w, c0.z, sh), __builtin_amdgcn_alignbyte(c1.x, c0.w, sh));
         const uint4 smp0 = s_off == 0u ? c0 : smp;  // pn_len 4: the sample is block 0
-        hmask = aes.encrypt_lrk<HNR>(smp0, hp_lds);
+        // (split over each quad: a quarter of the block's lookups per lane, next to the lane tree's table reads)
+        const uint32_t q = lane & 3u;
+        const uint32_t col = aes.encrypt_quad<HNR>(q == 0 ? smp0.x : q == 1 ? smp0.y : q == 2 ? smp0.z : smp0.w, hp_lds, q);
+        hmask = make_uint4((uint32_t)__builtin_amdgcn_mov_dpp((int)col, 0x00, 0xf, 0xf, false),
+                           (uint32_t)__builtin_amdgcn_mov_dpp((int)col, 0x55, 0xf, 0xf, false), 0u, 0u);
     }
     // lane tree: level t combines lanes l and l + 2^t (l a multiple of 2^(t+1)) as v_l * H^(2^t) ^ v_(l+2^t)
 #pragma unroll
@@ -456,9 +460,11 @@ __device__ __forceinline__ void txs_mask_item(const AesLds &aes, const qpp_pkt &
         for (int i = 0; i < 8; i++) hk[i] = lds_ld32(kTxsMaskKey + 16 + 4 * i);
         m0 = chacha_hp_quad(hk, smp, lane & 3u, &m1);
     } else {
-        const uint4 m = hp_nr == 14 ? aes.encrypt_lrk<14>(smp, kTxsMaskKey + 16) : aes.encrypt_lrk<10>(smp, kTxsMaskKey + 16);
-        m0 = m.x;
-        m1 = m.y;
+        const uint32_t q = lane & 3u, in = q == 0 ? smp.x : q == 1 ? smp.y : q == 2 ? smp.z : smp.w;
+        const uint32_t col = hp_nr == 14 ? aes.encrypt_quad<14>(in, kTxsMaskKey + 16, q)
+                                         : aes.encrypt_quad<10>(in, kTxsMaskKey + 16, q);
+        m0 = (uint32_t)__builtin_amdgcn_mov_dpp((int)col, 0x00, 0xf, 0xf, false);
+        m1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)col, 0x55, 0xf, 0xf, false);
     }
     if (lane == 0) {
         uint8_t *o = ring + d.off + 16;

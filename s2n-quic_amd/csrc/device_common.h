@@ -142,6 +142,27 @@ struct AesLds {
                           last(s[2], s[3], s[0], s[1], rk[2]), last(s[3], s[0], s[1], s[2], rk[3]));
     }
 
+    // One block over the 4 lanes of a quad (every lane of every quad active, the same block in a quad): lane s holds
+    // column s of the state and takes columns s + 1, s + 2, s + 3 from its neighbours by DPP quad_perm each round, so
+    // it does one column's 4 lookups instead of the block's 16; round keys from LDS at o (word s of each round).
+    // Returns column s of E(in) (in: column s of the plaintext block).
+    template <int NR>
+    __device__ __forceinline__ uint32_t encrypt_quad(uint32_t in, uint32_t o, uint32_t s) const {
+        auto nb = [](uint32_t v, auto ctrl) {
+            return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, decltype(ctrl)::value, 0xf, 0xf, false);
+        };
+        using R1 = std::integral_constant<int, 0x39>;  // lane s reads s + 1
+        using R2 = std::integral_constant<int, 0x4e>;  // s + 2
+        using R3 = std::integral_constant<int, 0x93>;  // s + 3
+        uint32_t x = in ^ lds_ld32(o + 4u * s);
+#pragma unroll
+        for (int r = 1; r < NR; r++) {
+            const uint32_t b = nb(x, R1{}), c = nb(x, R2{}), d = nb(x, R3{});
+            x = col(x, b, c, d, lds_ld32(o + 16u * (uint32_t)r + 4u * s));
+        }
+        const uint32_t b = nb(x, R1{}), c = nb(x, R2{}), d = nb(x, R3{});
+        return last(x, b, c, d, lds_ld32(o + 16u * (uint32_t)NR + 4u * s));
+    }
     // Full AES of one block with the round keys in LDS at byte offset o (read where used: no 44 / 60 registers held)
     template <int NR>
     __device__ __forceinline__ uint4 encrypt_lrk(uint4 in, uint32_t o) const {

@@ -44,7 +44,10 @@ __device__ __forceinline__ uint32_t tab(int t) { return kBurstGh + (uint32_t)t *
 // and on the pinned ring every scratch reload after the first payload stores waited for their PCIe round trip.
 // 8 positions in flight still keep the LDS pipe busy (16 b128 reads issue in 64 cycles, about its latency).
 __device__ __forceinline__ uint4 gmul(uint32_t base, uint4 z) {
-    constexpr int D = 8;
+#ifndef QPP_GMUL_DEPTH
+#define QPP_GMUL_DEPTH 8  // (12, and either without the schedule barriers: the same server latency, profiles/r04s)
+#endif
+    constexpr int D = QPP_GMUL_DEPTH;
     const uint32_t w[4] = {z.x, z.y, z.z, z.w};
     uint4 hi[D], lo[D], acc[4];
     auto issue = [&](auto kc) {
@@ -56,7 +59,9 @@ __device__ __forceinline__ uint4 gmul(uint32_t base, uint4 z) {
     static_for<D>([&](auto kc) { issue(kc); });
     static_for<16>([&](auto kc) {
         constexpr int k = decltype(kc)::value;
+#if !defined(QPP_GMUL_FREE)
         __builtin_amdgcn_sched_barrier(0);
+#endif
         acc[k & 3] = k < 4 ? hi[k % D] ^ lo[k % D] : xor3(acc[k & 3], hi[k % D], lo[k % D]);
         if constexpr (k + D < 16) issue(std::integral_constant<int, k + D>{});
     });

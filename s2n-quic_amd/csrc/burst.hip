@@ -133,7 +133,9 @@ constexpr uint32_t kTxsTrace = kTxsKey + 512;  // QPP_TXS_TRACE: wave 0's stamps
 // header-protection mask items (kTxsMaskNr): their key's record header (suite, nr, hp_nr, live) and HP round keys,
 // apart from the packet key above so that a mask between two seals of one key costs that key nothing
 constexpr uint32_t kTxsMaskKey = kTxsTrace + 32;
-constexpr uint32_t kTxsLds = kTxsMaskKey + 256;
+// two-wave per-packet items (txs_two_wave): wave 1's 64 GHASH accumulators, then wave 0's tag verdict
+constexpr uint32_t kTxsXchg = kTxsMaskKey + 256;
+constexpr uint32_t kTxsLds = kTxsXchg + 1024 + 16;
 static_assert(kTxsStopFlag + 4 <= kTxsKey && kTxsLds <= kLdsMax && kBurstWaves == (int)kTxsWaves, "server LDS");
 #ifndef QPP_TXS_TRACE
 #define QPP_TXS_TRACE 0  // 1: workgroup 0 stamps its phases into the mailbox (tools/diag/server_trace.py)
@@ -478,6 +480,109 @@ __device__ __forceinline__ void txs_mask_item(const AesLds &aes, const qpp_pkt &
     }
 }
 
+// A per-packet item (seal without HP, or open) of a packet of one or two 64-block passes, one wave per pass: wave w
+// runs pass w (one AES chain each instead of a pair interleaved on one wave -- for one pass burst_packet computes a
+// discarded second chain -- the chain is issue-bound on a single wave); with two passes wave 1 hands its lanes' GHASH
+// accumulators over LDS and wave 0 combines them (acc0 * H^64 + acc1, the Horner step of the pair); wave 0 runs the
+// lane tree and the tag.  Opening: wave 0's verdict goes back over LDS and each wave zeroes the plaintext it
+// wrote (a wave's own stores stay ordered).  Every wave of the workgroup calls it (one or two barriers).
+template <int NR, bool SEAL>
+__device__ __forceinline__ void txs_two_wave(const AesLds &aes, const qpp_pkt &d, uint32_t wave, uint8_t *ring,
+                                             int8_t *status) {
+    const uint32_t lane = threadIdx.x & 63u;
+    uint8_t *base = ring + d.off;
+    const uint32_t aad_len = d.aad_len, len = d.pt_len;
+    uint8_t *pay = base + aad_len;
+    const uint32_t a = (aad_len + 15u) >> 4, c = (len + 15u) >> 4, m = a + c + 1, K = m > 64u ? 2u : 1u,
+                   pad = 64u * K - m;
+    const uint32_t n0 = lds_ld32(kTxsKey), n1 = lds_ld32(kTxsKey + 4) ^ bswap32((uint32_t)(d.pn >> 32)),
+                   n2 = lds_ld32(kTxsKey + 8) ^ bswap32((uint32_t)d.pn);  // Iv::nonce (src/iv.rs:27-39)
+    const uint32_t k = wave;  // this wave's pass (waves >= 2: none)
+    const int i = (int)(lane + 64u * k) - (int)pad;
+    const bool data = i >= (int)a && i < (int)(a + c), aadb = i >= 0 && i < (int)a;
+    const uint32_t b = (uint32_t)i - a;
+    uint4 acc = make_uint4(0, 0, 0, 0), ek = acc, want = acc;
+    if (wave < K) {
+        uint4 raw = make_uint4(0, 0, 0, 0);
+        if (data) raw = ld16(pay + 16u * b);
+        else if (aadb) raw = ld16(base + 16u * (uint32_t)i);
+        if (!SEAL && wave == 0 && lane == 0) want = ld16(pay + len);
+        // AES of the lane's counter block (data block b: counter b + 2; every other lane J0 = counter 1)
+        uint32_t kk[4], kn[4];
+        auto rkey = [&](int r, uint32_t (&o)[4]) {
+            uint32_t off = kTxsKey + 16u + 16u * (uint32_t)r;
+            asm volatile("" : "+v"(off));
+            const uint4 v = lds_ld128(off);
+            o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+        };
+        rkey(0, kk);
+        rkey(1, kn);
+        const uint32_t ctr = bswap32(data ? b + 2u : 1u);
+        uint32_t st[4] = {n0 ^ kk[0], n1 ^ kk[1], n2 ^ kk[2], ctr ^ kk[3]};
+#pragma unroll
+        for (int r = 1; r < NR; r++) {
+#pragma unroll
+            for (int q = 0; q < 4; q++) kk[q] = kn[q];
+            rkey(r + 1, kn);
+            aes.round(st, kk);
+        }
+        const uint4 ks = aes.final(st, kn);
+        if (wave == 0 && i == -1) ek = ks;  // E_K(J0) from the idle lane pad - 1 of pass 0
+        uint4 x = make_uint4(0, 0, 0, 0);
+        if (aadb) {
+            const uint32_t off = 16u * (uint32_t)i;
+            x = aad_len - off < 16u ? keep_bytes(raw, aad_len - off) : raw;
+        } else if (data) {
+            const uint32_t r = len - 16u * b;
+            uint4 in = raw, out = raw ^ ks;
+            if (r >= 16u) {
+                st16(pay + 16u * b, out);
+            } else {
+                out = keep_bytes(out, r);
+                in = keep_bytes(in, r);
+                st_bytes(pay + 16u * b, out, r);
+            }
+            x = SEAL ? out : in;
+        } else if (i == (int)m - 1) {
+            x = make_uint4(0, bswap32(aad_len * 8u), 0, bswap32(len * 8u));  // be64 bit lengths
+        }
+        acc = x;
+        if (wave == 1) lds_st128(kTxsXchg + 16u * lane, acc);
+    }
+    __syncthreads();
+    bool ok = true;
+    if (wave == 0) {
+        if (K == 2) acc = gmul(tab(6), acc) ^ lds_ld128(kTxsXchg + 16u * lane);  // the pair's Horner step
+#pragma unroll
+        for (int t = 0; t < 6; t++) acc = gmul(tab(t), acc) ^ shfl4_down(acc, 1u << t);
+        const uint4 ek0 = pad ? shfl4(ek, (int)pad - 1)
+                              : aes.encrypt_lrk<NR>(make_uint4(n0, n1, n2, bswap32(1u)), kTxsKey + 16u);
+        const uint4 tag = shfl4(gmul(tab(0), acc), 0) ^ ek0;
+        if constexpr (SEAL) {
+            if (lane == 0) {
+                st16(pay + len, tag);
+                status[0] = QPP_OK;
+            }
+        } else {
+            const uint4 diff = tag ^ shfl4(want, 0);
+            ok = (diff.x | diff.y | diff.z | diff.w) == 0;  // all 16 bytes compared
+            if (lane == 0) {
+                lds_st32(kTxsXchg + 1024u, ok ? 1u : 0u);
+                status[0] = ok ? QPP_OK : QPP_DECRYPT_ERROR;
+            }
+        }
+    }
+    if constexpr (!SEAL) {
+        __syncthreads();
+        ok = lds_ld32(kTxsXchg + 1024u) != 0;
+        if (!ok && wave < K && data) {  // never release unauthenticated plaintext: each wave zeroes its own blocks
+            const uint32_t r = len - 16u * b;
+            if (r >= 16u) st16(pay + 16u * b, make_uint4(0, 0, 0, 0));
+            else st_bytes(pay + 16u * b, make_uint4(0, 0, 0, 0), r);
+        }
+    }
+}
+
 // one 16-byte chunk of the slot (lane < kTxsPollLanes), in ONE load past every cache (sc0 sc1: the host writes it;
 // a chunk is read whole, so its tag vouches for its other words)
 __device__ __forceinline__ uint4 txs_poll(const TxsSlot *slot, uint32_t lane) {
@@ -619,6 +724,32 @@ __global__ __launch_bounds__(kBurstWG) void txq_server_kernel(const DevKey *keys
             // launched path's kernels refuse them)
             const uint32_t k_suite = lds_ld32(kTxsKeyHdr), k_nr = lds_ld32(kTxsKeyHdr + 4),
                            k_live = lds_ld32(kTxsKeyHdr + 12);
+            if (first && w.count == 1 && k_live == 1 && k_nr == w.nr && (w.nr == 10 || w.nr == 14)) {
+                // a per-packet seal / open of a packet of one or two 64-block passes: a wave per pass (txs_two_wave).  Every
+                // wave decides from wave 0's descriptor (the slot copy in LDS), so all take the same branch.
+                const uint4 da = lds_ld128(kTxsCtl + 32), db = lds_ld128(kTxsCtl + 48);
+                qpp_pkt dd;
+                dd.pn = (uint64_t)da.x | (uint64_t)da.y << 32;
+                dd.key_idx = da.z;
+                dd.off = db.x;
+                dd.aad_len = (uint16_t)db.y;
+                dd.pt_len = (uint16_t)(db.y >> 16);
+                dd.pn_len = (uint8_t)db.z;
+                dd.flags = (uint8_t)(db.z >> 8);
+                dd.reserved = 0;
+                const uint32_t mm = ((dd.aad_len + 15u) >> 4) + ((dd.pt_len + 15u) >> 4) + 1u;
+                if ((dd.flags & (kTxsPktNoHp | kTxsPktOpen)) && !(dd.flags & QPP_PKT_SKIP) && mm <= 128u) {
+                    const bool open = (dd.flags & kTxsPktOpen) != 0;
+                    if (w.nr == 10) {
+                        if (open) txs_two_wave<10, false>(aes, dd, wave, ring, slot->status);
+                        else txs_two_wave<10, true>(aes, dd, wave, ring, slot->status);
+                    } else {
+                        if (open) txs_two_wave<14, false>(aes, dd, wave, ring, slot->status);
+                        else txs_two_wave<14, true>(aes, dd, wave, ring, slot->status);
+                    }
+                    continue;
+                }
+            }
             if (k_live == 1 && k_nr == w.nr) {
                 if (w.nr == 10) txs_item<10>(aes, key, d, wave, w.count, ring, slot->status);
                 else if (w.nr == 14) txs_item<14>(aes, key, d, wave, w.count, ring, slot->status);

@@ -258,18 +258,29 @@ __device__ __forceinline__ void burst_packet(const AesLds &aes, const DevKey *__
         rkey(0, kk);
         rkey(1, kn);
         uint32_t s0[4] = {c0.x ^ kk[0], c0.y ^ kk[1], c0.z ^ kk[2], c0.w ^ kk[3]};
-        uint32_t s1[4] = {c1.x ^ kk[0], c1.y ^ kk[1], c1.z ^ kk[2], c1.w ^ kk[3]};
+        if (k + 1 < K) {  // (uniform) a pair: two chains interleaved
+            uint32_t s1[4] = {c1.x ^ kk[0], c1.y ^ kk[1], c1.z ^ kk[2], c1.w ^ kk[3]};
 #pragma unroll
-        for (int r = 1; r < NR; r++) {
+            for (int r = 1; r < NR; r++) {
 #pragma unroll
-            for (int i = 0; i < 4; i++) kk[i] = kn[i];
-            rkey(r + 1, kn);
-            aes.round(s0, kk);
-            aes.round(s1, kk);
+                for (int i = 0; i < 4; i++) kk[i] = kn[i];
+                rkey(r + 1, kn);
+                aes.round(s0, kk);
+                aes.round(s1, kk);
+            }
+            const uint4 ks0 = aes.final(s0, kn), ks1 = aes.final(s1, kn);
+            pass(k, r0, ks0);
+            pass(k + 1, r1, ks1);
+        } else {  // the last pass of an odd count alone (the pair computed a discarded second chain)
+#pragma unroll
+            for (int r = 1; r < NR; r++) {
+#pragma unroll
+                for (int i = 0; i < 4; i++) kk[i] = kn[i];
+                rkey(r + 1, kn);
+                aes.round(s0, kk);
+            }
+            pass(k, r0, aes.final(s0, kn));
         }
-        const uint4 ks0 = aes.final(s0, kn), ks1 = aes.final(s1, kn);
-        pass(k, r0, ks0);
-        if (k + 1 < K) pass(k + 1, r1, ks1);
     }
     TXS_STAMP(2);
     // Header protection (seal): the sample (ciphertext || tag)[4 - pn_len, 20 - pn_len) (payload.rs:151-169) lies in

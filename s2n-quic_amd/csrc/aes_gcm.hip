@@ -348,8 +348,8 @@ hipError_t launch_aes_gcm_single(bool seal, const DevKey *keys, const qpp_pkt *d
     if (!n) return hipSuccess;
     const PlanBuffers none{};
     const uint32_t waves = (n + 15) / 16;  // quad layout: 16 packets per wave
-    return launch_aes_gcm_quad(seal, nr, dim3(waves < n_cu ? waves : n_cu), s, keys, descs, none, arena, masks, status,
-                               flags, slot, n);
+    const dim3 grid(waves < n_cu ? waves : n_cu);
+    return launch_aes_gcm_quad(seal, nr, grid, s, keys, descs, none, arena, masks, status, flags, slot, n);
 }
 
 hipError_t launch_aes_gcm_wave(bool seal, const DevKey *keys, const qpp_pkt *descs, const PlanBuffers &pb, uint32_t n,
@@ -384,10 +384,12 @@ hipError_t launch_aes_gcm(bool seal, const DevKey *keys, const qpp_pkt *descs, c
     // one slice per CU (quad.hip); a batch smaller than a wave per CU takes fewer workgroups
     const uint32_t waves = (n + 15) / 16;
     const dim3 grid(waves < n_cu ? waves : n_cu);
-    if (suites & (1u << QPP_SUITE_TLS_AES_128_GCM_SHA256))
-        launch_aes_gcm_quad(seal, 10, grid, s, keys, descs, pb, arena, masks, status, flags, 0xffffffffu, 0);
-    if (suites & (1u << QPP_SUITE_TLS_AES_256_GCM_SHA384))
-        launch_aes_gcm_quad(seal, 14, grid, s, keys, descs, pb, arena, masks, status, flags, 0xffffffffu, 0);
+    const bool a128 = suites & (1u << QPP_SUITE_TLS_AES_128_GCM_SHA256), a256 = suites & (1u << QPP_SUITE_TLS_AES_256_GCM_SHA384);
+    // both sizes in ONE launch when both are live (each workgroup: its AES-128 slice, then its AES-256 slice), not
+    // two serial full-chip launches
+    if (a128 || a256)
+        launch_aes_gcm_quad(seal, a128 && a256 ? 0u : a128 ? 10u : 14u, grid, s, keys, descs, pb, arena, masks, status,
+                            flags, 0xffffffffu, 0);
     return hipGetLastError();
 }
 

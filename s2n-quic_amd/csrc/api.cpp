@@ -19,9 +19,11 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <deque>
 #include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -193,6 +195,37 @@ bool fail(qpp_ctx *ctx, hipError_t e, const char *what) {
 int servers_stop(qpp_ctx *ctx);
 int servers_quiesce(qpp_ctx *ctx);
 uint32_t servers_cu(const qpp_ctx *ctx);
+// ---------------------------------------------------------------- resident servers of a device (process-wide)
+// Persistent server kernels -- transmit-queue servers and the contexts' packet servers -- hold whole CUs while they run,
+// and their streams share the device's greatest-priority hardware queues.  One registry per device, over every context
+// of the process:
+//   * cu_avail counts the workgroups of EVERY resident server of the device, so a full-chip grid -- above all the fused
+//     receive's, whose grid barriers need every workgroup resident at once -- is sized for the CUs really left;
+//   * fused receives of the device run one after another (each waits, device side, for the previous one: two on two
+//     streams would split the CUs and both time out), and a server launch waits for the latest fused receive (a server
+//     starting while a receive's workgroups are being dispatched would take CUs the receive's grid counted on);
+//   * at most GPU_MAX_HW_QUEUES (default 4) servers are resident per device: the runtime maps the streams of one
+//     priority level onto that many hardware queues, and a server launched onto a hardware queue a resident server
+//     holds would wait for that server's idle exit.  A queue finding no free server slot takes the launched path (a
+//     transmit-queue flush) or launches the per-packet kernel (the packet server's callers).
+struct DevServers {
+    std::mutex mu;
+    std::vector<qpp_txq *> queues;  // the persistent queues of every context on the device
+    hipEvent_t rx_tail = nullptr;   // recorded behind the device's latest fused receive
+};
+DevServers &dev_servers(int device) {
+    static DevServers regs[64];
+    return regs[(unsigned)device & 63u];
+}
+uint32_t server_slots() {
+    static const uint32_t n = [] {
+        const char *e = getenv("GPU_MAX_HW_QUEUES");
+        const unsigned long v = e ? strtoul(e, nullptr, 10) : 4ul;
+        return (uint32_t)(v ? std::min(v, 32ul) : 4ul);
+    }();
+    return n;
+}
+uint32_t resident_wgs_locked(const DevServers &r);  // (with qpp_txq below)
 // Key::encrypt / Key::decrypt of one packet through the context's packet server (defined with qpp_txq below);
 // *handled = false: the call is not one the server takes (FIPS seal, packet over kPktRing, server off) -- launch it
 int packet_server_run(const qpp_key *k, bool seal, uint64_t pn, const uint8_t *header, size_t header_len,
@@ -200,7 +233,8 @@ int packet_server_run(const qpp_key *k, bool seal, uint64_t pn, const uint8_t *h
                       bool *handled);
 // HeaderKey::*_header_protection_mask of one sample through the packet server (*handled = false: server off)
 int packet_server_mask(qpp_ctx *ctx, uint32_t slot, const uint8_t *sample, uint8_t mask[5], bool *handled);
-// CUs a full-chip kernel (one workgroup per CU) should size its grid for: those of running servers are taken
+// CUs a full-chip kernel (one workgroup per CU) should size its grid for: those of the device's resident servers --
+// every context's (servers_cu) -- are taken
 uint32_t cu_avail(const qpp_ctx *ctx) {
     const uint32_t r = servers_cu(ctx);
     return ctx->n_cu > r ? ctx->n_cu - r : 1u;
@@ -408,7 +442,8 @@ int ensure_plan(qpp_ctx *ctx, StreamState *st, uint32_t n) {
     HIP_TRY(ctx, hipMalloc(&p.istart, sizeof(uint32_t) * 2 * (kcap + 1)));
     HIP_TRY(ctx, hipMalloc(&p.perm, sizeof(uint32_t) * std::max<uint32_t>(ncap, 1)));
     HIP_TRY(ctx, hipMalloc(&p.work, sizeof(WorkItem) * (plan_max_work(ncap, kcap, kMinPacketsPerItem) + 1)));
-    HIP_TRY(ctx, hipMalloc(&p.n_work, 4 * sizeof(uint32_t)));
+    HIP_TRY(ctx, hipMalloc(&p.n_work, 8 * sizeof(uint32_t)));
+    HIP_TRY(ctx, hipMemsetAsync(p.n_work, 0, 8 * sizeof(uint32_t), st->stream));  // (meta[6] is a running count)
     st->plan_n_cap = ncap;
     st->plan_key_cap = kcap;
     return QPP_OK;
@@ -635,9 +670,21 @@ uint32_t single_aes_slot(const qpp_ctx *ctx) {
 }
 
 // Batch bodies: plan (AES) + kernels on st's stream; keys already flushed.
+// The ChaCha20 kernel of a batch: after a plan that listed the non-AES packets (ChaCha20 keys, refused slots) it visits
+// only those (selection mode); otherwise every packet (AES ones are skipped by each lane)
+hipError_t launch_chacha_batch(const qpp_ctx *ctx, const StreamState *st, bool seal, bool planned, const qpp_pkt *descs,
+                               uint32_t n, uint8_t *arena, uint8_t *masks, int8_t *status, uint32_t flags) {
+    const bool burst = n <= (ctx->burst_max >> kChachaBurstShift);
+    if (planned && !burst && plan_lists_others(n, ctx->key_cap))
+        return launch_chacha_sel_batch(seal, ctx->d_keys, ctx->key_cap, descs, n, arena, masks, status, flags,
+                                       st->plan.perm, st->plan.n_work + 4, st->stream);
+    return launch_chacha(seal, ctx->d_keys, ctx->key_cap, descs, n, arena, masks, status, flags, burst, st->stream);
+}
+
 int enqueue_seal(qpp_ctx *ctx, StreamState *st, const qpp_pkt *descs, uint32_t n, uint8_t *arena, uint8_t *masks,
                  int8_t *status, uint32_t flags, uint32_t *refused = nullptr) {
     hipStream_t s = st->stream;
+    bool planned = false;
     if (!(flags & QPP_ONLY_CHACHA)) RC_TRY(fips_gate(ctx, st, descs, n, status, refused));
     if (!(flags & QPP_ONLY_CHACHA) && (suite_mask(ctx) & kAesSuites)) {
         const AesPath path = aes_path(ctx, n);
@@ -649,17 +696,18 @@ int enqueue_seal(qpp_ctx *ctx, StreamState *st, const qpp_pkt *descs, uint32_t n
             RC_TRY(ensure_plan(ctx, st, n));
             HIP_TRY(ctx, launch_plan(ctx->d_keys, ctx->key_cap, descs, n, st->plan, aes_per_item(ctx, path, n), s));
             HIP_TRY(ctx, launch_aes(ctx, path, true, descs, st->plan, n, arena, masks, status, flags, s));
+            planned = true;
         }
     }
     if (!(flags & QPP_ONLY_AES))
-        HIP_TRY(ctx, launch_chacha(true, ctx->d_keys, ctx->key_cap, descs, n, arena, masks, status, flags,
-                                   n <= (ctx->burst_max >> kChachaBurstShift), s));
+        HIP_TRY(ctx, launch_chacha_batch(ctx, st, true, planned, descs, n, arena, masks, status, flags));
     return QPP_OK;
 }
 
 int enqueue_open(qpp_ctx *ctx, StreamState *st, const qpp_pkt *descs, uint32_t n, uint8_t *arena, int8_t *status,
                  uint32_t flags) {
     hipStream_t s = st->stream;
+    bool planned = false;
     if (!(flags & QPP_ONLY_CHACHA) && (suite_mask(ctx) & kAesSuites)) {
         const AesPath path = aes_path(ctx, n);
         const uint32_t one = path == AesPath::quad ? single_aes_slot(ctx) : UINT32_MAX;
@@ -670,11 +718,11 @@ int enqueue_open(qpp_ctx *ctx, StreamState *st, const qpp_pkt *descs, uint32_t n
             RC_TRY(ensure_plan(ctx, st, n));
             HIP_TRY(ctx, launch_plan(ctx->d_keys, ctx->key_cap, descs, n, st->plan, aes_per_item(ctx, path, n), s));
             HIP_TRY(ctx, launch_aes(ctx, path, false, descs, st->plan, n, arena, nullptr, status, 0, s));
+            planned = true;
         }
     }
     if (!(flags & QPP_ONLY_AES))
-        HIP_TRY(ctx, launch_chacha(false, ctx->d_keys, ctx->key_cap, descs, n, arena, nullptr, status, 0,
-                                   n <= (ctx->burst_max >> kChachaBurstShift), s));
+        HIP_TRY(ctx, launch_chacha_batch(ctx, st, false, planned, descs, n, arena, nullptr, status, 0));
     return QPP_OK;
 }
 
@@ -1459,9 +1507,21 @@ int qpp_unprotect_open_batch(qpp_ctx *ctx, const qpp_rx_pkt *rx, size_t n, uint8
             st->rx_scratch_keys = kc;
         }
         HIP_TRY(ctx, hipMemsetAsync(st->rx_scratch, 0, 4 * (16 + 2 * (size_t)kc), st->stream));
-        const uint32_t grid = std::min<uint32_t>(cu_avail(ctx), std::max<uint32_t>(1, (uint32_t)((n + 191) / 192)));
-        HIP_TRY(ctx, launch_aes_gcm_quad_rx(a256 ? (a128 ? 0u : 14u) : 10u, grid, st->stream, ctx->d_keys, kc, rx, (uint32_t)n, arena, descs_out, status,
-                                            st->rx_scratch, st->plan.perm, ctx->d_diag, chacha));
+        {
+            // The grid barriers need every workgroup resident: the grid is the CUs every resident server of the
+            // device leaves, the device's previous fused receive is waited for (two at once would split the CUs), and
+            // a server launched later waits for this one (srv_start) -- all under the device registry's lock
+            DevServers &r = dev_servers(ctx->device);
+            std::lock_guard<std::mutex> lk(r.mu);
+            if (!r.rx_tail) HIP_TRY(ctx, hipEventCreateWithFlags(&r.rx_tail, hipEventDisableTiming));
+            else HIP_TRY(ctx, hipStreamWaitEvent(st->stream, r.rx_tail, 0));
+            const uint32_t busy = resident_wgs_locked(r), free_cu = ctx->n_cu > busy ? ctx->n_cu - busy : 1u;
+            const uint32_t grid = std::min<uint32_t>(free_cu, std::max<uint32_t>(1, (uint32_t)((n + 191) / 192)));
+            HIP_TRY(ctx, launch_aes_gcm_quad_rx(a256 ? (a128 ? 0u : 14u) : 10u, grid, st->stream, ctx->d_keys, kc, rx,
+                                                (uint32_t)n, arena, descs_out, status, st->rx_scratch, st->plan.perm,
+                                                ctx->d_diag, chacha));
+            HIP_TRY(ctx, hipEventRecord(r.rx_tail, st->stream));
+        }
         if (chacha)
             HIP_TRY(ctx, launch_chacha_sel(ctx->d_keys, kc, descs_out, (uint32_t)n, arena, status, st->plan.perm,
                                            st->rx_scratch + 2, st->stream));
@@ -1817,6 +1877,7 @@ struct qpp_txq {
     qpp_pkt *h_sdesc = nullptr, *v_sdesc = nullptr;
     hipStream_t srv_stream = nullptr;
     bool srv_running = false;           // launched and not yet seen to have ended
+    std::atomic<bool> srv_launched{false};  // the same, readable by other contexts' threads (device registry)
     const DevKey *srv_keys = nullptr;   // the key table the running server reads
     uint32_t srv_seq = 0;               // seq of the last flush or stop written into the slots
     uint32_t srv_posted = 0;            // seq of the last flush posted (0: none)
@@ -1831,12 +1892,26 @@ struct qpp_txq {
 
 namespace {
 
+constexpr int kNoServerSlot = 1000;  // (internal) srv_start: every server slot of the device is taken
+
+// launched and its stream still busy: read-only on the queue, safe for another context's thread (registry lock held)
+bool srv_resident(const qpp_txq *q) {
+    return q->srv_launched.load(std::memory_order_acquire) && hipStreamQuery(q->srv_stream) == hipErrorNotReady;
+}
+uint32_t resident_wgs_locked(const DevServers &r) {
+    uint32_t w = 0;
+    for (const qpp_txq *o : r.queues)
+        if (srv_resident(o)) w += o->srv_wgs;
+    return w;
+}
+
 uint32_t srv_next(uint32_t s) { return s + 1u ? s + 1u : 1u; }  // 0 is never a flush's seq
 
 bool srv_alive(qpp_txq *q) {
     if (!q->srv_running) return false;
     if (hipStreamQuery(q->srv_stream) == hipErrorNotReady) return true;
     q->srv_running = false;  // it ended on its own (idle timeout), or failed (the next launch reports that)
+    q->srv_launched.store(false, std::memory_order_release);
     return false;
 }
 
@@ -1849,17 +1924,30 @@ bool srv_done(const qpp_txq *q, uint32_t seq) {
     return true;
 }
 
-int srv_start(qpp_txq *q) {
+// force: a posted flush waits for this server (srv_wait's restart), so it starts even past the device's server slots
+int srv_start(qpp_txq *q, bool force = false) {
     // (no stream query while the server is believed running: a server that left on its idle timeout is found by
     // srv_wait's slow path, which relaunches it behind the posted flush)
     if (q->srv_running) return QPP_OK;
     qpp_ctx *ctx = q->ctx;
+    DevServers &r = dev_servers(ctx->device);
+    std::lock_guard<std::mutex> lk(r.mu);
+    if (!force) {
+        uint32_t n = 0;
+        for (const qpp_txq *o : r.queues)
+            if (o != q && srv_resident(o)) n++;
+        if (n >= server_slots()) return kNoServerSlot;
+    }
+    // behind the device's latest fused receive (its grid did not count this server's CUs)
+    if (r.rx_tail) HIP_TRY(ctx, hipStreamWaitEvent(q->srv_stream, r.rx_tail, 0));
     const bool pending = q->srv_posted && !srv_done(q, q->srv_posted);
     const uint32_t seq0 = pending ? q->srv_posted - 1u : q->srv_seq;
     HIP_TRY(ctx, launch_txq_server(ctx->d_keys, ctx->pow, q->v_mail, q->v_slots, q->v_items, q->v_sdesc, q->v_ring,
                                    seq0, q->srv_idle_ticks, q->srv_wgs, q->srv_stream));
     q->srv_running = true;
+    q->srv_launched.store(true, std::memory_order_release);
     q->srv_keys = ctx->d_keys;
+    q->srv_last_post = std::chrono::steady_clock::now();  // (its idle clock starts now)
     q->n_starts++;
     return QPP_OK;
 }
@@ -1871,7 +1959,7 @@ int srv_wait(qpp_txq *q, uint32_t seq) {
     for (uint64_t spin = 0;; spin++) {
         if (srv_done(q, seq)) return QPP_OK;
         if ((spin & 4095u) == 4095u) {
-            if (!srv_alive(q)) RC_TRY(srv_start(q));  // it left (idle) before this flush was seen: a new one takes it
+            if (!srv_alive(q)) RC_TRY(srv_start(q, true));  // it left (idle) before this flush was seen: a new one takes it
             const auto now = std::chrono::steady_clock::now();
             if (spin == 4095u) t0 = now;
             else if (now - t0 > std::chrono::seconds(10)) {
@@ -1894,6 +1982,7 @@ int srv_stop(qpp_txq *q) {
     }
     HIP_TRY(q->ctx, hipStreamSynchronize(q->srv_stream));
     q->srv_running = false;
+    q->srv_launched.store(false, std::memory_order_release);
     return QPP_OK;
 }
 
@@ -1905,11 +1994,10 @@ int servers_quiesce(qpp_ctx *ctx) {
     for (qpp_txq *q : ctx->servers) RC_TRY(srv_wait(q, q->srv_posted));
     return QPP_OK;
 }
-uint32_t servers_cu(const qpp_ctx *ctx) {
-    uint32_t r = 0;
-    for (qpp_txq *q : ctx->servers)
-        if (srv_alive(q)) r += q->srv_wgs;
-    return r;
+uint32_t servers_cu(const qpp_ctx *ctx) {  // every resident server of the device, any context
+    DevServers &r = dev_servers(ctx->device);
+    std::lock_guard<std::mutex> lk(r.mu);
+    return resident_wgs_locked(r);
 }
 
 }  // namespace
@@ -1994,6 +2082,11 @@ void qpp_txq_destroy(qpp_txq *q) {
         srv_stop(q);
         std::vector<qpp_txq *> &v = q->ctx->servers;
         v.erase(std::remove(v.begin(), v.end(), q), v.end());
+        {
+            DevServers &r = dev_servers(q->ctx->device);
+            std::lock_guard<std::mutex> lk(r.mu);
+            r.queues.erase(std::remove(r.queues.begin(), r.queues.end(), q), r.queues.end());
+        }
         if (q->srv_stream) { hipStreamSynchronize(q->srv_stream); hipStreamDestroy(q->srv_stream); }
         if (q->h_mail) hipHostFree(q->h_mail);
         if (q->h_slots) { secure_zero(q->h_slots, sizeof(TxsSlot) * q->srv_wgs); hipHostFree(q->h_slots); }
@@ -2165,12 +2258,11 @@ static int srv_prepare(qpp_txq *q, std::chrono::steady_clock::time_point now) {
     return QPP_OK;
 }
 
-static int srv_submit(qpp_txq *q) {
+// (the caller ran srv_prepare and started the server)
+static int srv_submit(qpp_txq *q, std::chrono::steady_clock::time_point now) {
     qpp_ctx *ctx = q->ctx;
     TxqSlot &sl = q->slots[q->cur];
     const uint32_t n = (uint32_t)q->count;
-    const auto now = std::chrono::steady_clock::now();
-    RC_TRY(srv_prepare(q, now));
     const uint32_t W = kTxsWaves;
     std::vector<uint32_t> &ord = q->order;
     ord.resize(n);
@@ -2197,7 +2289,6 @@ static int srv_submit(qpp_txq *q) {
         }
         i = j;
     }
-    RC_TRY(srv_start(q));
     q->srv_seq = srv_next(q->srv_seq);
     const uint32_t seq = q->srv_seq, word = (q->srv_epoch << 24) | items;
     // each workgroup's slot: its first item and that item's descriptors, every 16-byte chunk tagged, then the seq (x86
@@ -2240,7 +2331,16 @@ static int txq_submit(qpp_txq *q) {
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     RC_TRY(flush_keys(ctx));
     if (q->persistent) {
-        if (!ctx->fips_live) return srv_submit(q);
+        if (!ctx->fips_live) {
+            const auto now = std::chrono::steady_clock::now();
+            RC_TRY(srv_prepare(q, now));
+            const int rc = srv_start(q);
+            if (rc != kNoServerSlot) {
+                RC_TRY(rc);
+                return srv_submit(q, now);
+            }
+            // every server slot of the device is taken: this flush is launched (the same bytes)
+        }
         // FIPS gating takes the launched path (its nonce-order gate), behind the posted flush
         RC_TRY(srv_wait(q, q->srv_posted));
     }
@@ -2385,6 +2485,11 @@ static int txq_create_server(qpp_ctx *ctx, size_t ring_bytes, size_t max_packets
     };
     q->persistent = true;
     ctx->servers.push_back(q);
+    {
+        DevServers &r = dev_servers(ctx->device);
+        std::lock_guard<std::mutex> lk(r.mu);
+        r.queues.push_back(q);
+    }
     const size_t W = kTxsWaves;
     void *v = nullptr;
     if (bad(hipHostMalloc(&q->h_mail, sizeof(TxsMail), fl), "txq server mailbox") ||
@@ -2474,6 +2579,12 @@ namespace {
 // workgroups' LDS), sealed without header protection or opened in place there, and copied back.  No launch, no
 // runtime call: the cost is the post's PCIe round trip, the packet's own read / AES / GHASH / write chain and the copies.
 constexpr size_t kPktRing = 16384;  // header + payload + tag; longer packets take the launched path
+// zeroes the packet server's ring bytes of a call on every exit path (an early return left plaintext there)
+struct RingWipe {
+    uint8_t *p;
+    size_t n;
+    ~RingWipe() { secure_zero(p, n); }
+};
 constexpr uint32_t kPktWgs = 4;
 
 // Posts one work item of one packet (ring offset 0) to workgroup wg of the packet server -- every other workgroup an
@@ -2481,7 +2592,7 @@ constexpr uint32_t kPktWgs = 4;
 // what the item names).
 int srv_post_one(qpp_txq *q, std::chrono::steady_clock::time_point now, uint32_t wg, uint32_t slot, uint32_t nr,
                  uint64_t pn, uint32_t lens, uint32_t misc) {
-    RC_TRY(srv_start(q));
+    RC_TRY(srv_start(q, true));  // (the caller found it a server slot)
     q->srv_seq = srv_next(q->srv_seq);
     const uint32_t seq = q->srv_seq;
     const uint32_t word = (q->srv_epoch << 24) | q->srv_wgs;  // item b for workgroup b; all but one empty
@@ -2532,7 +2643,11 @@ int packet_server_run(const qpp_key *k, bool seal, uint64_t pn, const uint8_t *h
     RC_TRY(flush_keys(ctx));
     const auto now = std::chrono::steady_clock::now();
     RC_TRY(srv_prepare(q, now));
+    const int rc = srv_start(q);
+    if (rc == kNoServerSlot) return QPP_OK;  // every server slot of the device is taken: the caller launches it
+    RC_TRY(rc);
     uint8_t *r = q->h_ring;
+    RingWipe wipe{r, total};  // the plaintext never stays in the host-visible ring, whatever the exit path
     if (header_len) memcpy(r, header, header_len);
     if (payload_len) memcpy(r + header_len, payload, payload_len);
     if (!seal) memcpy(r + header_len + payload_len, tag_out, 16);
@@ -2545,7 +2660,6 @@ int packet_server_run(const qpp_key *k, bool seal, uint64_t pn, const uint8_t *h
         memcpy(out, r + header_len, payload_len);
         if (seal) memcpy(tag_out, r + header_len + payload_len, 16);
     }
-    secure_zero(r, total);
     return QPP_OK;
 }
 
@@ -2563,12 +2677,15 @@ int packet_server_mask(qpp_ctx *ctx, uint32_t slot, const uint8_t *sample, uint8
     RC_TRY(flush_keys(ctx));
     const auto now = std::chrono::steady_clock::now();
     RC_TRY(srv_prepare(q, now));
+    const int rc = srv_start(q);
+    if (rc == kNoServerSlot) return QPP_OK;  // every server slot of the device is taken: the caller launches it
+    RC_TRY(rc);
     uint8_t *r = q->h_ring;
+    RingWipe wipe{r, 32};
     memcpy(r, sample, 16);
     memset(r + 16, 0, 16);
     RC_TRY(srv_post_one(q, now, slot % q->srv_wgs, slot, kTxsMaskNr, 0, 16, 0));
     memcpy(mask, r + 16, 5);
-    secure_zero(r, 32);
     *handled = true;
     return QPP_OK;
 }

@@ -34,8 +34,9 @@ __device__ __forceinline__ uint32_t chacha_rho(uint32_t p) { return (p + (p >> 4
 // RX (open only): the fused receive path for a context with no live AES record -- each lane first unprotects its
 // packet of rx[] (rx_unprotect_one: HP removal, PN expansion, key phase; ChaCha20 header keys only), writes the
 // qpp_pkt to descs_out and opens it with the key the phase picked.  Same outputs as unprotect_kernel + this kernel.
-// Selection mode (sel != nullptr, open only): the packets are descs[sel[sel_meta[1] + i]], i < min(n, sel_meta[0]) --
-// the ChaCha20 packets the fused receive kernel (quad.hip) sorted behind its AES packets, their count on the device.
+// Selection mode (sel != nullptr): the packets are descs[sel[sel_meta[1] + i]], i < min(n, sel_meta[0]) -- the ChaCha20
+// packets the fused receive kernel (quad.hip) sorted behind its AES packets, or the non-AES packets a batch's plan
+// listed behind its AES packets (plan.hip), their count on the device.
 template <bool SEAL, bool RX = false>
 __global__ __launch_bounds__(256, 3) void chacha_kernel(const DevKey *__restrict__ keys, uint32_t key_cap,
                                                     const qpp_pkt *__restrict__ descs, uint32_t n,
@@ -345,6 +346,21 @@ hipError_t launch_chacha_sel(const DevKey *keys, uint32_t key_cap, const qpp_pkt
     const uint32_t lds = 4u * kChachaWaveLds;
     hipLaunchKernelGGL((chacha_kernel<false, false>), grid, block, lds, s, keys, key_cap, descs, n_max, arena, nullptr,
                        status, 0u, nullptr, nullptr, sel, sel_meta);
+    return hipGetLastError();
+}
+
+hipError_t launch_chacha_sel_batch(bool seal, const DevKey *keys, uint32_t key_cap, const qpp_pkt *descs, uint32_t n_max,
+                                   uint8_t *arena, uint8_t *masks, int8_t *status, uint32_t flags, const uint32_t *sel,
+                                   const uint32_t *sel_meta, hipStream_t s) {
+    if (!n_max) return hipSuccess;
+    const dim3 grid((n_max + 255) / 256), block(256);
+    const uint32_t lds = 4u * kChachaWaveLds;
+    if (seal)
+        hipLaunchKernelGGL((chacha_kernel<true, false>), grid, block, lds, s, keys, key_cap, descs, n_max, arena, masks,
+                           status, flags, nullptr, nullptr, sel, sel_meta);
+    else
+        hipLaunchKernelGGL((chacha_kernel<false, false>), grid, block, lds, s, keys, key_cap, descs, n_max, arena, nullptr,
+                           status, 0u, nullptr, nullptr, sel, sel_meta);
     return hipGetLastError();
 }
 

@@ -4,7 +4,9 @@
 //   1. plan_hist   : packets per key (LDS-privatised counts, one global add per touched key per block)
 //   2. plan_scan   : one workgroup: key offsets, work list {key, begin, count<=per, rounds}, n_work
 //   3. plan_scatter: perm[] = packet indices grouped by key (LDS ranks + one global reservation per key)
-// ChaCha20-Poly1305 packets are skipped (their kernel needs no grouping).
+// Every other packet (ChaCha20-Poly1305 keys, refused slots) goes, ungrouped, behind the AES packets in perm[] (round
+// 5): the ChaCha20 kernel then visits only those (selection mode) instead of every packet of a mixed batch -- its lane
+// per packet idled on the AES packets, so a third of ChaCha packets cost a whole ChaCha batch.
 // The reference has no batching at all (Key::encrypt is per packet); this is the
 // batch former the MI355X design adds in front of the kernels.
 #include "device_common.h"
@@ -25,11 +27,13 @@ __device__ __forceinline__ bool is_aes(const DevKey *keys, uint32_t k) {
 // key_cap <= kMaxPlanKeys: bins in LDS.  Larger key tables use global atomics directly.
 __global__ __launch_bounds__(kPlanBlock) void plan_hist(const DevKey *__restrict__ keys, uint32_t key_cap,
                                                        const qpp_pkt *__restrict__ descs, uint32_t n,
-                                                       uint32_t *__restrict__ counts) {
+                                                       uint32_t *__restrict__ counts, uint32_t *__restrict__ meta) {
     __shared__ uint32_t bins[kMaxPlanKeys];
+    __shared__ uint32_t others;
     const bool local = key_cap <= (uint32_t)kMaxPlanKeys;
     if (local)
         for (uint32_t i = threadIdx.x; i < key_cap; i += blockDim.x) bins[i] = 0;
+    if (threadIdx.x == 0) others = 0;
     __syncthreads();
 #pragma unroll
     for (uint32_t j = 0; j < kPlanPerThread; j++) {
@@ -51,11 +55,15 @@ __global__ __launch_bounds__(kPlanBlock) void plan_hist(const DevKey *__restrict
             if (local) atomicAdd(&bins[k], 1u);
             else atomicAdd(&counts[k], 1u);
         }
+        // the other packets (not a live AES key): one count for all of them
+        const uint64_t other = __ballot(pi < n && k == ~0u);
+        if (other && (threadIdx.x & 63u) == 0) atomicAdd(&others, (uint32_t)__popcll(other));
     }
     __syncthreads();
     if (local)
         for (uint32_t i = threadIdx.x; i < key_cap; i += blockDim.x)
             if (bins[i]) atomicAdd(&counts[i], bins[i]);
+    if (threadIdx.x == 0 && others) atomicAdd(&meta[6], others);
 }
 
 // Single workgroup.  Exclusive scans over keys of (a) packet counts -> cursor (scatter base per key) and
@@ -63,7 +71,8 @@ __global__ __launch_bounds__(kPlanBlock) void plan_hist(const DevKey *__restrict
 // search of istart (in LDS), so a single key with 16 Ki work items is not written by one lane.
 // Class-major: the AES-128 keys' packets and items come first, then the AES-256 keys' (two scans), so each AES size's
 // launch sees one contiguous range of perm and of the work list.  meta = {items, AES-128 items, AES-128 packets,
-// AES-256 packets}.
+// AES-256 packets, other packets, their first perm index, [6] the other packets' count (plan_hist; zeroed here after
+// its read), [7] their scatter cursor (plan_scatter)}.
 __global__ __launch_bounds__(kPlanBlock) void plan_scan(const DevKey *__restrict__ keys, uint32_t key_cap,
                                                        uint32_t *__restrict__ counts, uint32_t *__restrict__ cursor,
                                                        uint32_t *__restrict__ istart_g, WorkItem *__restrict__ work,
@@ -105,7 +114,10 @@ __global__ __launch_bounds__(kPlanBlock) void plan_scan(const DevKey *__restrict
         __syncthreads();
     }
     const uint32_t total = cls_i[1], i10 = cls_i[0];
-    if (threadIdx.x == 0) { meta[0] = total; meta[1] = i10; meta[2] = cls_c[0]; meta[3] = cls_c[1] - cls_c[0]; }
+    if (threadIdx.x == 0) {
+        meta[0] = total; meta[1] = i10; meta[2] = cls_c[0]; meta[3] = cls_c[1] - cls_c[0];
+        meta[4] = meta[6]; meta[5] = cls_c[1]; meta[6] = 0; meta[7] = cls_c[1];
+    }
     for (uint32_t w = threadIdx.x; w < total; w += kPlanBlock) {
         const uint32_t *ist = istart + (w >= i10 ? key_cap + 1 : 0);
         uint32_t lo = 0, hi = key_cap;  // largest k with ist[k] <= w (keys with no items share a start)
@@ -126,14 +138,17 @@ __global__ __launch_bounds__(kPlanBlock) void plan_scan(const DevKey *__restrict
 
 __global__ __launch_bounds__(kPlanBlock) void plan_scatter(const DevKey *__restrict__ keys, uint32_t key_cap,
                                                           const qpp_pkt *__restrict__ descs, uint32_t n,
-                                                          uint32_t *__restrict__ cursor, uint32_t *__restrict__ perm) {
+                                                          uint32_t *__restrict__ cursor, uint32_t *__restrict__ perm,
+                                                          uint32_t *__restrict__ meta) {
     __shared__ uint32_t bins[kMaxPlanKeys];
+    __shared__ uint32_t others;
     const bool local = key_cap <= (uint32_t)kMaxPlanKeys;
     if (local)
         for (uint32_t i = threadIdx.x; i < key_cap; i += blockDim.x) bins[i] = 0;
+    if (threadIdx.x == 0) others = 0;
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
-    uint32_t ks[kPlanPerThread], rank[kPlanPerThread];
+    uint32_t ks[kPlanPerThread], rank[kPlanPerThread], orank[kPlanPerThread];
 #pragma unroll
     for (uint32_t j = 0; j < kPlanPerThread; j++) {
         const uint32_t pi = (blockIdx.x * kPlanPerThread + j) * blockDim.x + threadIdx.x;
@@ -157,8 +172,21 @@ __global__ __launch_bounds__(kPlanBlock) void plan_scatter(const DevKey *__restr
             else perm[atomicAdd(&cursor[k], 1u)] = pi;
         }
         ks[j] = k;
+        // the other packets: a rank in the block's run of them (wave ballot + one LDS add per wave)
+        const bool oth = pi < n && k == 0xffffffffu;
+        const uint64_t ob = __ballot(oth);
+        uint32_t obase = 0;
+        if (ob && lane == 0) obase = atomicAdd(&others, (uint32_t)__popcll(ob));
+        obase = (uint32_t)__shfl((int)obase, 0, 64);
+        orank[j] = oth ? obase + (uint32_t)__popcll(ob & ((1ull << lane) - 1ull)) : 0xffffffffu;
     }
     __syncthreads();
+    // one reservation of the block's run of other packets behind the AES packets (meta[7]: plan_scan set it there)
+    if (threadIdx.x == 0 && others) others = atomicAdd(&meta[7], others);
+    __syncthreads();
+#pragma unroll
+    for (uint32_t j = 0; j < kPlanPerThread; j++)
+        if (orank[j] != 0xffffffffu) perm[others + orank[j]] = (blockIdx.x * kPlanPerThread + j) * blockDim.x + threadIdx.x;
     if (local) {
         // reserve one contiguous range per touched key; reuse bins[] for the range start
         for (uint32_t i = threadIdx.x; i < key_cap; i += blockDim.x)
@@ -278,18 +306,20 @@ uint32_t plan_max_work(uint32_t n, uint32_t key_cap, uint32_t per) {
     return by_packets + by_keys;
 }
 
+bool plan_lists_others(uint32_t n, uint32_t key_cap) { return !(n <= kPlanSmallMax && key_cap <= (uint32_t)kMaxPlanKeys); }
+
 hipError_t launch_plan(const DevKey *keys, uint32_t key_cap, const qpp_pkt *descs, uint32_t n, PlanBuffers pb,
                        uint32_t per, hipStream_t s) {
-    if (n <= kPlanSmallMax && key_cap <= (uint32_t)kMaxPlanKeys) {
+    if (!plan_lists_others(n, key_cap)) {
         hipLaunchKernelGGL(plan_small, dim3(1), dim3(kPlanBlock), kPlanSmallLds, s, keys, key_cap, descs, n, pb.perm,
                            pb.work, pb.n_work, per);
         return hipGetLastError();
     }
     const dim3 grid((n + kPlanBlock * kPlanPerThread - 1) / (kPlanBlock * kPlanPerThread));
-    hipLaunchKernelGGL(plan_hist, grid, dim3(kPlanBlock), 0, s, keys, key_cap, descs, n, pb.counts);
+    hipLaunchKernelGGL(plan_hist, grid, dim3(kPlanBlock), 0, s, keys, key_cap, descs, n, pb.counts, pb.n_work);
     hipLaunchKernelGGL(plan_scan, dim3(1), dim3(kPlanBlock), 0, s, keys, key_cap, pb.counts, pb.cursor, pb.istart, pb.work,
                        pb.n_work, per);
-    hipLaunchKernelGGL(plan_scatter, grid, dim3(kPlanBlock), 0, s, keys, key_cap, descs, n, pb.cursor, pb.perm);
+    hipLaunchKernelGGL(plan_scatter, grid, dim3(kPlanBlock), 0, s, keys, key_cap, descs, n, pb.cursor, pb.perm, pb.n_work);
     return hipGetLastError();
 }
 

@@ -120,7 +120,9 @@ struct PlanBuffers {
     uint32_t *istart;   // [2][key_cap + 1] first work item per key and AES size (used when key_cap > kMaxPlanKeys)
     uint32_t *perm;     // [n_cap] packet indices grouped by key
     WorkItem *work;     // [n_cap / kMinPacketsPerItem + key_cap + 1]
-    uint32_t *n_work;   // [4] plan meta: work items, AES-128 items, AES-128 packets, AES-256 packets
+    uint32_t *n_work;   // [8] plan meta: work items, AES-128 items, AES-128 packets, AES-256 packets, other packets
+                        // (ChaCha20, refused) and their first perm index, and plan-internal [6] count and [7] cursor
+                        // (zero between plans; plan.hip)
 };
 
 // aes_gcm.hip: records[i] (device, may be nullptr = already in place) -> keys[slots[i]], then H / V[m] for AES keys
@@ -134,6 +136,9 @@ hipError_t launch_key_derive(DevKey *keys, const uint32_t *slots, uint32_t n, in
                              const uint8_t *hp_in, uint32_t updates, uint8_t *material, uint32_t fips,
                              const PowTables &pow, hipStream_t s);
 uint32_t key_material_bytes();
+// the plan of an n-packet batch also lists the non-AES packets behind the AES ones (pb.perm[meta[5] ..], meta[4] of
+// them) -- the three-launch plan does, plan_small does not
+bool plan_lists_others(uint32_t n, uint32_t key_cap);
 hipError_t launch_plan(const DevKey *keys, uint32_t key_cap, const qpp_pkt *descs, uint32_t n, PlanBuffers pb,
                        uint32_t per, hipStream_t s);
 uint32_t plan_max_work(uint32_t n, uint32_t key_cap, uint32_t per);
@@ -215,6 +220,10 @@ hipError_t launch_aes_gcm_quad_rx(uint32_t aes, uint32_t grid, hipStream_t s, co
 // chacha.hip: open descs[sel[sel_meta[1] + i]] for i < min(n_max, sel_meta[0]) (count and base on the device)
 hipError_t launch_chacha_sel(const DevKey *keys, uint32_t key_cap, const qpp_pkt *descs, uint32_t n_max,
                              uint8_t *arena, int8_t *status, const uint32_t *sel, const uint32_t *sel_meta, hipStream_t s);
+// the same selection for seal or open of a planned batch (sel = the plan's perm, sel_meta = its meta + 4)
+hipError_t launch_chacha_sel_batch(bool seal, const DevKey *keys, uint32_t key_cap, const qpp_pkt *descs, uint32_t n_max,
+                                   uint8_t *arena, uint8_t *masks, int8_t *status, uint32_t flags, const uint32_t *sel,
+                                   const uint32_t *sel_meta, hipStream_t s);
 hipError_t launch_aes_gcm_quad(bool seal, uint32_t nr, dim3 grid, hipStream_t s, const DevKey *keys,
                                const qpp_pkt *descs, const PlanBuffers &pb, uint8_t *arena, uint8_t *masks,
                                int8_t *status, uint32_t flags, uint32_t single, uint32_t n_single);

@@ -67,8 +67,18 @@ __device__ __forceinline__ void st_payload(uint8_t *p, uint4 v) {
     if (QPP_QUAD_NT) st16_nt(p, v);  // streaming: the sealed / opened bytes are not read again
     else st16(p, v);
 }
-template <int NR>
-constexpr int kQuadWG = NR == 10 ? QPP_QUAD_WG : QPP_QUAD_WG256;
+template <int NR>  // (NR = 0: a launch over both sizes)
+constexpr int kQuadWG = NR == 14 ? QPP_QUAD_WG256 : QPP_QUAD_WG;
+// Counter blocks per lane in one group (a group = 4 QNB slots of the packet per quad).  4: 16 slots = 256 bytes of a
+// packet per group; fewer blocks per group hold fewer registers (the 1024-thread build, 4 waves per SIMD).
+#ifndef QPP_QUAD_NB
+#define QPP_QUAD_NB 4
+#endif
+constexpr int kQNB = QPP_QUAD_NB, kQSG = 4 * kQNB;
+static_assert(kQNB >= 2 && kQNB <= 4, "group size");
+#ifndef QPP_QUAD_HOLD
+#define QPP_QUAD_HOLD 1  // the deferred last chunk of interior groups (0: every chunk stored in its own group)
+#endif
 
 // X * H through the 8-bit tables of H at [0, 64K) (T_j[x] at 256 x + 16 j): the setup's products
 __device__ __forceinline__ uint4 mul_h8(uint4 x) {
@@ -218,12 +228,12 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
     };
     QPage pg;
     pg.build(aes, round_keys(), n0, n1, n2, 0);
-    const int ngroups = has ? (m + 1 + 15) >> 4 : 0;  // counter slots 0 (J0) .. m
+    const int ngroups = has ? (m + kQSG) / kQSG : 0;  // counter slots 0 (J0) .. m
     const int G = (int)wave_max((uint32_t)ngroups);
     const int min_full = (int)__builtin_amdgcn_readfirstlane(wave_min(has ? (uint32_t)nfull : 0u));
-    auto interior = [&](int g) { return g >= 1 && 16 * g + 15 <= min_full; };  // every slot a whole payload block
+    auto interior = [&](int g) { return g >= 1 && kQSG * g + kQSG - 1 <= min_full; };  // every slot a whole payload block
     // counter blocks per lane the last group needs (uniform): the longest packet's slots past 16 (G - 1)
-    const int tail_slots = (int)wave_max(has ? (uint32_t)max(0, m + 1 - 16 * (G - 1)) : 0u);
+    const int tail_slots = (int)wave_max(has ? (uint32_t)max(0, m + 1 - kQSG * (G - 1)) : 0u);
     // length block: be64(aad bits) || be64(payload bits)
     auto lenblk = [&]() { return make_uint4(0, bswap32(aad_len * 8), 0, bswap32(len * 8)); };
     bool len_done = !has;
@@ -260,19 +270,19 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
         hp_done = true;
     };
 
-    // one group: slots t = 16 g + 4 k + s, k < NBG; slot t holds counter t + 1 and ciphertext block t - 1
+    // one group: slots t = kQSG g + 4 k + s, k < NBG; slot t holds counter t + 1 and ciphertext block t - 1
     auto group = [&](auto nbc, int g) __attribute__((always_inline)) {
         constexpr int NBG = decltype(nbc)::value;
-        const bool inner = NBG == 4 && interior(g);  // uniform
+        const bool inner = NBG == kQNB && interior(g);  // uniform
         const RkPtr rkp = round_keys();
-        const int t0 = 16 * g + (int)s;
+        const int t0 = kQSG * g + (int)s;
         uint4 ks[NBG];
         const uint32_t c0 = (uint32_t)t0 + 1u;
         // The nonce words are laundered where the loop uses them (a new page; the straddling group): left alone, the
         // compiler hoisted the page build's first-round lookups addresses out of the loop as loop invariants and
         // spilled them (16 scratch accesses per group in the open kernel).
         uint32_t m0 = n0, m1 = n1, m2 = n2;
-        if ((g & 15) != 15) {  // uniform: no lane's counters straddle a 256-block page
+        if (((kQSG * g + 1) >> 8) == ((kQSG * g + kQSG) >> 8)) {  // uniform: no lane's counters straddle a 256-block page
             if ((c0 >> 8) != pg.page) {
                 asm volatile("" : "+v"(m0), "+v"(m1), "+v"(m2));
                 pg.build(aes, rkp, m0, m1, m2, c0 >> 8);
@@ -325,7 +335,7 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
             if (held_ok) st_payload(at(b - 64), held);
 #pragma unroll
             for (int k = 1; k < NBG - 1; k++) st_payload(at(b + 64 * k), out[k]);
-            held_ok = interior(g + 1) && (g + 1 < G - 1 || tail_slots > 12);  // uniform: the next group is interior
+            held_ok = QPP_QUAD_HOLD && interior(g + 1) && (g + 1 < G - 1 || tail_slots > kQSG - 4);  // uniform: the next group is interior
             if (held_ok) held = out[NBG - 1];
             else st_payload(at(b + 64 * (NBG - 1)), out[NBG - 1]);
 #pragma unroll
@@ -350,13 +360,13 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
         }
         if (SEAL && g == 0) hp_early(out[0]);
     };
-    for (int g = 0; g + 1 < G; g++) group(std::integral_constant<int, 4>{}, g);
+    for (int g = 0; g + 1 < G; g++) group(std::integral_constant<int, kQNB>{}, g);
     if (G > 0) {  // the last group with as few counter blocks per lane as its longest packet needs
         // (small packets: a 300-B packet's second group needs 1 block per lane, not 3)
         if (tail_slots <= 4) group(std::integral_constant<int, 1>{}, G - 1);
-        else if (tail_slots <= 8) group(std::integral_constant<int, 2>{}, G - 1);
-        else if (tail_slots <= 12) group(std::integral_constant<int, 3>{}, G - 1);
-        else group(std::integral_constant<int, 4>{}, G - 1);
+        else if (kQNB == 2 || tail_slots <= 8) group(std::integral_constant<int, 2>{}, G - 1);
+        else if (kQNB == 3 || tail_slots <= 12) group(std::integral_constant<int, kQNB < 3 ? kQNB : 3>{}, G - 1);
+        else group(std::integral_constant<int, kQNB>{}, G - 1);
     }
     if (!len_done && (((m + 1) & 3) == (int)s)) w = gh.mulx(w, lenblk());
     // this lane's chain times H^e, e = (m + 2) - its last slot; then the quad's sum
@@ -483,6 +493,9 @@ __device__ __forceinline__ void quad_slices(const DevKey *__restrict__ keys, con
     }
 }
 
+// NR = 10 / 14: one AES size; NR = 0: a planned batch holding both sizes in ONE launch -- each workgroup opens its
+// slice of the AES-128 packets, then its slice of the AES-256 packets (round count per key segment, tables per key),
+// as the fused receive's open phase does, instead of two serial full-chip launches
 template <bool SEAL, int NR>
 __global__ __launch_bounds__(kQuadWG<NR>) void aes_gcm_quad_kernel(const DevKey *__restrict__ keys,
                                                               const qpp_pkt *__restrict__ descs,
@@ -492,7 +505,9 @@ __global__ __launch_bounds__(kQuadWG<NR>) void aes_gcm_quad_kernel(const DevKey 
                                                               uint8_t *__restrict__ arena, uint8_t *masks,
                                                               int8_t *status, uint32_t flags, uint32_t single,
                                                               uint32_t n_single) {
-    quad_slices<SEAL, NR>(keys, descs, perm, work, meta, arena, masks, status, flags, single, n_single);
+    constexpr int WG = kQuadWG<NR>;
+    if constexpr (NR != 14) quad_slices<SEAL, 10, WG>(keys, descs, perm, work, meta, arena, masks, status, flags, single, n_single);
+    if constexpr (NR != 10) quad_slices<SEAL, 14, WG>(keys, descs, perm, work, meta, arena, masks, status, flags, single, n_single);
 }
 
 // ---------------------------------------------------------------- fused receive path, any key mix, ONE launch
@@ -515,7 +530,9 @@ __global__ __launch_bounds__(kQuadWG<NR>) void aes_gcm_quad_kernel(const DevKey 
 #ifndef QPP_RX_TRACE
 #define QPP_RX_TRACE 0  // 1: workgroups 0, grid/2 and the last print their phase times (s_memrealtime)
 #endif
-constexpr uint32_t kRxCtl = kQLdsPow;     // LDS: barrier verdict; [kRxCtl + 64, +6 KiB) phase B scan sums
+constexpr uint32_t kRxCtl = kQLdsPow;     // LDS: barrier verdict; [kRxCtl + 64, +320 B) phase B scan sums
+constexpr uint32_t kRxCls = kRxCtl + 1024;  // LDS: phase B's class byte per key (<= kRxHistMax)
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
 constexpr uint32_t kRxHistMax = 16384;    // LDS bins [0, 64 KiB): keys per workgroup in phases A-C
 constexpr uint64_t kRxBarrierTicks = 100000000ull;  // 1 s of s_memrealtime (100 MHz)
 constexpr int8_t kRxOpen = 0x7f;  // status of a packet bound for the open phase (never a final status)
@@ -630,7 +647,12 @@ __global__ __launch_bounds__(kRxWG<AES>) void aes_gcm_quad_rx_kernel(const DevKe
         for (uint32_t k = k0; k < k1; k++) {
             const uint32_t c = counts[k];
             if (!c) continue;
-            const uint32_t cls = cls_of(k);  // (< 3: phase A counted only packets of open classes)
+            // (< 3: phase A counted only packets of open classes; a record that changed since -- never while the
+            // batch is in flight, by the key-retirement rules -- is opened as AES-128 with whatever it holds, so it
+            // fails its tags instead of indexing past the three classes; the class is kept for the second loop)
+            uint32_t cls = cls_of(k);
+            if (cls >= 3) cls = 0;
+            *(lds_u8 *)(size_t)(kRxCls + k) = (uint8_t)cls;
             v[cls] += c;
             if (cls < 2) v[3 + cls] += 1;
         }
@@ -680,7 +702,7 @@ __global__ __launch_bounds__(kRxWG<AES>) void aes_gcm_quad_rx_kernel(const DevKe
         for (uint32_t k = k0; k < k1; k++) {
             const uint32_t c = counts[k];
             if (!c) continue;
-            const uint32_t cls = cls_of(k);
+            const uint32_t cls = *(const lds_u8 *)(size_t)(kRxCls + k);  // (the first loop's verdict, same thread)
             cursor[k] = off[cls];
             if (cls < 2) work[item[cls]++] = WorkItem{k, off[cls], c, cls ? 14u : 10u};
             off[cls] += c;
@@ -755,9 +777,12 @@ hipError_t launch_aes_gcm_quad(bool seal, uint32_t nr, dim3 grid, hipStream_t s,
     if (nr == 10) {
         if (seal) launch_quad<true, 10>(grid, s, keys, descs, pb, arena, masks, status, flags, single, n_single);
         else launch_quad<false, 10>(grid, s, keys, descs, pb, arena, masks, status, flags, single, n_single);
-    } else {
+    } else if (nr == 14) {
         if (seal) launch_quad<true, 14>(grid, s, keys, descs, pb, arena, masks, status, flags, single, n_single);
         else launch_quad<false, 14>(grid, s, keys, descs, pb, arena, masks, status, flags, single, n_single);
+    } else {  // both sizes (a planned batch)
+        if (seal) launch_quad<true, 0>(grid, s, keys, descs, pb, arena, masks, status, flags, single, n_single);
+        else launch_quad<false, 0>(grid, s, keys, descs, pb, arena, masks, status, flags, single, n_single);
     }
     return hipGetLastError();
 }

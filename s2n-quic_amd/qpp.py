@@ -225,6 +225,10 @@ class DeviceBuffer:
             if self.ctx.handle:
                 lib().qpp_dev_free(self.ctx.handle, self.ptr)
             self.ptr = None
+        try:  # (a long-lived context that makes temporary buffers does not keep them listed)
+            self.ctx._bufs.remove(self)
+        except ValueError:
+            pass
 
 
 class Context:
@@ -251,7 +255,7 @@ class Context:
             lib().qpp_event_destroy(h, e)
         for s in self._streams:
             lib().qpp_stream_destroy(h, s)
-        for b in self._bufs:
+        for b in list(self._bufs):
             b.free()
         for p in self._host:
             lib().qpp_host_free(h, p)

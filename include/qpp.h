@@ -71,7 +71,13 @@ int qpp_ctx_set_burst_max(qpp_ctx *ctx, size_t max_packets);
  * env QPP_PACKET_SERVER=0 turns it off): a persistent kernel of 4 workgroups, started by the first such call, that
  * seals / opens one packet posted through pinned memory without a kernel launch, and leaves after
  * QPP_TXQ_SERVER_IDLE_MS (200) without a call.  Packets of more than 16 KiB (header + payload + tag) and FIPS seals
- * take the launched path.  Outputs are identical either way.  on = 0 stops and frees the server. */
+ * take the launched path.  Outputs are identical either way.  on = 0 stops and frees the server.
+ * Resident servers are accounted per DEVICE, over every context of the process (packet servers and persistent
+ * transmit queues alike): at most GPU_MAX_HW_QUEUES (default 4) are resident on a device at once -- the runtime maps
+ * the streams of one priority level onto that many hardware queues, and a server launched onto a hardware queue
+ * another server holds would wait for that server's idle exit -- so a call that finds every server slot taken is
+ * launched instead (same results), and a transmit-queue flush takes the launched path.  A server's launch also waits
+ * for the device's latest fused receive (qpp_unprotect_open_batch): its grid did not count the server's CUs. */
 int qpp_ctx_set_packet_server(qpp_ctx *ctx, int on);
 /* Per-packet calls the packet server has taken so far, and its kernel launches (it leaves when idle). */
 int qpp_ctx_packet_server_info(const qpp_ctx *ctx, uint64_t *calls, uint64_t *starts);
@@ -313,7 +319,9 @@ int qpp_txq_create_async(qpp_ctx *ctx, size_t ring_bytes, size_t max_packets, si
  * flush through a doorbell word in pinned host memory instead of launching kernels, and qpp_txq_wait spins on a
  * completion word the kernel writes back into the same page (no launch, no runtime call, no interrupt per flush).
  * The server keeps the AES tables and the last key's GHASH tables in LDS between flushes; it occupies a few CUs
- * (QPP_TXQ_SERVER_WGS, default 16; full-chip batch kernels of the context size their grids around them).  A flush
+ * (QPP_TXQ_SERVER_WGS, default 16; full-chip batch kernels of every context on the device size their grids around
+ * them).  It counts against the device's GPU_MAX_HW_QUEUES server slots (qpp_ctx_set_packet_server): with none free,
+ * flushes take the launched path until one is.  A flush
  * after a quarter of QPP_TXQ_SERVER_IDLE_MS (default 200) without one restarts it first (one launch); the kernel itself
  * leaves after the whole idle time (a host that went away).  Flushes with a
  * ChaCha20-Poly1305 packet, or while a FIPS key is live, take the launched path of qpp_txq_create (same results).
@@ -323,6 +331,9 @@ int qpp_txq_create_persistent(qpp_ctx *ctx, size_t ring_bytes, size_t max_packet
 int qpp_txq_info(const qpp_txq *q, uint64_t *server_flushes, uint64_t *launched_flushes, uint64_t *server_starts);
 /* Persistent queue: microseconds from the server seeing the last posted flush's doorbell to its completion word. */
 int qpp_txq_server_time(const qpp_txq *q, double *us);
+/* Persistent queue: descriptors its server refused because their bytes were not inside the ring (never read or
+ * written; qpp_txq_push validates every packet, so this stays 0 -- a device-side check of every ring offset). */
+int qpp_txq_server_refused(const qpp_txq *q, uint64_t *count);
 /* Diagnostics: the server's clock (100 MHz) at the last flush's doorbell, workgroup 0's phase stamps and shader-clock
  * cycles over its work (a build with QPP_TXS_TRACE, else 0) and its completion word:
  * {seen, broadcast, item read, packets done, arrival, done, shader cycles broadcast -> arrival}, then the low words
@@ -390,9 +401,12 @@ typedef struct qpp_rx_pkt {
  * ONE cooperative launch unprotects, groups by the chosen key and opens the AES packets of both sizes, and one more
  * launch on the same stream opens the ChaCha20 packets it sorted out (when ChaCha20 keys are live); with no AES record
  * live, one launch of the ChaCha20 kernel; otherwise unprotect + plan + open kernels.  Identical outputs on every path
- * (env QPP_RX_FUSED=0 forces the multi-launch one).  The cooperative launch needs all its workgroups resident at once:
- * if they are not within a second (CUs held by a foreign kernel), its AES packets report QPP_INTERNAL_ERROR with the
- * header unprotected and the payload untouched, and qpp_ctx_rx_timeouts counts it.
+ * (env QPP_RX_FUSED=0 forces the multi-launch one).  The fused launch needs all its workgroups resident at once (grid
+ * barriers), which the engine arranges within the process: its grid is the CUs every context's resident servers leave
+ * on the device, fused receives of a device run one after another (a second one, on any stream of any context, waits
+ * for the first), and a server starts only after the latest fused receive.  If the workgroups are still not all
+ * resident within a second (CUs held by another process's kernels), its AES packets report QPP_INTERNAL_ERROR with
+ * the header unprotected and the payload untouched, and qpp_ctx_rx_timeouts counts it.
  * rx, descs_out, arena and status are device pointers.  Asynchronous. */
 int qpp_unprotect_open_batch(qpp_ctx *ctx, const qpp_rx_pkt *rx, size_t n, uint8_t *arena, qpp_pkt *descs_out,
                              int8_t *status, uint32_t flags, void *stream);

@@ -1943,7 +1943,8 @@ int srv_start(qpp_txq *q, bool force = false) {
     const bool pending = q->srv_posted && !srv_done(q, q->srv_posted);
     const uint32_t seq0 = pending ? q->srv_posted - 1u : q->srv_seq;
     HIP_TRY(ctx, launch_txq_server(ctx->d_keys, ctx->pow, q->v_mail, q->v_slots, q->v_items, q->v_sdesc, q->v_ring,
-                                   seq0, q->srv_idle_ticks, q->srv_wgs, q->srv_stream));
+                                   (uint32_t)std::min<size_t>(q->ring_bytes, UINT32_MAX), seq0, q->srv_idle_ticks,
+                                   q->srv_wgs, q->srv_stream));
     q->srv_running = true;
     q->srv_launched.store(true, std::memory_order_release);
     q->srv_keys = ctx->d_keys;
@@ -2538,6 +2539,12 @@ int qpp_txq_create_persistent(qpp_ctx *ctx, size_t ring_bytes, size_t max_packet
     uint32_t wgs = 16;
     if (const char *e = getenv("QPP_TXQ_SERVER_WGS")) wgs = (uint32_t)strtoul(e, nullptr, 10);
     return txq_create_server(ctx, ring_bytes, max_packets, wgs, srv_idle_ms(), out);
+}
+
+int qpp_txq_server_refused(const qpp_txq *q, uint64_t *count) {
+    if (!q || !count || !q->persistent) return QPP_INTERNAL_ERROR;
+    *count = __atomic_load_n(&q->h_mail->oob, __ATOMIC_ACQUIRE);
+    return QPP_OK;
 }
 
 int qpp_txq_server_time(const qpp_txq *q, double *us) {

@@ -189,10 +189,14 @@ struct alignas(64) TxsMail {  // telemetry (s_memrealtime, 100 MHz)
     uint64_t t_seen, t_done;  // workgroup 0 saw the flush / finished it
     uint64_t pad0[6];         // QPP_TXS_TRACE: workgroup 0's phase stamps and shader cycles
     uint32_t pad1[16];        // QPP_TXS_TRACE: wave 0's stamps inside its packet
+    uint32_t oob;             // descriptors the server refused because their bytes lie outside the ring (0: always)
+    uint32_t pad2[15];
 };
+// ring_bytes: the ring's size -- a descriptor whose bytes [off, off + aad + payload + 16) do not lie inside is refused
+// (never read or written) and counted in mail->oob
 hipError_t launch_txq_server(const DevKey *keys, const PowTables &pow, TxsMail *mail, TxsSlot *slots,
-                             const WorkItem *items, const qpp_pkt *sdesc, uint8_t *ring, uint32_t seq0,
-                             uint32_t idle_ticks, uint32_t wgs, hipStream_t s);
+                             const WorkItem *items, const qpp_pkt *sdesc, uint8_t *ring, uint32_t ring_bytes,
+                             uint32_t seq0, uint32_t idle_ticks, uint32_t wgs, hipStream_t s);
 // the burst power tables of keys[slots[i]] (AES packet keys with slot < pow.cap), after their V[m] are in place
 hipError_t launch_pow_setup(const DevKey *keys, const uint32_t *slots, uint32_t count, const PowTables &pow,
                             hipStream_t s);

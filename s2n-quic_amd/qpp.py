@@ -56,7 +56,7 @@ EXPORTS = [
     "qpp_event_elapsed_ms", "qpp_stream_wait_event", "qpp_unprotect_open_batch", "qpp_pn_truncate", "qpp_pn_expand",
     "qpp_key_new_batch", "qpp_txq_create", "qpp_txq_destroy", "qpp_txq_ring", "qpp_txq_push", "qpp_txq_flush",
     "qpp_txq_create_async", "qpp_txq_flush_async", "qpp_txq_poll", "qpp_txq_wait", "qpp_txq_push_descs", "qpp_txq_set_coalesce", "qpp_txq_push_scatter",
-    "qpp_txq_create_persistent", "qpp_txq_info", "qpp_txq_server_time", "qpp_ctx_set_conn_keys",
+    "qpp_txq_create_persistent", "qpp_txq_info", "qpp_txq_server_time", "qpp_txq_server_refused", "qpp_ctx_set_conn_keys",
     "qpp_txq_server_stamps",
     "qpp_txq_pending", "qpp_memcpy_d2d", "qpp_ctx_set_burst_max", "qpp_dc_key_new", "qpp_dc_seal", "qpp_dc_open",
     "qpp_dc_open_in_place", "qpp_ctx_key_slots", "qpp_key_new_pair", "qpp_key_update_batch", "qpp_initial_keys_pair",
@@ -155,6 +155,7 @@ def lib():
             "qpp_txq_create_persistent": (ctypes.c_int, [vp, sz, sz, ctypes.POINTER(vp)]),
             "qpp_txq_info": (ctypes.c_int, [vp, ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u64)]),
             "qpp_txq_server_time": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double)]),
+            "qpp_txq_server_refused": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_uint64)]),
             "qpp_ctx_set_conn_keys": (ctypes.c_int, [vp, vp, sz]),
             "qpp_txq_server_stamps": (ctypes.c_int, [vp, vp]),
             "qpp_txq_set_coalesce": (ctypes.c_int, [vp, sz]),
@@ -756,6 +757,14 @@ class TxQueue:
         if rc != OK:
             raise QppError(rc, "qpp_txq_info")
         return a.value, b.value, c.value
+
+    def server_refused(self):
+        """qpp_txq_server_refused: descriptors the server refused as lying outside the ring (always 0)"""
+        c = ctypes.c_uint64()
+        rc = lib().qpp_txq_server_refused(self.handle, ctypes.byref(c))
+        if rc != OK:
+            raise QppError(rc, "qpp_txq_server_refused")
+        return c.value
 
     def server_time_us(self):
         """qpp_txq_server_time: doorbell seen -> completion of the last posted flush, on the server's clock"""

@@ -305,13 +305,14 @@ def test_hp_mask_batch_receive_side(ctx):
         assert got[5 * i:5 * i + 5] == want
 
 
-@pytest.mark.parametrize("suite", [1, 2, 3])
+@pytest.mark.parametrize("suite", [1, 2, 3, 0], ids=["aes128", "aes256", "chacha", "mixed"])
 def test_full_size_round_trip(ctx, suite):
-    """BASELINE configs 2/3 size (1 Mi x 1200 B): seal -> open round trip restores every payload, every
-    status is OK, a seeded sample of packets is bit-exact against the oracle and every packet against the full-size
-    checker."""
+    """BASELINE configs 2/3 size (1 Mi x 1200 B): a seeded sample of sealed packets is bit-exact against the oracle and
+    every packet against the full-size checker; the open of every packet (a tampered subset among them) is compared
+    with the expected arena byte for byte.  mixed: 66 keys of all three suites in ONE batch (negotiated.rs:15-30; the
+    single both-sizes AES launch and the plan-selected ChaCha20 packets)."""
     n, pt_len = 1 << 20, 1200
-    keys, okeys = _keys(ctx, [suite] * (1 if suite == 1 else 64), seed=suite)
+    keys, okeys = _keys(ctx, ([suite] * (1 if suite == 1 else 64)) if suite else [1, 2, 3] * 22, seed=suite)
     slots = [k.slot for k in keys]
     descs, arena = qpp.make_batch(n, pt_len, slots, seed=0x5eed0002, pn_base=(2**32 if suite == 2 else 0))
     d_desc, d_arena, d_mask, d_status = ctx.alloc(descs.nbytes), ctx.alloc(arena.nbytes), ctx.alloc(5 * n), ctx.alloc(n)
@@ -333,13 +334,35 @@ def test_full_size_round_trip(ctx, suite):
     assert np.concatenate([masks[5 * i:5 * i + 5] for i in pick]).tobytes() == want_masks
     # and EVERY packet (ciphertext, tag, mask) against the full-size checker (oracle/fastcheck.c)
     assert orc.check_full_seal(okeys, slots, descs, arena, sealed, masks, qpp.HP_MASK_OUT) == n
+    # open EVERY packet and compare the whole arena byte for byte (only the round trip and the status were
+    # checked at this size): one packet in 997 tampered -- a ciphertext bit or a tag bit -- must come back
+    # DECRYPT_ERROR with its payload zeroed (aead/default.rs:65-93: no unauthenticated plaintext), every other one
+    # with its plaintext; headers and tags are left as they were
+    bad = np.arange(3, n, 997)
+    tampered = sealed.copy().reshape(n, stride)
+    for j, i in enumerate(bad):
+        col = 21 + int(i % pt_len) if j % 2 == 0 else 21 + pt_len + int(i % 16)
+        tampered[i, col] ^= np.uint8(1 << (j % 8))
+    d_arena.upload(tampered.reshape(-1))
     ctx.open_batch(d_desc, n, d_arena, d_status)
     st = d_status.download(dtype=np.int8)
-    opened = d_arena.download()
-    assert (st == 0).all()
-    v = opened.reshape(n, stride)
+    opened = d_arena.download().reshape(n, stride)
+    want_st = np.zeros(n, dtype=np.int8)
+    want_st[bad] = qpp.DECRYPT_ERROR
+    assert (st == want_st).all()
+    want = tampered.copy()
     a = arena.reshape(n, stride)
-    assert (v[:, 21:21 + pt_len] == a[:, 21:21 + pt_len]).all()
+    want[:, 21:21 + pt_len] = a[:, 21:21 + pt_len]
+    want[bad, 21:21 + pt_len] = 0
+    assert (opened == want).all()
+    # the oracle's open on a sample of the tampered packets and their neighbours: the same statuses and bytes
+    pick = np.sort(np.concatenate([bad[:40], bad[:40] + 1]))
+    sub_d = descs[pick].copy()
+    sub_d["off"] = np.arange(len(pick)) * stride
+    sub_a = np.concatenate([tampered[i] for i in pick])
+    want_sub = orc.open_batch(okeys, _oracle_keys_for(okeys, sub_d, slots), sub_a)
+    assert (np.array(want_sub, dtype=np.int8) == st[pick]).all()
+    assert (sub_a.reshape(len(pick), stride) == opened[pick]).all()
     # a checksum of checksums over the ciphertext: identical across two runs (determinism)
     d_arena.upload(arena)
     ctx.seal_batch(d_desc, n, d_arena, d_mask, d_status, qpp.HP_MASK_OUT)

@@ -11,6 +11,8 @@
 #   bench[:name bench args]   python bench.py <args> -> <name>.json (name defaults to "bench")
 #   ab[:sub CFGS|ARGS]        tools/ab.sh (same-box alternating A/B); CFGS and bench args separated by '|'
 #                             e.g. "ab:aad ab/x.so:x s2n-quic_amd/libqpp.so:new|--aad 32"
+#   pmcab[:sub LIBS|ARGS]     tools/pmc_ab.sh: FETCH_SIZE / WRITE_SIZE per library build (same box), LIBS and bench args
+#                             separated by '|', e.g. "pmcab:nt s2n-quic_amd/libqpp.so ab/nt0.so"
 #   prof[:bench args]         rocprofv3 kernel trace + PMC passes (tools/profile.sh) -> gpurun_out/<tag>_prof,
 #                             then prof_summary.txt and traffic.json of the default workload in gpurun_out/<tag>/
 #   rxtrace                   rocprofv3 kernel trace of the fused receive (exit status recorded)
@@ -40,6 +42,9 @@ for step in "$@"; do
     ab)
       sub=${args%% *}; rest=${args#* }; cfgs=${rest%%|*}; bargs=""; [[ "$rest" == *"|"* ]] && bargs=${rest#*|}
       CFGS="$cfgs" BENCH_ARGS="$bargs" bash tools/ab.sh ${tag}_$sub || exit 1 ;;
+    pmcab)
+      sub=${args%% *}; rest=${args#* }; libs=${rest%%|*}; bargs=""; [[ "$rest" == *"|"* ]] && bargs=${rest#*|}
+      LIBS="$libs" BENCH_ARGS="$bargs" bash tools/pmc_ab.sh ${tag}_$sub || exit 1 ;;
     prof)
       bash tools/profile.sh ${tag}_prof $args || exit 1
       python tools/summarize_prof.py gpurun_out/${tag}_prof > $o/prof_summary.txt && head -14 $o/prof_summary.txt || exit 1

@@ -47,6 +47,10 @@ struct StreamState {
     uint32_t *fips_refused = nullptr;  // device word: packets the gate refused (txq flushes report it)
     uint32_t *rx_scratch = nullptr;    // fused receive kernel (quad.hip): barrier, per-key counts / cursors, work items
     uint32_t rx_scratch_keys = 0;      // the key_cap it is sized for
+    // a mixed-suite batch's ChaCha20 kernel runs on this side stream beside the AES kernel (fork after the plan, join
+    // before the batch's last event): its workgroups fill the CUs the AES kernel's last workgroups leave
+    hipStream_t side = nullptr;
+    hipEvent_t fork_ev = nullptr, join_ev = nullptr;
 };
 
 struct KStage {
@@ -275,6 +279,12 @@ void free_stream_state(StreamState *st) {
     hipFree(st->fips_buf);
     hipFree(st->fips_refused);
     hipFree(st->rx_scratch);
+    if (st->side) {
+        hipStreamSynchronize(st->side);
+        hipStreamDestroy(st->side);
+    }
+    if (st->fork_ev) hipEventDestroy(st->fork_ev);
+    if (st->join_ev) hipEventDestroy(st->join_ev);
     if (st->last) hipEventDestroy(st->last);
     delete st;
 }
@@ -671,20 +681,50 @@ uint32_t single_aes_slot(const qpp_ctx *ctx) {
 
 // Batch bodies: plan (AES) + kernels on st's stream; keys already flushed.
 // The ChaCha20 kernel of a batch: after a plan that listed the non-AES packets (ChaCha20 keys, refused slots) it visits
-// only those (selection mode); otherwise every packet (AES ones are skipped by each lane)
-hipError_t launch_chacha_batch(const qpp_ctx *ctx, const StreamState *st, bool seal, bool planned, const qpp_pkt *descs,
-                               uint32_t n, uint8_t *arena, uint8_t *masks, int8_t *status, uint32_t flags) {
+// only those (selection mode) -- on the stream's side stream when ChaCha20 keys are live (a mixed-suite batch: it runs
+// beside the AES kernel, forked behind the plan, joined before the batch ends); otherwise every packet (AES ones are
+// skipped by each lane).  fork: recorded on st->stream right after the plan (the AES kernel follows it there).
+hipError_t launch_chacha_batch(const qpp_ctx *ctx, StreamState *st, bool seal, bool planned, bool forked,
+                               const qpp_pkt *descs, uint32_t n, uint8_t *arena, uint8_t *masks, int8_t *status,
+                               uint32_t flags) {
     const bool burst = n <= (ctx->burst_max >> kChachaBurstShift);
-    if (planned && !burst && plan_lists_others(n, ctx->key_cap))
-        return launch_chacha_sel_batch(seal, ctx->d_keys, ctx->key_cap, descs, n, arena, masks, status, flags,
-                                       st->plan.perm, st->plan.n_work + 4, st->stream);
+    if (planned && !burst && plan_lists_others(n, ctx->key_cap)) {
+        hipStream_t s = forked ? st->side : st->stream;
+        hipError_t e = launch_chacha_sel_batch(seal, ctx->d_keys, ctx->key_cap, descs, n, arena, masks, status, flags,
+                                               st->plan.perm, st->plan.n_work + 4, s);
+        if (e != hipSuccess || !forked) return e;
+        e = hipEventRecord(st->join_ev, st->side);
+        return e != hipSuccess ? e : hipStreamWaitEvent(st->stream, st->join_ev, 0);
+    }
     return launch_chacha(seal, ctx->d_keys, ctx->key_cap, descs, n, arena, masks, status, flags, burst, st->stream);
+}
+
+// Whether a planned batch forks its ChaCha20 kernel onto the side stream (ChaCha20 keys live beside AES ones, a plan
+// that lists them, the lane kernel): creates the side stream on first use and records the fork point
+int chacha_fork(qpp_ctx *ctx, StreamState *st, uint32_t n, uint32_t flags, bool *forked) {
+    *forked = false;
+    if ((flags & QPP_ONLY_AES) || !ctx->live_by_suite[QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256]) return QPP_OK;
+    if (n <= (ctx->burst_max >> kChachaBurstShift) || !plan_lists_others(n, ctx->key_cap)) return QPP_OK;
+    static const bool off = [] {
+        const char *e = getenv("QPP_CHACHA_SIDE");
+        return e && e[0] == '0';
+    }();
+    if (off) return QPP_OK;
+    if (!st->side) {
+        HIP_TRY(ctx, hipStreamCreateWithFlags(&st->side, hipStreamNonBlocking));
+        HIP_TRY(ctx, hipEventCreateWithFlags(&st->fork_ev, hipEventDisableTiming));
+        HIP_TRY(ctx, hipEventCreateWithFlags(&st->join_ev, hipEventDisableTiming));
+    }
+    HIP_TRY(ctx, hipEventRecord(st->fork_ev, st->stream));
+    HIP_TRY(ctx, hipStreamWaitEvent(st->side, st->fork_ev, 0));
+    *forked = true;
+    return QPP_OK;
 }
 
 int enqueue_seal(qpp_ctx *ctx, StreamState *st, const qpp_pkt *descs, uint32_t n, uint8_t *arena, uint8_t *masks,
                  int8_t *status, uint32_t flags, uint32_t *refused = nullptr) {
     hipStream_t s = st->stream;
-    bool planned = false;
+    bool planned = false, forked = false;
     if (!(flags & QPP_ONLY_CHACHA)) RC_TRY(fips_gate(ctx, st, descs, n, status, refused));
     if (!(flags & QPP_ONLY_CHACHA) && (suite_mask(ctx) & kAesSuites)) {
         const AesPath path = aes_path(ctx, n);
@@ -695,19 +735,20 @@ int enqueue_seal(qpp_ctx *ctx, StreamState *st, const qpp_pkt *descs, uint32_t n
         } else {
             RC_TRY(ensure_plan(ctx, st, n));
             HIP_TRY(ctx, launch_plan(ctx->d_keys, ctx->key_cap, descs, n, st->plan, aes_per_item(ctx, path, n), s));
+            RC_TRY(chacha_fork(ctx, st, n, flags, &forked));
             HIP_TRY(ctx, launch_aes(ctx, path, true, descs, st->plan, n, arena, masks, status, flags, s));
             planned = true;
         }
     }
     if (!(flags & QPP_ONLY_AES))
-        HIP_TRY(ctx, launch_chacha_batch(ctx, st, true, planned, descs, n, arena, masks, status, flags));
+        HIP_TRY(ctx, launch_chacha_batch(ctx, st, true, planned, forked, descs, n, arena, masks, status, flags));
     return QPP_OK;
 }
 
 int enqueue_open(qpp_ctx *ctx, StreamState *st, const qpp_pkt *descs, uint32_t n, uint8_t *arena, int8_t *status,
                  uint32_t flags) {
     hipStream_t s = st->stream;
-    bool planned = false;
+    bool planned = false, forked = false;
     if (!(flags & QPP_ONLY_CHACHA) && (suite_mask(ctx) & kAesSuites)) {
         const AesPath path = aes_path(ctx, n);
         const uint32_t one = path == AesPath::quad ? single_aes_slot(ctx) : UINT32_MAX;
@@ -717,12 +758,13 @@ int enqueue_open(qpp_ctx *ctx, StreamState *st, const qpp_pkt *descs, uint32_t n
         } else {
             RC_TRY(ensure_plan(ctx, st, n));
             HIP_TRY(ctx, launch_plan(ctx->d_keys, ctx->key_cap, descs, n, st->plan, aes_per_item(ctx, path, n), s));
+            RC_TRY(chacha_fork(ctx, st, n, flags, &forked));
             HIP_TRY(ctx, launch_aes(ctx, path, false, descs, st->plan, n, arena, nullptr, status, 0, s));
             planned = true;
         }
     }
     if (!(flags & QPP_ONLY_AES))
-        HIP_TRY(ctx, launch_chacha_batch(ctx, st, false, planned, descs, n, arena, nullptr, status, 0));
+        HIP_TRY(ctx, launch_chacha_batch(ctx, st, false, planned, forked, descs, n, arena, nullptr, status, 0));
     return QPP_OK;
 }
 

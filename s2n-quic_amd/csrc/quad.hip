@@ -79,6 +79,9 @@ static_assert(kQNB >= 2 && kQNB <= 4, "group size");
 #ifndef QPP_QUAD_HOLD
 #define QPP_QUAD_HOLD 1  // the deferred last chunk of interior groups (0: every chunk stored in its own group)
 #endif
+#ifndef QPP_QUAD_HEAD
+#define QPP_QUAD_HEAD 0  // the packet's first 64 ciphertext bytes (and its header bytes) stored at its end (write traffic)
+#endif
 
 // X * H through the 8-bit tables of H at [0, 64K) (T_j[x] at 256 x + 16 j): the setup's products
 __device__ __forceinline__ uint4 mul_h8(uint4 x) {
@@ -243,6 +246,14 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
     uint4 ek0 = make_uint4(0, 0, 0, 0);  // seal: E_K(J0) (slot 0: lane 0, group 0)
     uint4 held = make_uint4(0, 0, 0, 0);  // the previous interior group's blocks k = 3 (deferred last chunk)
     bool held_ok = false;
+    // The packet's first 64 ciphertext bytes (slots 1..4: block k = 0 of lanes 1-3, block k = 1 of lane 0, group 0)
+    // share their 64-byte segments with the packet's header and the previous packet's tag.  Stored at the packet's
+    // end -- with the tag, while the neighbouring quad of the same wave stores the previous packet's tail -- those
+    // segments are written while both packets' bytes are in L2 (one HBM write instead of two or three).
+    // The header bytes of header protection follow them to the end.  (Packets of >= 4 whole blocks and >= 2 groups.)
+    const bool hold_head = QPP_QUAD_HEAD && has && nfull >= 4 && ngroups > 1;  // quad-uniform
+    uint4 head = make_uint4(0, 0, 0, 0);
+    uint32_t hp_m0 = 0, hp_m1 = 0;  // lane 0: the header-protection mask, applied at the end when hold_head
     bool hp_done = false;                // seal: header protection applied after group 0 (quad-uniform)
     // Header protection as soon as the sample exists: the sample (ciphertext bytes [4 - pn_len, 20 - pn_len),
     // payload.rs:151-169) lies in ciphertext blocks 0 and 1 -- slots 1 and 2, group 0, lanes 1 and 2 -- when the payload
@@ -265,7 +276,14 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
                 mo[3] = (uint8_t)(m0 >> 24); mo[4] = (uint8_t)m1;
             }
             const uint32_t hdr_len = aad_len - pn_len;
-            if (flags & QPP_HP_APPLY) hdr_apply(at(dt.off), hdr_len, pn_len, hdr_load(at(dt.off), hdr_len), m0, m1);
+            if (flags & QPP_HP_APPLY) {
+                if (hold_head) {
+                    hp_m0 = m0;
+                    hp_m1 = m1;
+                } else {
+                    hdr_apply(at(dt.off), hdr_len, pn_len, hdr_load(at(dt.off), hdr_len), m0, m1);
+                }
+            }
         }
         hp_done = true;
     };
@@ -349,7 +367,9 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
             for (int k = 0; k < NBG; k++) {
                 const int t = t0 + 4 * k, j = t - 1;
                 const bool full = t >= 1 && j < nfull, part = rem && j == nfull, lenslot = has && t == m + 1;
-                if (full) st_payload(at(pay + 16 * (uint32_t)j), out[k]);
+                const bool headblk = hold_head && j >= 0 && j <= 3;  // (group 0 only: j <= 3 is slots 1..4)
+                if (headblk) head = out[k];
+                if (full && !headblk) st_payload(at(pay + 16 * (uint32_t)j), out[k]);
                 if (part) st_bytes(at(pay + 16 * (uint32_t)j), keep_bytes(out[k], rl), rl);
                 // the length block rides in the slot after the payload when the group reaches it
                 const uint4 x = lenslot ? lenblk() : part ? keep_bytes(SEAL ? out[k] : in[k], rl)
@@ -389,6 +409,13 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
         if (has && s == 0) st16(at(pay + len), y ^ ek0);  // tag = GHASH ^ E_K(J0)
         const qpp_pkt dt = reload_desc(descs, pkt_index);
         const uint32_t pn_len = dt.pn_len;
+        if (hold_head) {  // the packet's head (see hold_head), and its header bytes
+            st_payload(at(pay + 16u * (s == 0 ? 3u : s - 1u)), head);
+            if (s == 0 && (flags & QPP_HP_APPLY) && hp_done) {
+                const uint32_t hdr_len = aad_len - pn_len;
+                hdr_apply(at(dt.off), hdr_len, pn_len, hdr_load(at(dt.off), hdr_len), hp_m0, hp_m1);
+            }
+        }
         const bool hp = want_hp && has && pn_len >= 1 && pn_len <= 4 && len >= 4 - pn_len;  // quad-uniform
         if (hp && !hp_done) {  // short payloads: the sample runs into the tag
             // header-protection sample = ciphertext||tag bytes [4 - pn_len, 20 - pn_len) (payload.rs:151-169), column s
@@ -426,6 +453,8 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
         uint32_t diff = ys ^ ek0 ^ want;
         diff |= qperm<kQuadSwap1>(diff);
         diff |= qperm<kQuadSwap2>(diff);
+        // the packet's head (see hold_head): released only with a good tag
+        if (hold_head && diff == 0) st_payload(at(pay + 16u * (s == 0 ? 3u : s - 1u)), head);
         if (!has || s != 0) return;
         const bool ok = diff == 0;
         if (!ok) {

@@ -76,12 +76,7 @@ constexpr int kQuadWG = NR == 14 ? QPP_QUAD_WG256 : QPP_QUAD_WG;
 #endif
 constexpr int kQNB = QPP_QUAD_NB, kQSG = 4 * kQNB;
 static_assert(kQNB >= 2 && kQNB <= 4, "group size");
-#ifndef QPP_QUAD_HOLD
-#define QPP_QUAD_HOLD 1  // the deferred last chunk of interior groups (0: every chunk stored in its own group)
-#endif
-#ifndef QPP_QUAD_HEAD
-#define QPP_QUAD_HEAD 0  // the packet's first 64 ciphertext bytes (and its header bytes) stored at its end (write traffic)
-#endif
+
 
 // X * H through the 8-bit tables of H at [0, 64K) (T_j[x] at 256 x + 16 j): the setup's products
 __device__ __forceinline__ uint4 mul_h8(uint4 x) {
@@ -244,16 +239,7 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
     constexpr int HNR = NR == 10 ? 10 : 14;
     const bool want_hp = SEAL && (flags & (QPP_HP_MASK_OUT | QPP_HP_APPLY)) != 0;
     uint4 ek0 = make_uint4(0, 0, 0, 0);  // seal: E_K(J0) (slot 0: lane 0, group 0)
-    uint4 held = make_uint4(0, 0, 0, 0);  // the previous interior group's blocks k = 3 (deferred last chunk)
-    bool held_ok = false;
-    // The packet's first 64 ciphertext bytes (slots 1..4: block k = 0 of lanes 1-3, block k = 1 of lane 0, group 0)
-    // share their 64-byte segments with the packet's header and the previous packet's tag.  Stored at the packet's
-    // end -- with the tag, while the neighbouring quad of the same wave stores the previous packet's tail -- those
-    // segments are written while both packets' bytes are in L2 (one HBM write instead of two or three).
-    // The header bytes of header protection follow them to the end.  (Packets of >= 4 whole blocks and >= 2 groups.)
-    const bool hold_head = QPP_QUAD_HEAD && has && nfull >= 4 && ngroups > 1;  // quad-uniform
-    uint4 head = make_uint4(0, 0, 0, 0);
-    uint32_t hp_m0 = 0, hp_m1 = 0;  // lane 0: the header-protection mask, applied at the end when hold_head
+
     bool hp_done = false;                // seal: header protection applied after group 0 (quad-uniform)
     // Header protection as soon as the sample exists: the sample (ciphertext bytes [4 - pn_len, 20 - pn_len),
     // payload.rs:151-169) lies in ciphertext blocks 0 and 1 -- slots 1 and 2, group 0, lanes 1 and 2 -- when the payload
@@ -276,14 +262,7 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
                 mo[3] = (uint8_t)(m0 >> 24); mo[4] = (uint8_t)m1;
             }
             const uint32_t hdr_len = aad_len - pn_len;
-            if (flags & QPP_HP_APPLY) {
-                if (hold_head) {
-                    hp_m0 = m0;
-                    hp_m1 = m1;
-                } else {
-                    hdr_apply(at(dt.off), hdr_len, pn_len, hdr_load(at(dt.off), hdr_len), m0, m1);
-                }
-            }
+            if (flags & QPP_HP_APPLY) hdr_apply(at(dt.off), hdr_len, pn_len, hdr_load(at(dt.off), hdr_len), m0, m1);
         }
         hp_done = true;
     };
@@ -343,19 +322,12 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
         }
         if (inner) {
             const uint32_t b = pay + 16 * (uint32_t)(t0 - 1);
-            // The 64-byte segment that straddles two groups' ciphertext gets its two parts from stores a whole group
-            // apart, and in between L2 had often written the first part back on its own (a second partial write of
-            // the segment).  So between interior groups the last 64 bytes (blocks k = 3) wait for the next group and
-            // go out right after its first 64.  (Holding them into the tail group as well measured no fewer HBM
-            // writes -- 1.473 vs 1.492 MB WRITE_SIZE per launch, profiles/r04d -- and holding group 0's across group
-            // 1's keystream pushed the edge path past the register budget: its GHASH state went to scratch memory.)
-            st_payload(at(b), out[0]);
-            if (held_ok) st_payload(at(b - 64), held);
+            // (Every chunk in its own group.  Deferring the last 64 bytes of an interior group to the next group's
+            // first store, and holding the packet's first 64 ciphertext bytes and its header bytes to its end next to
+            // the tag, were both measured to write MORE, not less, and to run slower: round 5, profiles/r05/r05i --
+            // seal WRITE_SIZE 1.473 / 1.491 vs 1.457 MB per launch, seal 1.161 / 1.173 vs 1.152 ms.)
 #pragma unroll
-            for (int k = 1; k < NBG - 1; k++) st_payload(at(b + 64 * k), out[k]);
-            held_ok = QPP_QUAD_HOLD && interior(g + 1) && (g + 1 < G - 1 || tail_slots > kQSG - 4);  // uniform: the next group is interior
-            if (held_ok) held = out[NBG - 1];
-            else st_payload(at(b + 64 * (NBG - 1)), out[NBG - 1]);
+            for (int k = 0; k < NBG; k++) st_payload(at(b + 64 * k), out[k]);
 #pragma unroll
             for (int k = 0; k < NBG; k++) w = gh.mulx(w, SEAL ? out[k] : in[k]);
         } else {
@@ -367,9 +339,7 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
             for (int k = 0; k < NBG; k++) {
                 const int t = t0 + 4 * k, j = t - 1;
                 const bool full = t >= 1 && j < nfull, part = rem && j == nfull, lenslot = has && t == m + 1;
-                const bool headblk = hold_head && j >= 0 && j <= 3;  // (group 0 only: j <= 3 is slots 1..4)
-                if (headblk) head = out[k];
-                if (full && !headblk) st_payload(at(pay + 16 * (uint32_t)j), out[k]);
+                if (full) st_payload(at(pay + 16 * (uint32_t)j), out[k]);
                 if (part) st_bytes(at(pay + 16 * (uint32_t)j), keep_bytes(out[k], rl), rl);
                 // the length block rides in the slot after the payload when the group reaches it
                 const uint4 x = lenslot ? lenblk() : part ? keep_bytes(SEAL ? out[k] : in[k], rl)
@@ -409,13 +379,6 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
         if (has && s == 0) st16(at(pay + len), y ^ ek0);  // tag = GHASH ^ E_K(J0)
         const qpp_pkt dt = reload_desc(descs, pkt_index);
         const uint32_t pn_len = dt.pn_len;
-        if (hold_head) {  // the packet's head (see hold_head), and its header bytes
-            st_payload(at(pay + 16u * (s == 0 ? 3u : s - 1u)), head);
-            if (s == 0 && (flags & QPP_HP_APPLY) && hp_done) {
-                const uint32_t hdr_len = aad_len - pn_len;
-                hdr_apply(at(dt.off), hdr_len, pn_len, hdr_load(at(dt.off), hdr_len), hp_m0, hp_m1);
-            }
-        }
         const bool hp = want_hp && has && pn_len >= 1 && pn_len <= 4 && len >= 4 - pn_len;  // quad-uniform
         if (hp && !hp_done) {  // short payloads: the sample runs into the tag
             // header-protection sample = ciphertext||tag bytes [4 - pn_len, 20 - pn_len) (payload.rs:151-169), column s
@@ -453,8 +416,6 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
         uint32_t diff = ys ^ ek0 ^ want;
         diff |= qperm<kQuadSwap1>(diff);
         diff |= qperm<kQuadSwap2>(diff);
-        // the packet's head (see hold_head): released only with a good tag
-        if (hold_head && diff == 0) st_payload(at(pay + 16u * (s == 0 ? 3u : s - 1u)), head);
         if (!has || s != 0) return;
         const bool ok = diff == 0;
         if (!ok) {

@@ -27,4 +27,9 @@ run txq_chacha_64inflight --mode txq --suite chacha20poly1305 --inflight 64 --co
 run e2e_aes128 --mode e2e --steps 3 && \
 run e2e_c5_4ki_keys_rotating --mode e2e --keys 4096 --packets 2097152 --rotate --steps 3 && \
 run c2_aes128_keyruns64_64keys --keys 64 --key-run 64 && \
-run c3_aes128_64keys --keys 64
+run c3_aes128_64keys --keys 64 && \
+run c3_mixed_66keys --suite mixed --keys 66 && \
+run rx_aes128_64keys --mode rx --keys 64 && \
+run rx_aes256_64keys --mode rx --suite aes256gcm --keys 64 && \
+run rx_mixed_66keys --mode rx --suite mixed --keys 66 && \
+run c4_aes128_pt600 --pt 600 --packets 2097152

@@ -16,6 +16,7 @@
 #   prof[:bench args]         rocprofv3 kernel trace + PMC passes (tools/profile.sh) -> gpurun_out/<tag>_prof,
 #                             then prof_summary.txt and traffic.json of the default workload in gpurun_out/<tag>/
 #   rxtrace                   rocprofv3 kernel trace of the fused receive (exit status recorded)
+#   matrix                    tools/bench_matrix.sh: every BASELINE config and mode -> gpurun_out/<tag>_matrix/
 #   lat                       the latency faces: per-packet seal/open (AES, ChaCha), 64-packet txq flush (AES, ChaCha)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(cd $(dirname $0)/.. && pwd)}"
@@ -52,6 +53,8 @@ for step in "$@"; do
     rxtrace)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $o/rxtrace -o trace -- python3 bench.py --mode rx --keys 64 --steps 4 --warmup 1 --no-cpu > $o/rxtrace.log 2>&1
       rc=$?; echo "rx trace exit $rc" | tee $o/rxtrace.rc; [ $rc -eq 0 ] || exit 1 ;;
+    matrix)
+      bash tools/bench_matrix.sh ${tag}_matrix || exit 1 ;;
     lat)
       run_json packet_aes 120 python bench.py --mode packet --no-cpu && \
       run_json packet_chacha 120 python bench.py --mode packet --suite chacha20poly1305 --no-cpu && \

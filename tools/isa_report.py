@@ -10,7 +10,7 @@ import tempfile
 SRC = sys.argv[1] if len(sys.argv) > 1 else "s2n-quic_amd/csrc/quad.hip"
 PATS = sys.argv[2:] or ["aes_gcm_quad_kernel"]
 tmp = tempfile.mkdtemp()
-subprocess.check_call(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-c", os.path.abspath(SRC),
+subprocess.check_call(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-munsafe-fp-atomics", "-c", os.path.abspath(SRC),
                        "-o", os.path.join(tmp, "x.o"), "-save-temps"], cwd=tmp, stderr=subprocess.DEVNULL)
 asm = [f for f in os.listdir(tmp) if f.endswith("gfx950.s")][0]
 src = open(os.path.join(tmp, asm)).read()

@@ -62,6 +62,10 @@ int qpp_ctx_create(int device, qpp_ctx **out);
 void qpp_ctx_destroy(qpp_ctx *ctx);
 /* Default stream used by the per-packet functions and by batch calls given stream == NULL. */
 void *qpp_ctx_stream(qpp_ctx *ctx);
+/* Waits for every stream of THIS context (batch streams, key installs and retirements, the host pipeline, transmit
+ * queues' flushes) and stops its resident servers; never the whole device: another context's resident server keeps
+ * running (hipDeviceSynchronize would wait for its idle exit, or forever while it is fed).  The same holds for every
+ * call of the library: no free or wait of one context waits for another context's servers (see qpp_dev_free). */
 int qpp_ctx_synchronize(qpp_ctx *ctx);
 /* AES-GCM batches of at most max_packets packets (default 16384, env QPP_BURST_MAX) run one wave per packet
  * (latency: a 64-packet GSO burst); larger ones by the throughput kernels (quad / wave-item; qpp_ctx_set_aes_kernel).  ChaCha20-Poly1305 batches switch
@@ -419,6 +423,12 @@ uint64_t qpp_pn_expand(uint64_t largest_acked, uint64_t truncated, size_t pn_len
 
 /* ------------------------------------------------------------------ device plumbing */
 
+/* Device memory from the stream-ordered allocator.  qpp_dev_free returns at once: the memory goes back behind the work
+ * already enqueued on the context's streams (work the caller enqueued on streams of its own must be complete), and no
+ * resident server -- of this context or another -- is stopped or waited for (hipFree waits for every stream of the
+ * device).  qpp_host_free stops this context's own servers (hipHostFree waits for every stream of the device); while
+ * another context of the device has a resident server the pinned buffer is parked and freed by the next free or
+ * qpp_ctx_synchronize of any context that finds none.  No view of a freed buffer may be used afterwards. */
 int qpp_dev_alloc(qpp_ctx *ctx, size_t bytes, void **out);
 void qpp_dev_free(qpp_ctx *ctx, void *ptr);
 int qpp_host_alloc(qpp_ctx *ctx, size_t bytes, void **out); /* pinned host memory */

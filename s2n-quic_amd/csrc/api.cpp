@@ -101,6 +101,7 @@ struct qpp_ctx {
     hipStream_t stream = nullptr;
     hipStream_t kstream = nullptr;  // key installs / derivations
     hipStream_t rstream = nullptr;  // key retirements (zeroization behind in-flight batches)
+    hipStream_t astream = nullptr;  // device allocations and frees (stream-ordered allocator: dmalloc / dfree)
     hipEvent_t keys_ready = nullptr;
     uint64_t key_gen = 0;           // installs so far (keys_ready marks the latest)
     // device key table + host mirror
@@ -216,6 +217,7 @@ struct DevServers {
     std::mutex mu;
     std::vector<qpp_txq *> queues;  // the persistent queues of every context on the device
     hipEvent_t rx_tail = nullptr;   // recorded behind the device's latest fused receive
+    std::vector<void *> parked;     // pinned buffers whose hipHostFree waits for no resident server (hfree)
 };
 DevServers &dev_servers(int device) {
     static DevServers regs[64];
@@ -243,11 +245,21 @@ uint32_t cu_avail(const qpp_ctx *ctx) {
     const uint32_t r = servers_cu(ctx);
     return ctx->n_cu > r ? ctx->n_cu - r : 1u;
 }
-// hipFree / hipHostFree wait for every stream of the device, a running server's too -- and a server only ends on its
-// idle timeout (200 ms by default), or never while flushes come.  So every free of device or pinned memory stops the
-// context's servers first (the next flush of their queue restarts them): growing a plan or a scratch buffer while a
-// persistent queue is live costs a server restart, not the idle time (tests/test_gpu_txq_server.py).
+// Memory without device-wide waits.  hipFree, hipHostFree, hipHostUnregister and hipDeviceSynchronize wait for EVERY
+// stream of the device -- a resident server's too, and a server leaves only on its idle timeout (200 ms by default),
+// or never while its flushes keep coming.  Measured beside a resident kernel (tools/diag/free_sync.hip,
+// profiles/r05/r05v): each of those calls took 1950 ms next to a 2-s kernel; hipMallocAsync, hipFreeAsync,
+// hipHostMalloc, hipMalloc, hipStreamDestroy and hipEventDestroy did not wait.  A context stops its OWN servers before
+// freeing what they read and before a pinned free (quiet_for_free; the next flush or per-packet call restarts them),
+// but it cannot stop another context's, so it never makes a device-wide wait:
+//   * device memory comes from the stream-ordered allocator (dmalloc) and goes back through hipFreeAsync on the
+//     context's allocation stream: dfree_idle when every stream that used the buffer has been synchronized, dfree
+//     behind every stream of the context otherwise (device-side waits, no host wait);
+//   * pinned memory is freed at once when no other context of the device has a resident server, else parked in the
+//     device registry until a context finds none (hfree);
+//   * a context's synchronize waits for every stream of the context (ctx_sync), never the device.
 int quiet_for_free(qpp_ctx *ctx) { return servers_stop(ctx); }
+void hfree(qpp_ctx *ctx, void *p);  // (with the registry's users below)
 
 bool valid_suite(int s) {
     return s == QPP_SUITE_TLS_AES_128_GCM_SHA256 || s == QPP_SUITE_TLS_AES_256_GCM_SHA384 ||
@@ -270,19 +282,61 @@ void put_event(qpp_ctx *ctx, hipEvent_t e) {
     if (e) ctx->event_pool.push_back(e);
 }
 
-void free_plan(PlanBuffers &p) {
-    hipFree(p.counts); hipFree(p.cursor); hipFree(p.istart); hipFree(p.perm); hipFree(p.work); hipFree(p.n_work);
+// every stream the context's work runs on (the resident servers' excepted): its own, each batch stream's (with its
+// ChaCha side stream, and the transmit queues' flush streams, which are batch streams), the host pipeline's
+std::vector<hipStream_t> ctx_streams(const qpp_ctx *ctx) {
+    std::vector<hipStream_t> v;
+    for (hipStream_t s : {ctx->stream, ctx->kstream, ctx->rstream})
+        if (s) v.push_back(s);
+    for (const StreamState *st : ctx->streams) {
+        if (st->stream != ctx->stream) v.push_back(st->stream);
+        if (st->side) v.push_back(st->side);
+    }
+    if (ctx->pipe)
+        for (hipStream_t s : {ctx->pipe->h2d, ctx->pipe->comp, ctx->pipe->d2h})
+            if (s) v.push_back(s);
+    return v;
+}
+int ctx_sync(qpp_ctx *ctx) {
+    for (hipStream_t s : ctx_streams(ctx)) HIP_TRY(ctx, hipStreamSynchronize(s));
+    if (ctx->astream) HIP_TRY(ctx, hipStreamSynchronize(ctx->astream));
+    return QPP_OK;
+}
+template <class T>
+hipError_t dmalloc(qpp_ctx *ctx, T **p, size_t bytes) {
+    const hipError_t e = hipMallocAsync((void **)p, bytes ? bytes : 1, ctx->astream);
+    if (e != hipSuccess) return e;
+    return hipStreamSynchronize(ctx->astream);  // usable on any stream from here on
+}
+void dfree_idle(qpp_ctx *ctx, void *p) {
+    if (p) hipFreeAsync(p, ctx->astream);
+}
+void dfree(qpp_ctx *ctx, void *p) {
+    if (!p) return;
+    for (hipStream_t s : ctx_streams(ctx)) {
+        hipEvent_t e = get_event(ctx);
+        if (!e || hipEventRecord(e, s) != hipSuccess || hipStreamWaitEvent(ctx->astream, e, 0) != hipSuccess)
+            hipStreamSynchronize(s);
+        put_event(ctx, e);
+    }
+    hipFreeAsync(p, ctx->astream);
+}
+
+// (the plan's stream has been synchronized)
+void free_plan(qpp_ctx *ctx, PlanBuffers &p) {
+    for (void *b : {(void *)p.counts, (void *)p.cursor, (void *)p.istart, (void *)p.perm, (void *)p.work,
+                    (void *)p.n_work})
+        dfree_idle(ctx, b);
     p = PlanBuffers{};
 }
-void free_stream_state(StreamState *st) {
-    free_plan(st->plan);
-    hipFree(st->fips_buf);
-    hipFree(st->fips_refused);
-    hipFree(st->rx_scratch);
-    if (st->side) {
-        hipStreamSynchronize(st->side);
-        hipStreamDestroy(st->side);
-    }
+void free_stream_state(qpp_ctx *ctx, StreamState *st) {
+    hipStreamSynchronize(st->stream);
+    if (st->side) hipStreamSynchronize(st->side);
+    free_plan(ctx, st->plan);
+    dfree_idle(ctx, st->fips_buf);
+    dfree_idle(ctx, st->fips_refused);
+    dfree_idle(ctx, st->rx_scratch);
+    if (st->side) hipStreamDestroy(st->side);
     if (st->fork_ev) hipEventDestroy(st->fork_ev);
     if (st->join_ev) hipEventDestroy(st->join_ev);
     if (st->last) hipEventDestroy(st->last);
@@ -332,8 +386,8 @@ int grow_keys(qpp_ctx *ctx, uint32_t need) {
     while (cap < need) cap *= 2;
     DevKey *nk = nullptr;
     RC_TRY(servers_stop(ctx));  // they hold the old table's address
-    HIP_TRY(ctx, hipDeviceSynchronize());  // no batch may still read the old table
-    HIP_TRY(ctx, hipMalloc(&nk, sizeof(DevKey) * cap));
+    RC_TRY(ctx_sync(ctx));      // no batch may still read the old table
+    HIP_TRY(ctx, dmalloc(ctx, &nk, sizeof(DevKey) * cap));
     // Stream-ordered and waited for: a plain hipMemset runs on the null stream, which does not order against the
     // context's non-blocking streams (a batch could read the table before it is zeroed).
     HIP_TRY(ctx, hipMemsetAsync(nk, 0, sizeof(DevKey) * cap, ctx->kstream));
@@ -345,7 +399,7 @@ int grow_keys(qpp_ctx *ctx, uint32_t need) {
     const uint32_t pcap = std::min<uint32_t>(cap, kPowSlots);
     uint8_t *np = ctx->pow.base;
     if (pcap > ctx->pow.cap) {  // the precomputed tables of the slots so far move along
-        HIP_TRY(ctx, hipMalloc(&np, (size_t)pcap * kPowBytes));
+        HIP_TRY(ctx, dmalloc(ctx, &np, (size_t)pcap * kPowBytes));
         if (ctx->pow.cap) {
             HIP_TRY(ctx, hipMemcpyAsync(np, ctx->pow.base, (size_t)ctx->pow.cap * kPowBytes, hipMemcpyDeviceToDevice,
                                         ctx->kstream));
@@ -354,9 +408,9 @@ int grow_keys(qpp_ctx *ctx, uint32_t need) {
         }
     }
     HIP_TRY(ctx, hipStreamSynchronize(ctx->kstream));
-    if (ctx->d_keys) HIP_TRY(ctx, hipFree(ctx->d_keys));
+    dfree_idle(ctx, ctx->d_keys);
     if (np != ctx->pow.base) {
-        if (ctx->pow.base) HIP_TRY(ctx, hipFree(ctx->pow.base));
+        dfree_idle(ctx, ctx->pow.base);
         ctx->pow = PowTables{np, pcap};
     }
     ctx->d_keys = nk;
@@ -381,12 +435,12 @@ int take_kstage(qpp_ctx *ctx, size_t bytes, KStage **out) {
         size_t cap = std::max<size_t>(1 << 16, k.cap);
         while (cap < bytes) cap *= 2;
         RC_TRY(quiet_for_free(ctx));
-        if (k.d) hipFree(k.d);
-        if (k.h) { secure_zero(k.h, k.cap); hipHostFree(k.h); }
+        dfree_idle(ctx, k.d);  // (its last job, the previous user of this stage, is done)
+        if (k.h) { secure_zero(k.h, k.cap); hfree(ctx, k.h); }
         k.d = nullptr;
         k.h = nullptr;
         k.cap = 0;
-        HIP_TRY(ctx, hipMalloc(&k.d, cap));
+        HIP_TRY(ctx, dmalloc(ctx, &k.d, cap));
         HIP_TRY(ctx, hipHostMalloc(&k.h, cap, hipHostMallocDefault));
         k.cap = cap;
     }
@@ -438,21 +492,20 @@ void mark_dirty(qpp_ctx *ctx, uint32_t slot) {
 int ensure_plan(qpp_ctx *ctx, StreamState *st, uint32_t n) {
     if (n <= st->plan_n_cap && ctx->key_cap <= st->plan_key_cap) return QPP_OK;
     HIP_TRY(ctx, hipStreamSynchronize(st->stream));  // the old scratch is no longer read
-    RC_TRY(quiet_for_free(ctx));
     PlanBuffers &p = st->plan;
-    free_plan(p);
+    free_plan(ctx, p);
     st->plan_n_cap = st->plan_key_cap = 0;
     const uint32_t ncap = std::max(n, st->plan_n_cap), kcap = ctx->key_cap;
-    HIP_TRY(ctx, hipMalloc(&p.counts, sizeof(uint32_t) * kcap));
+    HIP_TRY(ctx, dmalloc(ctx, &p.counts, sizeof(uint32_t) * kcap));
     // zeroed on the batch's own stream: plan_hist on this stream follows it.  (A plain hipMemset goes to the null
     // stream, which does not order against non-blocking streams: with recycled device memory plan_hist then counted
     // on top of stale words and the scatter wrote past perm[] -- an illegal address under two concurrent streams.)
     HIP_TRY(ctx, hipMemsetAsync(p.counts, 0, sizeof(uint32_t) * kcap, st->stream));  // plan_scan re-zeroes it after each plan
-    HIP_TRY(ctx, hipMalloc(&p.cursor, sizeof(uint32_t) * kcap));
-    HIP_TRY(ctx, hipMalloc(&p.istart, sizeof(uint32_t) * 2 * (kcap + 1)));
-    HIP_TRY(ctx, hipMalloc(&p.perm, sizeof(uint32_t) * std::max<uint32_t>(ncap, 1)));
-    HIP_TRY(ctx, hipMalloc(&p.work, sizeof(WorkItem) * (plan_max_work(ncap, kcap, kMinPacketsPerItem) + 1)));
-    HIP_TRY(ctx, hipMalloc(&p.n_work, 8 * sizeof(uint32_t)));
+    HIP_TRY(ctx, dmalloc(ctx, &p.cursor, sizeof(uint32_t) * kcap));
+    HIP_TRY(ctx, dmalloc(ctx, &p.istart, sizeof(uint32_t) * 2 * (kcap + 1)));
+    HIP_TRY(ctx, dmalloc(ctx, &p.perm, sizeof(uint32_t) * std::max<uint32_t>(ncap, 1)));
+    HIP_TRY(ctx, dmalloc(ctx, &p.work, sizeof(WorkItem) * (plan_max_work(ncap, kcap, kMinPacketsPerItem) + 1)));
+    HIP_TRY(ctx, dmalloc(ctx, &p.n_work, 8 * sizeof(uint32_t)));
     HIP_TRY(ctx, hipMemsetAsync(p.n_work, 0, 8 * sizeof(uint32_t), st->stream));  // (meta[6] is a running count)
     st->plan_n_cap = ncap;
     st->plan_key_cap = kcap;
@@ -462,18 +515,17 @@ int ensure_plan(qpp_ctx *ctx, StreamState *st, uint32_t n) {
 // FIPS gate scratch for batches of up to n packets on st (plus its refused-packet counter)
 int ensure_fips(qpp_ctx *ctx, StreamState *st, uint32_t n) {
     if (!st->fips_refused) {
-        HIP_TRY(ctx, hipMalloc(&st->fips_refused, 256));
+        HIP_TRY(ctx, dmalloc(ctx, &st->fips_refused, 256));
         HIP_TRY(ctx, hipMemsetAsync(st->fips_refused, 0, 4, st->stream));
     }
     if (n <= st->fips_n_cap) return QPP_OK;
     HIP_TRY(ctx, hipStreamSynchronize(st->stream));  // the old scratch is no longer read
-    RC_TRY(quiet_for_free(ctx));
-    hipFree(st->fips_buf);
+    dfree_idle(ctx, st->fips_buf);
     st->fips_buf = nullptr;
     st->fips_n_cap = 0;
     const uint32_t cap = std::max<uint32_t>(n, 1024);
     st->fips_bytes = fips_scratch_bytes(cap);
-    HIP_TRY(ctx, hipMalloc(&st->fips_buf, st->fips_bytes));
+    HIP_TRY(ctx, dmalloc(ctx, &st->fips_buf, st->fips_bytes));
     st->fips_n_cap = cap;
     return QPP_OK;
 }
@@ -500,11 +552,11 @@ int ensure_stage(qpp_ctx *ctx, size_t bytes) {
     while (cap < bytes) cap *= 2;
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     RC_TRY(quiet_for_free(ctx));
-    if (ctx->d_stage) hipFree(ctx->d_stage);
-    if (ctx->h_stage) hipHostFree(ctx->h_stage);
+    dfree_idle(ctx, ctx->d_stage);
+    hfree(ctx, ctx->h_stage);
     ctx->d_stage = ctx->h_stage = ctx->v_stage = nullptr;
     ctx->stage_cap = 0;
-    HIP_TRY(ctx, hipMalloc(&ctx->d_stage, cap));
+    HIP_TRY(ctx, dmalloc(ctx, &ctx->d_stage, cap));
     HIP_TRY(ctx, hipHostMalloc(&ctx->h_stage, cap, hipHostMallocDefault));
     void *v = nullptr;
     HIP_TRY(ctx, hipHostGetDevicePointer(&v, ctx->h_stage, 0));
@@ -957,10 +1009,10 @@ int pipe_init(qpp_ctx *ctx) {
     if (p->slots.size() == p->nslots && !p->slots.empty() && p->slots[0].arena) return QPP_OK;
     p->slots.resize(p->nslots);
     for (PipeSlot &sl : p->slots) {
-        HIP_TRY(ctx, hipMalloc(&sl.arena, p->chunk_bytes));
-        HIP_TRY(ctx, hipMalloc(&sl.descs, sizeof(qpp_pkt) * p->chunk_packets));
-        HIP_TRY(ctx, hipMalloc(&sl.masks, 5 * p->chunk_packets));
-        HIP_TRY(ctx, hipMalloc(&sl.status, p->chunk_packets));
+        HIP_TRY(ctx, dmalloc(ctx, &sl.arena, p->chunk_bytes));
+        HIP_TRY(ctx, dmalloc(ctx, &sl.descs, sizeof(qpp_pkt) * p->chunk_packets));
+        HIP_TRY(ctx, dmalloc(ctx, &sl.masks, 5 * p->chunk_packets));
+        HIP_TRY(ctx, dmalloc(ctx, &sl.status, p->chunk_packets));
         HIP_TRY(ctx, hipEventCreateWithFlags(&sl.h2d, hipEventDisableTiming));
         HIP_TRY(ctx, hipEventCreateWithFlags(&sl.comp, hipEventDisableTiming));
         HIP_TRY(ctx, hipEventCreateWithFlags(&sl.d2h, hipEventDisableTiming));
@@ -973,14 +1025,15 @@ int pipe_init(qpp_ctx *ctx) {
 void pipe_release(qpp_ctx *ctx) {
     HostPipe *p = ctx->pipe;
     if (!p) return;
-    quiet_for_free(ctx);
+    for (hipStream_t s : {p->h2d, p->comp, p->d2h})
+        if (s) hipStreamSynchronize(s);  // no chunk is in flight
     for (PipeSlot &sl : p->slots) {
         if (sl.arena) {
             hipMemsetAsync(sl.arena, 0, p->chunk_bytes, ctx->stream);
             hipStreamSynchronize(ctx->stream);
-            hipFree(sl.arena);
+            dfree_idle(ctx, sl.arena);
         }
-        hipFree(sl.descs); hipFree(sl.masks); hipFree(sl.status);
+        dfree_idle(ctx, sl.descs); dfree_idle(ctx, sl.masks); dfree_idle(ctx, sl.status);
         if (sl.h2d) hipEventDestroy(sl.h2d);
         if (sl.comp) hipEventDestroy(sl.comp);
         if (sl.d2h) hipEventDestroy(sl.d2h);
@@ -1018,12 +1071,15 @@ int qpp_ctx_create(int device, qpp_ctx **out) {
         if (fail(ctx, hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking), "stream") ||
             fail(ctx, hipStreamCreateWithFlags(&ctx->kstream, hipStreamNonBlocking), "key stream") ||
             fail(ctx, hipStreamCreateWithFlags(&ctx->rstream, hipStreamNonBlocking), "retire stream") ||
+            fail(ctx, hipStreamCreateWithFlags(&ctx->astream, hipStreamNonBlocking), "allocation stream") ||
             fail(ctx, hipEventCreateWithFlags(&ctx->keys_ready, hipEventDisableTiming), "key event")) {
             rc = QPP_DEVICE_ERROR;
             break;
         }
         if (!stream_state(ctx, ctx->stream)) { rc = QPP_DEVICE_ERROR; break; }
-        if (fail(ctx, hipMalloc(&ctx->d_diag, 64), "diag") || fail(ctx, hipMemset(ctx->d_diag, 0, 64), "diag")) {
+        if (fail(ctx, dmalloc(ctx, &ctx->d_diag, 64), "diag") ||
+            fail(ctx, hipMemsetAsync(ctx->d_diag, 0, 64, ctx->astream), "diag") ||
+            fail(ctx, hipStreamSynchronize(ctx->astream), "diag")) {
             rc = QPP_DEVICE_ERROR;
             break;
         }
@@ -1067,19 +1123,20 @@ void qpp_ctx_destroy(qpp_ctx *ctx) {
     ctx->pkt_q = nullptr;
     if (ctx->d_keys) flush_retire(ctx);  // pending zeroizations, while the table and the stream states still exist
     servers_stop(ctx);
-    hipDeviceSynchronize();
+    ctx_sync(ctx);  // (the context's streams only: another context's resident servers may run on)
     if (ctx->d_keys) {
         hipMemsetAsync(ctx->d_keys, 0, sizeof(DevKey) * ctx->key_cap, ctx->stream);
         hipStreamSynchronize(ctx->stream);
-        hipFree(ctx->d_keys);
+        dfree_idle(ctx, ctx->d_keys);
     }
     secure_zero(ctx->h_keys.data(), sizeof(DevKey) * ctx->h_keys.size());
     if (ctx->pow.base) {
         hipMemsetAsync(ctx->pow.base, 0, (size_t)ctx->pow.cap * kPowBytes, ctx->stream);
         hipStreamSynchronize(ctx->stream);
-        hipFree(ctx->pow.base);
+        dfree_idle(ctx, ctx->pow.base);
     }
-    for (StreamState *st : ctx->streams) free_stream_state(st);
+    for (StreamState *st : ctx->streams) free_stream_state(ctx, st);
+    ctx->streams.clear();
     for (Retired &r : ctx->retired) hipEventDestroy(r.done);
     for (hipEvent_t e : ctx->event_pool) hipEventDestroy(e);
     if (ctx->pipe) {
@@ -1090,16 +1147,20 @@ void qpp_ctx_destroy(qpp_ctx *ctx) {
         if (ctx->pipe->d2h) hipStreamDestroy(ctx->pipe->d2h);
         delete ctx->pipe;
     }
-    hipFree(ctx->d_stage);
-    hipFree(ctx->d_connmap);
-    hipFree(ctx->d_diag);
-    if (ctx->h_connstage) hipHostFree(ctx->h_connstage);
+    dfree_idle(ctx, ctx->d_stage);
+    dfree_idle(ctx, ctx->d_connmap);
+    dfree_idle(ctx, ctx->d_diag);
+    hfree(ctx, ctx->h_connstage);
     if (ctx->connstage_ev) hipEventDestroy(ctx->connstage_ev);
-    if (ctx->h_stage) hipHostFree(ctx->h_stage);
+    hfree(ctx, ctx->h_stage);
     for (KStage &k : ctx->kstage) {
-        hipFree(k.d);
-        if (k.h) { secure_zero(k.h, k.cap); hipHostFree(k.h); }
+        dfree_idle(ctx, k.d);
+        if (k.h) { secure_zero(k.h, k.cap); hfree(ctx, k.h); }
         if (k.free_ev) hipEventDestroy(k.free_ev);
+    }
+    if (ctx->astream) {
+        hipStreamSynchronize(ctx->astream);  // the frees above are done
+        hipStreamDestroy(ctx->astream);
     }
     if (ctx->stream) hipStreamDestroy(ctx->stream);
     if (ctx->kstream) hipStreamDestroy(ctx->kstream);
@@ -1115,7 +1176,8 @@ int qpp_ctx_synchronize(qpp_ctx *ctx) {
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     RC_TRY(flush_retire(ctx));
     RC_TRY(servers_stop(ctx));  // (restarted by the next flush of their queue)
-    HIP_TRY(ctx, hipDeviceSynchronize());
+    RC_TRY(ctx_sync(ctx));      // every stream of the context (not the device: other contexts' servers run on)
+    hfree(ctx, nullptr);        // pinned buffers parked while other contexts' servers were resident
     return QPP_OK;
 }
 
@@ -1126,7 +1188,8 @@ int qpp_ctx_rx_timeouts(qpp_ctx *ctx, uint64_t *count) {
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     for (StreamState *st : ctx->streams) HIP_TRY(ctx, hipStreamSynchronize(st->stream));
     uint32_t v = 0;
-    HIP_TRY(ctx, hipMemcpy(&v, ctx->d_diag, 4, hipMemcpyDeviceToHost));
+    HIP_TRY(ctx, hipMemcpyAsync(&v, ctx->d_diag, 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     *count = v;
     return QPP_OK;
 }
@@ -1541,11 +1604,10 @@ int qpp_unprotect_open_batch(qpp_ctx *ctx, const qpp_rx_pkt *rx, size_t n, uint8
         const uint32_t kc = ctx->key_cap;
         if (st->rx_scratch_keys < kc) {
             HIP_TRY(ctx, hipStreamSynchronize(st->stream));  // the old scratch is no longer read
-            RC_TRY(quiet_for_free(ctx));
-            hipFree(st->rx_scratch);
+            dfree_idle(ctx, st->rx_scratch);
             st->rx_scratch = nullptr;
             st->rx_scratch_keys = 0;
-            HIP_TRY(ctx, hipMalloc(&st->rx_scratch, 4 * (16 + 2 * (size_t)kc + 4 + 4 * ((size_t)kc + 1))));
+            HIP_TRY(ctx, dmalloc(ctx, &st->rx_scratch, 4 * (16 + 2 * (size_t)kc + 4 + 4 * ((size_t)kc + 1))));
             st->rx_scratch_keys = kc;
         }
         HIP_TRY(ctx, hipMemsetAsync(st->rx_scratch, 0, 4 * (16 + 2 * (size_t)kc), st->stream));
@@ -1626,7 +1688,7 @@ int qpp_ctx_set_host_pipe(qpp_ctx *ctx, size_t chunk_packets, size_t chunk_bytes
         return QPP_INTERNAL_ERROR;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     RC_TRY(servers_stop(ctx));
-    HIP_TRY(ctx, hipDeviceSynchronize());
+    RC_TRY(ctx_sync(ctx));
     if (!ctx->pipe) ctx->pipe = new HostPipe();
     pipe_release(ctx);
     ctx->pipe->chunk_packets = chunk_packets;
@@ -1725,12 +1787,11 @@ int qpp_ctx_set_conn_keys(qpp_ctx *ctx, const uint32_t *slots, size_t n) {
     hipStream_t s = ctx->pipe->comp;  // the remap launches' stream: earlier batches read the old table first
     if (n > ctx->connmap_cap) {
         HIP_TRY(ctx, hipStreamSynchronize(s));
-        RC_TRY(quiet_for_free(ctx));
-        hipFree(ctx->d_connmap);
+        dfree(ctx, ctx->d_connmap);  // (behind every stream: conn-keyed batches of any stream read it)
         ctx->d_connmap = nullptr;
         ctx->connmap_cap = ctx->connmap_n = 0;
         const size_t cap = std::max<size_t>(n, 1024);
-        HIP_TRY(ctx, hipMalloc(&ctx->d_connmap, 4 * cap));
+        HIP_TRY(ctx, dmalloc(ctx, &ctx->d_connmap, 4 * cap));
         ctx->connmap_cap = cap;
     }
     // through the pinned stage: the caller may reuse `slots` on return (the previous copy from the stage is waited
@@ -1740,7 +1801,7 @@ int qpp_ctx_set_conn_keys(qpp_ctx *ctx, const uint32_t *slots, size_t n) {
     ctx->connstage_used = false;
     if (n > ctx->connstage_cap) {
         RC_TRY(quiet_for_free(ctx));
-        if (ctx->h_connstage) hipHostFree(ctx->h_connstage);
+        hfree(ctx, ctx->h_connstage);
         ctx->h_connstage = nullptr;
         ctx->connstage_cap = 0;
         const size_t cap = std::max<size_t>(n, 1024);
@@ -1782,14 +1843,13 @@ int qpp_host_batch_wait(qpp_ctx *ctx, uint64_t ticket) {
 
 int qpp_dev_alloc(qpp_ctx *ctx, size_t bytes, void **out) {
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    HIP_TRY(ctx, hipMalloc(out, bytes ? bytes : 1));
+    HIP_TRY(ctx, dmalloc(ctx, out, bytes));
     return QPP_OK;
 }
 void qpp_dev_free(qpp_ctx *ctx, void *ptr) {
     if (!ptr) return;
     hipSetDevice(ctx->device);
-    quiet_for_free(ctx);
-    hipFree(ptr);
+    dfree(ctx, ptr);  // behind the work every stream of the context has been given so far
 }
 int qpp_host_alloc(qpp_ctx *ctx, size_t bytes, void **out) {
     HIP_TRY(ctx, hipSetDevice(ctx->device));
@@ -1798,8 +1858,12 @@ int qpp_host_alloc(qpp_ctx *ctx, size_t bytes, void **out) {
 }
 void qpp_host_free(qpp_ctx *ctx, void *ptr) {
     if (!ptr) return;
-    if (ctx) quiet_for_free(ctx);
-    hipHostFree(ptr);
+    if (!ctx) {
+        hipHostFree(ptr);
+        return;
+    }
+    quiet_for_free(ctx);  // (hipHostFree waits for every stream of the device: the context's own servers first)
+    hfree(ctx, ptr);
 }
 int qpp_memcpy_d2d(qpp_ctx *ctx, void *dst, const void *src, size_t bytes, void *stream) {
     HIP_TRY(ctx, hipSetDevice(ctx->device));
@@ -1834,7 +1898,7 @@ void qpp_stream_destroy(qpp_ctx *ctx, void *stream) {
         for (size_t i = 0; i < ctx->streams.size(); i++) {
             StreamState *st = ctx->streams[i];
             if (st->stream != s) continue;
-            free_stream_state(st);
+            free_stream_state(ctx, st);
             ctx->streams.erase(ctx->streams.begin() + (long)i);
             break;
         }
@@ -1945,6 +2009,22 @@ uint32_t resident_wgs_locked(const DevServers &r) {
     for (const qpp_txq *o : r.queues)
         if (srv_resident(o)) w += o->srv_wgs;
     return w;
+}
+
+// hipHostFree waits for every stream of the device: at once only while no other context's server is resident (the
+// caller stopped its own), else parked; p = nullptr only frees what is parked, if it can.  Under the registry lock,
+// so no server starts between the check and the free.
+void hfree(qpp_ctx *ctx, void *p) {
+    DevServers &r = dev_servers(ctx->device);
+    std::lock_guard<std::mutex> lk(r.mu);
+    for (const qpp_txq *o : r.queues)
+        if (o->ctx != ctx && srv_resident(o)) {
+            if (p) r.parked.push_back(p);
+            return;
+        }
+    for (void *x : r.parked) hipHostFree(x);
+    r.parked.clear();
+    if (p) hipHostFree(p);
 }
 
 uint32_t srv_next(uint32_t s) { return s + 1u ? s + 1u : 1u; }  // 0 is never a flush's seq
@@ -2072,7 +2152,7 @@ static int txq_create(qpp_ctx *ctx, size_t ring_bytes, size_t max_packets, size_
         return true;
     };
     if (bad(hipHostMalloc(&q->h_ring, ring_bytes, ring_flags), "txq ring") ||
-        bad(hipMalloc(&q->d_ring, ring_bytes), "txq ring") || bad(hipHostGetDevicePointer(&v, q->h_ring, 0), "ring view"))
+        bad(dmalloc(ctx, &q->d_ring, ring_bytes), "txq ring") || bad(hipHostGetDevicePointer(&v, q->h_ring, 0), "ring view"))
         return QPP_DEVICE_ERROR;
     q->v_ring = (uint8_t *)v;
     // one stream per in-flight flush up to 4 (the hardware queues a process gets), shared round-robin beyond
@@ -2087,7 +2167,7 @@ static int txq_create(qpp_ctx *ctx, size_t ring_bytes, size_t max_packets, size_
         TxqSlot &sl = q->slots[i];
         sl.stream = q->streams[i % nstreams];
         if (bad(hipHostMalloc(&sl.h_desc, sizeof(qpp_pkt) * max_packets, hipHostMallocDefault), "txq descs") ||
-            bad(hipMalloc(&sl.d_desc, sizeof(qpp_pkt) * max_packets), "txq descs") ||
+            bad(dmalloc(ctx, &sl.d_desc, sizeof(qpp_pkt) * max_packets), "txq descs") ||
             bad(hipHostMalloc(&sl.h_perm, 4 * (max_packets + 4) + sizeof(WorkItem) * (max_packets + 1),
                               hipHostMallocDefault), "txq plan") ||
             bad(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming), "txq event") ||
@@ -2131,24 +2211,24 @@ void qpp_txq_destroy(qpp_txq *q) {
             r.queues.erase(std::remove(r.queues.begin(), r.queues.end(), q), r.queues.end());
         }
         if (q->srv_stream) { hipStreamSynchronize(q->srv_stream); hipStreamDestroy(q->srv_stream); }
-        if (q->h_mail) hipHostFree(q->h_mail);
-        if (q->h_slots) { secure_zero(q->h_slots, sizeof(TxsSlot) * q->srv_wgs); hipHostFree(q->h_slots); }
-        if (q->h_items) hipHostFree(q->h_items);
-        if (q->h_sdesc) { secure_zero(q->h_sdesc, sizeof(qpp_pkt) * q->max_packets * kTxsWaves); hipHostFree(q->h_sdesc); }
+        hfree(q->ctx, q->h_mail);
+        if (q->h_slots) { secure_zero(q->h_slots, sizeof(TxsSlot) * q->srv_wgs); hfree(q->ctx, q->h_slots); }
+        hfree(q->ctx, q->h_items);
+        if (q->h_sdesc) { secure_zero(q->h_sdesc, sizeof(qpp_pkt) * q->max_packets * kTxsWaves); hfree(q->ctx, q->h_sdesc); }
     }
     for (hipStream_t st : q->streams) hipStreamSynchronize(st);
-    if (q->h_ring) { secure_zero(q->h_ring, q->ring_bytes); hipHostFree(q->h_ring); }
+    if (q->h_ring) { secure_zero(q->h_ring, q->ring_bytes); hfree(q->ctx, q->h_ring); }
     if (q->d_ring) {
         hipMemsetAsync(q->d_ring, 0, q->ring_bytes, q->ctx->stream);
         hipStreamSynchronize(q->ctx->stream);
-        hipFree(q->d_ring);
+        dfree_idle(q->ctx, q->d_ring);
     }
     for (TxqSlot &sl : q->slots) {
-        if (sl.h_desc) hipHostFree(sl.h_desc);
-        if (sl.d_desc) hipFree(sl.d_desc);
-        if (sl.h_perm) hipHostFree(sl.h_perm);
+        hfree(q->ctx, sl.h_desc);
+        dfree_idle(q->ctx, sl.d_desc);  // (the queue's streams are synchronized above)
+        hfree(q->ctx, sl.h_perm);
         if (sl.done) hipEventDestroy(sl.done);
-        if (sl.h_refused) hipHostFree(sl.h_refused);
+        hfree(q->ctx, sl.h_refused);
     }
     for (hipStream_t st : q->streams) {
         // the stream's StreamState (plan scratch of the DMA path) goes with it

@@ -488,7 +488,7 @@ class Context:
         return c.value
 
     def synchronize(self):
-        """whole device (qpp_ctx_synchronize): every stream, key installs and retirements included"""
+        """qpp_ctx_synchronize: every stream of this context (key installs and retirements included), not the device"""
         self._check(lib().qpp_ctx_synchronize(self.handle), "synchronize")
 
     def wait(self, stream, ev):

@@ -70,8 +70,8 @@ def test_server_matches_launched_path():
 
 
 def test_server_restarts_and_long_packets(monkeypatch):
-    """the server leaves on its idle time and is stopped by a free (hipFree waits for every stream); the next call
-    restarts it.  A packet over the
+    """the server leaves on its idle time, and a pinned free stops it (hipHostFree waits for every stream of the
+    device); the next call restarts it.  A device free does not stop it (stream-ordered free).  A packet over the
     ring (16 KiB) and a FIPS seal take the launched path, identical bytes."""
     monkeypatch.setenv("QPP_TXQ_SERVER_IDLE_MS", "20")
     rng = np.random.default_rng(7300)
@@ -91,7 +91,9 @@ def test_server_restarts_and_long_packets(monkeypatch):
         s0 = ctx.packet_server_info()[1]
         time.sleep(0.1)  # past the idle time: the server left
         one(2, 1200)
-        ctx.alloc(4096).free()  # a free stops the context's servers
+        assert ctx.packet_server_info()[1] >= s0 + 1
+        h = ctx.host_alloc(4096)
+        ctx.host_free(h)  # a pinned free stops the context's servers
         one(3, 1200)
         assert ctx.packet_server_info()[1] >= s0 + 2
         served = ctx.packet_server_info()[0]
@@ -105,6 +107,37 @@ def test_server_restarts_and_long_packets(monkeypatch):
         assert ctx.packet_server_info()[0] == served  # FIPS seal: launched (nonce-order gate)
         with pytest.raises(qpp.QppError):
             f.encrypt(10, header, payload)  # the same packet number again: refused
+    finally:
+        ctx.close()
+
+
+def test_device_free_keeps_the_server(monkeypatch):
+    """qpp_dev_free is stream-ordered (hipFreeAsync behind the context's streams): the packet server stays resident
+    (one launch for every call), while a pinned free stops it and the next call restarts it"""
+    monkeypatch.setenv("QPP_TXQ_SERVER_IDLE_MS", "10000")
+    rng = np.random.default_rng(7301)
+    ctx = qpp.Context(0)
+    try:
+        k = ctx.key(1, rng.integers(0, 256, 32, dtype=np.uint8).tobytes())
+        kk, iv, _ = k.material()
+        header = bytes(21)
+
+        def one(pn):
+            payload = rng.integers(0, 256, 700, dtype=np.uint8).tobytes()
+            assert k.encrypt(pn, header, payload) == b"".join(orc.seal(1, kk, orc.nonce(iv, pn), header, payload))
+
+        one(1)
+        starts = ctx.packet_server_info()[1]
+        for i in range(5):
+            b = ctx.alloc(1 << 20)
+            b.upload(np.full(1 << 20, i, dtype=np.uint8))
+            b.free()
+            one(2 + i)
+        assert ctx.packet_server_info()[1] == starts
+        h = ctx.host_alloc(4096)
+        ctx.host_free(h)
+        one(10)
+        assert ctx.packet_server_info()[1] == starts + 1
     finally:
         ctx.close()
 

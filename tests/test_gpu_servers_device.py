@@ -222,3 +222,78 @@ def test_two_fused_receives_on_two_streams():
         assert ctx.rx_timeouts() == 0
     finally:
         ctx.close()
+
+
+def test_other_context_frees_and_syncs_do_not_wait_for_a_resident_server(monkeypatch):
+    """hipFree / hipHostFree / hipDeviceSynchronize wait for every stream of the device, another context's resident
+    server too (tools/diag/free_sync.hip: 1950 ms beside a 2-s kernel), and a context cannot stop another's servers.
+    Context B keeps a persistent transmit queue and a packet server resident (20 s idle); context A allocates and frees
+    device and pinned memory, grows its key table, synchronizes and closes: every call returns at once, and B's server
+    was never restarted (its flushes before and after stay bit-exact on one server launch)."""
+    monkeypatch.setenv("QPP_TXQ_SERVER_IDLE_MS", "20000")
+    rng = np.random.default_rng(5053)
+    b = qpp.Context(0)
+    q = None
+    try:
+        kb = b.key(1, rng.integers(0, 256, 32, dtype=np.uint8).tobytes())
+        q = qpp.TxQueue(b, 64 * STRIDE, 64, persistent=True)
+        pn = [5000]
+
+        def flush():
+            want = []
+            for i in range(64):
+                header = bytes([0x43]) + rng.integers(0, 256, 16, dtype=np.uint8).tobytes()
+                payload = rng.integers(0, 256, 1100, dtype=np.uint8).tobytes()
+                trunc, pn_len = qpp.pn_truncate(pn[0] + i, pn[0] - 1)
+                pkt = header + trunc.to_bytes(pn_len, "big") + payload
+                q.ring[i * STRIDE:i * STRIDE + len(pkt)] = np.frombuffer(pkt, dtype=np.uint8)
+                q.push(kb, pn[0] + i, i * STRIDE, len(header), pn_len, len(payload))
+                kk, iv, hp = kb.material()
+                want.append((i * STRIDE, orc.protect_packet(1, kk, iv, hp, pn[0] + i, header, pn_len, payload)[1]))
+            q.flush()
+            for off, p in want:
+                assert q.ring[off:off + len(p)].tobytes() == p
+            pn[0] += 64
+
+        flush()
+        _seal_one(rng, kb, 1)  # B's packet server is resident too
+        assert q.info()[2] == 1
+
+        a = qpp.Context(0)
+        times = {}
+
+        def timed(name, f):
+            t0 = time.perf_counter()
+            r = f()
+            times[name] = time.perf_counter() - t0
+            return r
+
+        d = timed("dev_alloc", lambda: a.alloc(1 << 24))
+        d.upload(np.arange(1 << 24, dtype=np.uint64).astype(np.uint8))
+        timed("dev_free", d.free)
+        h = timed("host_alloc", lambda: a.host_alloc(1 << 20))
+        timed("host_free", lambda: a.host_free(h))
+        keys = timed("key_table_growth", lambda: [a.key(2, rng.integers(0, 256, 48, dtype=np.uint8).tobytes())
+                                                  for _ in range(80)])  # past the 64-slot table: grow_keys
+        descs, arena = qpp.make_batch(4096, 1200, [k.slot for k in keys], seed=9)
+        da, dd, ds = a.alloc(arena.nbytes), a.alloc(descs.nbytes), a.alloc(4096)
+        da.upload(arena)
+        dd.upload(descs)
+        a.seal_batch(dd, 4096, da, None, ds)
+        timed("synchronize", a.synchronize)
+        assert (ds.download(dtype=np.int8) == 0).all()
+        _seal_one(rng, keys[0], 2)  # A's own packet server: stopped by its close below
+        timed("close", a.close)
+        print({k: round(1e3 * v, 2) for k, v in times.items()}, "ms")
+        for name, dt in times.items():
+            assert dt < 2.0, (name, dt)  # (the 20-s idle server of B would hold each for 20 s)
+
+        flush()
+        _seal_one(rng, kb, 1)
+        served, launched, starts = q.info()
+        assert (served, launched, starts) == (2, 0, 1)  # one server launch for both flushes: never stopped
+        assert q.server_refused() == 0
+    finally:
+        if q is not None:
+            q.close()
+        b.close()

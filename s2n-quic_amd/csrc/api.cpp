@@ -218,7 +218,9 @@ struct DevServers {
     std::vector<qpp_txq *> queues;  // the persistent queues of every context on the device
     hipEvent_t rx_tail = nullptr;   // recorded behind the device's latest fused receive
     std::vector<void *> parked;     // pinned buffers whose hipHostFree waits for no resident server (hfree)
+    size_t parked_bytes = 0;
 };
+constexpr size_t kParkedMax = size_t(1) << 30;  // past this, hfree frees at once (and waits)
 DevServers &dev_servers(int device) {
     static DevServers regs[64];
     return regs[(unsigned)device & 63u];
@@ -2012,18 +2014,28 @@ uint32_t resident_wgs_locked(const DevServers &r) {
 }
 
 // hipHostFree waits for every stream of the device: at once only while no other context's server is resident (the
-// caller stopped its own), else parked; p = nullptr only frees what is parked, if it can.  Under the registry lock,
-// so no server starts between the check and the free.
+// caller stopped its own), else parked -- up to kParkedMax bytes per device, past which the free happens anyway and
+// waits (a bound on what a context that keeps freeing pinned memory beside a busy server can hold); p = nullptr
+// only frees what is parked, if it can.  Under the registry lock, so no server starts between the check and the free.
 void hfree(qpp_ctx *ctx, void *p) {
     DevServers &r = dev_servers(ctx->device);
     std::lock_guard<std::mutex> lk(r.mu);
+    bool others = false;
     for (const qpp_txq *o : r.queues)
-        if (o->ctx != ctx && srv_resident(o)) {
-            if (p) r.parked.push_back(p);
+        if (o->ctx != ctx && srv_resident(o)) others = true;
+    if (others && p) {
+        size_t bytes = 0;
+        if (hipMemPtrGetInfo(p, &bytes) != hipSuccess) bytes = 0;
+        if (r.parked_bytes + bytes <= kParkedMax) {
+            r.parked.push_back(p);
+            r.parked_bytes += bytes;
             return;
         }
+    }
+    if (others && !p) return;
     for (void *x : r.parked) hipHostFree(x);
     r.parked.clear();
+    r.parked_bytes = 0;
     if (p) hipHostFree(p);
 }
 

@@ -427,8 +427,8 @@ uint64_t qpp_pn_expand(uint64_t largest_acked, uint64_t truncated, size_t pn_len
  * already enqueued on the context's streams (work the caller enqueued on streams of its own must be complete), and no
  * resident server -- of this context or another -- is stopped or waited for (hipFree waits for every stream of the
  * device).  qpp_host_free stops this context's own servers (hipHostFree waits for every stream of the device); while
- * another context of the device has a resident server the pinned buffer is parked and freed by the next free or
- * qpp_ctx_synchronize of any context that finds none.  No view of a freed buffer may be used afterwards. */
+ * another context of the device has a resident server the pinned buffer is parked (up to 1 GiB per device; past that
+ * the free waits) and freed by the next free or qpp_ctx_synchronize of any context that finds none.  No view of a freed buffer may be used afterwards. */
 int qpp_dev_alloc(qpp_ctx *ctx, size_t bytes, void **out);
 void qpp_dev_free(qpp_ctx *ctx, void *ptr);
 int qpp_host_alloc(qpp_ctx *ctx, size_t bytes, void **out); /* pinned host memory */

@@ -423,12 +423,13 @@ uint64_t qpp_pn_expand(uint64_t largest_acked, uint64_t truncated, size_t pn_len
 
 /* ------------------------------------------------------------------ device plumbing */
 
-/* Device memory from the stream-ordered allocator.  qpp_dev_free returns at once: the memory goes back behind the work
- * already enqueued on the context's streams (work the caller enqueued on streams of its own must be complete), and no
- * resident server -- of this context or another -- is stopped or waited for (hipFree waits for every stream of the
- * device).  qpp_host_free stops this context's own servers (hipHostFree waits for every stream of the device); while
- * another context of the device has a resident server the pinned buffer is parked (up to 1 GiB per device; past that
- * the free waits) and freed by the next free or qpp_ctx_synchronize of any context that finds none.  No view of a freed buffer may be used afterwards. */
+/* hipFree / hipHostFree wait for every stream of the device, a resident server's too (which leaves only on its idle
+ * time, or never while it is fed).  So qpp_dev_free / qpp_host_free -- and every free inside the library -- free at
+ * once only while no server of the device (of any context, this one's included) is resident; otherwise the buffer is
+ * parked (up to 2 GiB per device; past that this context's servers are stopped and the free waits for the others')
+ * and freed by the next free, qpp_ctx_synchronize or qpp_ctx_destroy of any context that finds none resident.  A free
+ * never stops a server and never waits for one; work already enqueued that reads the buffer is unaffected.  No view
+ * of a freed buffer may be used afterwards. */
 int qpp_dev_alloc(qpp_ctx *ctx, size_t bytes, void **out);
 void qpp_dev_free(qpp_ctx *ctx, void *ptr);
 int qpp_host_alloc(qpp_ctx *ctx, size_t bytes, void **out); /* pinned host memory */

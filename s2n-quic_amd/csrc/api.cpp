@@ -101,7 +101,6 @@ struct qpp_ctx {
     hipStream_t stream = nullptr;
     hipStream_t kstream = nullptr;  // key installs / derivations
     hipStream_t rstream = nullptr;  // key retirements (zeroization behind in-flight batches)
-    hipStream_t astream = nullptr;  // device allocations and frees (stream-ordered allocator: dmalloc / dfree)
     hipEvent_t keys_ready = nullptr;
     uint64_t key_gen = 0;           // installs so far (keys_ready marks the latest)
     // device key table + host mirror
@@ -217,10 +216,10 @@ struct DevServers {
     std::mutex mu;
     std::vector<qpp_txq *> queues;  // the persistent queues of every context on the device
     hipEvent_t rx_tail = nullptr;   // recorded behind the device's latest fused receive
-    std::vector<void *> parked;     // pinned buffers whose hipHostFree waits for no resident server (hfree)
+    std::vector<std::pair<void *, bool>> parked;  // buffers (pinned: true) freed once no server is resident (release)
     size_t parked_bytes = 0;
 };
-constexpr size_t kParkedMax = size_t(1) << 30;  // past this, hfree frees at once (and waits)
+constexpr size_t kParkedMax = size_t(2) << 30;  // past this, release frees at once (and waits)
 DevServers &dev_servers(int device) {
     static DevServers regs[64];
     return regs[(unsigned)device & 63u];
@@ -250,18 +249,25 @@ uint32_t cu_avail(const qpp_ctx *ctx) {
 // Memory without device-wide waits.  hipFree, hipHostFree, hipHostUnregister and hipDeviceSynchronize wait for EVERY
 // stream of the device -- a resident server's too, and a server leaves only on its idle timeout (200 ms by default),
 // or never while its flushes keep coming.  Measured beside a resident kernel (tools/diag/free_sync.hip,
-// profiles/r05/r05v): each of those calls took 1950 ms next to a 2-s kernel; hipMallocAsync, hipFreeAsync,
-// hipHostMalloc, hipMalloc, hipStreamDestroy and hipEventDestroy did not wait.  A context stops its OWN servers before
-// freeing what they read and before a pinned free (quiet_for_free; the next flush or per-packet call restarts them),
-// but it cannot stop another context's, so it never makes a device-wide wait:
-//   * device memory comes from the stream-ordered allocator (dmalloc) and goes back through hipFreeAsync on the
-//     context's allocation stream: dfree_idle when every stream that used the buffer has been synchronized, dfree
-//     behind every stream of the context otherwise (device-side waits, no host wait);
-//   * pinned memory is freed at once when no other context of the device has a resident server, else parked in the
-//     device registry until a context finds none (hfree);
+// profiles/r05/r05v): each of those calls took 1950 ms next to a 2-s kernel; hipMalloc, hipHostMalloc, hipMallocAsync,
+// hipFreeAsync, hipStreamDestroy and hipEventDestroy did not wait.  (The stream-ordered allocator was tried for device
+// memory and corrupted batch buffers in the fuzz test -- 6-8 of 44 seeds, with or without device-wide synchronizes,
+// 0 of 44 with hipMalloc / hipFree: profiles/r05/r05v/fuzzab.txt -- so it is not used.)  Hence:
+//   * device and pinned buffers are freed at once only while no server of the device is resident (any context's,
+//     this one's included), else parked in the device registry and freed by the next free, synchronize or destroy of
+//     any context that finds none resident (release); parked memory is never reused before that hipFree, so work
+//     still reading it is unaffected, and no server is stopped to free memory it does not read;
 //   * a context's synchronize waits for every stream of the context (ctx_sync), never the device.
 int quiet_for_free(qpp_ctx *ctx) { return servers_stop(ctx); }
-void hfree(qpp_ctx *ctx, void *p);  // (with the registry's users below)
+void release(qpp_ctx *ctx, void *p, bool pinned);  // (with the registry's users below)
+void hfree(qpp_ctx *ctx, void *p) { release(ctx, p, true); }
+void dfree(qpp_ctx *ctx, void *p) {
+    if (p) release(ctx, p, false);
+}
+template <class T>
+hipError_t dmalloc(qpp_ctx *, T **p, size_t bytes) {
+    return hipMalloc((void **)p, bytes ? bytes : 1);
+}
 
 bool valid_suite(int s) {
     return s == QPP_SUITE_TLS_AES_128_GCM_SHA256 || s == QPP_SUITE_TLS_AES_256_GCM_SHA384 ||
@@ -301,43 +307,23 @@ std::vector<hipStream_t> ctx_streams(const qpp_ctx *ctx) {
 }
 int ctx_sync(qpp_ctx *ctx) {
     for (hipStream_t s : ctx_streams(ctx)) HIP_TRY(ctx, hipStreamSynchronize(s));
-    if (ctx->astream) HIP_TRY(ctx, hipStreamSynchronize(ctx->astream));
     return QPP_OK;
-}
-template <class T>
-hipError_t dmalloc(qpp_ctx *ctx, T **p, size_t bytes) {
-    const hipError_t e = hipMallocAsync((void **)p, bytes ? bytes : 1, ctx->astream);
-    if (e != hipSuccess) return e;
-    return hipStreamSynchronize(ctx->astream);  // usable on any stream from here on
-}
-void dfree_idle(qpp_ctx *ctx, void *p) {
-    if (p) hipFreeAsync(p, ctx->astream);
-}
-void dfree(qpp_ctx *ctx, void *p) {
-    if (!p) return;
-    for (hipStream_t s : ctx_streams(ctx)) {
-        hipEvent_t e = get_event(ctx);
-        if (!e || hipEventRecord(e, s) != hipSuccess || hipStreamWaitEvent(ctx->astream, e, 0) != hipSuccess)
-            hipStreamSynchronize(s);
-        put_event(ctx, e);
-    }
-    hipFreeAsync(p, ctx->astream);
 }
 
 // (the plan's stream has been synchronized)
 void free_plan(qpp_ctx *ctx, PlanBuffers &p) {
     for (void *b : {(void *)p.counts, (void *)p.cursor, (void *)p.istart, (void *)p.perm, (void *)p.work,
                     (void *)p.n_work})
-        dfree_idle(ctx, b);
+        dfree(ctx, b);
     p = PlanBuffers{};
 }
 void free_stream_state(qpp_ctx *ctx, StreamState *st) {
     hipStreamSynchronize(st->stream);
     if (st->side) hipStreamSynchronize(st->side);
     free_plan(ctx, st->plan);
-    dfree_idle(ctx, st->fips_buf);
-    dfree_idle(ctx, st->fips_refused);
-    dfree_idle(ctx, st->rx_scratch);
+    dfree(ctx, st->fips_buf);
+    dfree(ctx, st->fips_refused);
+    dfree(ctx, st->rx_scratch);
     if (st->side) hipStreamDestroy(st->side);
     if (st->fork_ev) hipEventDestroy(st->fork_ev);
     if (st->join_ev) hipEventDestroy(st->join_ev);
@@ -410,9 +396,9 @@ int grow_keys(qpp_ctx *ctx, uint32_t need) {
         }
     }
     HIP_TRY(ctx, hipStreamSynchronize(ctx->kstream));
-    dfree_idle(ctx, ctx->d_keys);
+    dfree(ctx, ctx->d_keys);
     if (np != ctx->pow.base) {
-        dfree_idle(ctx, ctx->pow.base);
+        dfree(ctx, ctx->pow.base);
         ctx->pow = PowTables{np, pcap};
     }
     ctx->d_keys = nk;
@@ -436,8 +422,7 @@ int take_kstage(qpp_ctx *ctx, size_t bytes, KStage **out) {
     if (bytes > k.cap) {
         size_t cap = std::max<size_t>(1 << 16, k.cap);
         while (cap < bytes) cap *= 2;
-        RC_TRY(quiet_for_free(ctx));
-        dfree_idle(ctx, k.d);  // (its last job, the previous user of this stage, is done)
+        dfree(ctx, k.d);  // (its last job, the previous user of this stage, is done)
         if (k.h) { secure_zero(k.h, k.cap); hfree(ctx, k.h); }
         k.d = nullptr;
         k.h = nullptr;
@@ -522,7 +507,7 @@ int ensure_fips(qpp_ctx *ctx, StreamState *st, uint32_t n) {
     }
     if (n <= st->fips_n_cap) return QPP_OK;
     HIP_TRY(ctx, hipStreamSynchronize(st->stream));  // the old scratch is no longer read
-    dfree_idle(ctx, st->fips_buf);
+    dfree(ctx, st->fips_buf);
     st->fips_buf = nullptr;
     st->fips_n_cap = 0;
     const uint32_t cap = std::max<uint32_t>(n, 1024);
@@ -553,8 +538,7 @@ int ensure_stage(qpp_ctx *ctx, size_t bytes) {
     size_t cap = std::max<size_t>(4096, ctx->stage_cap);
     while (cap < bytes) cap *= 2;
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    RC_TRY(quiet_for_free(ctx));
-    dfree_idle(ctx, ctx->d_stage);
+    dfree(ctx, ctx->d_stage);
     hfree(ctx, ctx->h_stage);
     ctx->d_stage = ctx->h_stage = ctx->v_stage = nullptr;
     ctx->stage_cap = 0;
@@ -1033,9 +1017,9 @@ void pipe_release(qpp_ctx *ctx) {
         if (sl.arena) {
             hipMemsetAsync(sl.arena, 0, p->chunk_bytes, ctx->stream);
             hipStreamSynchronize(ctx->stream);
-            dfree_idle(ctx, sl.arena);
+            dfree(ctx, sl.arena);
         }
-        dfree_idle(ctx, sl.descs); dfree_idle(ctx, sl.masks); dfree_idle(ctx, sl.status);
+        dfree(ctx, sl.descs); dfree(ctx, sl.masks); dfree(ctx, sl.status);
         if (sl.h2d) hipEventDestroy(sl.h2d);
         if (sl.comp) hipEventDestroy(sl.comp);
         if (sl.d2h) hipEventDestroy(sl.d2h);
@@ -1073,15 +1057,14 @@ int qpp_ctx_create(int device, qpp_ctx **out) {
         if (fail(ctx, hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking), "stream") ||
             fail(ctx, hipStreamCreateWithFlags(&ctx->kstream, hipStreamNonBlocking), "key stream") ||
             fail(ctx, hipStreamCreateWithFlags(&ctx->rstream, hipStreamNonBlocking), "retire stream") ||
-            fail(ctx, hipStreamCreateWithFlags(&ctx->astream, hipStreamNonBlocking), "allocation stream") ||
             fail(ctx, hipEventCreateWithFlags(&ctx->keys_ready, hipEventDisableTiming), "key event")) {
             rc = QPP_DEVICE_ERROR;
             break;
         }
         if (!stream_state(ctx, ctx->stream)) { rc = QPP_DEVICE_ERROR; break; }
         if (fail(ctx, dmalloc(ctx, &ctx->d_diag, 64), "diag") ||
-            fail(ctx, hipMemsetAsync(ctx->d_diag, 0, 64, ctx->astream), "diag") ||
-            fail(ctx, hipStreamSynchronize(ctx->astream), "diag")) {
+            fail(ctx, hipMemsetAsync(ctx->d_diag, 0, 64, ctx->stream), "diag") ||
+            fail(ctx, hipStreamSynchronize(ctx->stream), "diag")) {
             rc = QPP_DEVICE_ERROR;
             break;
         }
@@ -1129,13 +1112,13 @@ void qpp_ctx_destroy(qpp_ctx *ctx) {
     if (ctx->d_keys) {
         hipMemsetAsync(ctx->d_keys, 0, sizeof(DevKey) * ctx->key_cap, ctx->stream);
         hipStreamSynchronize(ctx->stream);
-        dfree_idle(ctx, ctx->d_keys);
+        dfree(ctx, ctx->d_keys);
     }
     secure_zero(ctx->h_keys.data(), sizeof(DevKey) * ctx->h_keys.size());
     if (ctx->pow.base) {
         hipMemsetAsync(ctx->pow.base, 0, (size_t)ctx->pow.cap * kPowBytes, ctx->stream);
         hipStreamSynchronize(ctx->stream);
-        dfree_idle(ctx, ctx->pow.base);
+        dfree(ctx, ctx->pow.base);
     }
     for (StreamState *st : ctx->streams) free_stream_state(ctx, st);
     ctx->streams.clear();
@@ -1149,20 +1132,16 @@ void qpp_ctx_destroy(qpp_ctx *ctx) {
         if (ctx->pipe->d2h) hipStreamDestroy(ctx->pipe->d2h);
         delete ctx->pipe;
     }
-    dfree_idle(ctx, ctx->d_stage);
-    dfree_idle(ctx, ctx->d_connmap);
-    dfree_idle(ctx, ctx->d_diag);
+    dfree(ctx, ctx->d_stage);
+    dfree(ctx, ctx->d_connmap);
+    dfree(ctx, ctx->d_diag);
     hfree(ctx, ctx->h_connstage);
     if (ctx->connstage_ev) hipEventDestroy(ctx->connstage_ev);
     hfree(ctx, ctx->h_stage);
     for (KStage &k : ctx->kstage) {
-        dfree_idle(ctx, k.d);
+        dfree(ctx, k.d);
         if (k.h) { secure_zero(k.h, k.cap); hfree(ctx, k.h); }
         if (k.free_ev) hipEventDestroy(k.free_ev);
-    }
-    if (ctx->astream) {
-        hipStreamSynchronize(ctx->astream);  // the frees above are done
-        hipStreamDestroy(ctx->astream);
     }
     if (ctx->stream) hipStreamDestroy(ctx->stream);
     if (ctx->kstream) hipStreamDestroy(ctx->kstream);
@@ -1606,7 +1585,7 @@ int qpp_unprotect_open_batch(qpp_ctx *ctx, const qpp_rx_pkt *rx, size_t n, uint8
         const uint32_t kc = ctx->key_cap;
         if (st->rx_scratch_keys < kc) {
             HIP_TRY(ctx, hipStreamSynchronize(st->stream));  // the old scratch is no longer read
-            dfree_idle(ctx, st->rx_scratch);
+            dfree(ctx, st->rx_scratch);
             st->rx_scratch = nullptr;
             st->rx_scratch_keys = 0;
             HIP_TRY(ctx, dmalloc(ctx, &st->rx_scratch, 4 * (16 + 2 * (size_t)kc + 4 + 4 * ((size_t)kc + 1))));
@@ -1802,7 +1781,6 @@ int qpp_ctx_set_conn_keys(qpp_ctx *ctx, const uint32_t *slots, size_t n) {
     if (ctx->connstage_used) HIP_TRY(ctx, hipEventSynchronize(ctx->connstage_ev));
     ctx->connstage_used = false;
     if (n > ctx->connstage_cap) {
-        RC_TRY(quiet_for_free(ctx));
         hfree(ctx, ctx->h_connstage);
         ctx->h_connstage = nullptr;
         ctx->connstage_cap = 0;
@@ -1864,8 +1842,7 @@ void qpp_host_free(qpp_ctx *ctx, void *ptr) {
         hipHostFree(ptr);
         return;
     }
-    quiet_for_free(ctx);  // (hipHostFree waits for every stream of the device: the context's own servers first)
-    hfree(ctx, ptr);
+    hfree(ctx, ptr);  // (parked while a server of the device is resident)
 }
 int qpp_memcpy_d2d(qpp_ctx *ctx, void *dst, const void *src, size_t bytes, void *stream) {
     HIP_TRY(ctx, hipSetDevice(ctx->device));
@@ -2013,30 +1990,35 @@ uint32_t resident_wgs_locked(const DevServers &r) {
     return w;
 }
 
-// hipHostFree waits for every stream of the device: at once only while no other context's server is resident (the
-// caller stopped its own), else parked -- up to kParkedMax bytes per device, past which the free happens anyway and
-// waits (a bound on what a context that keeps freeing pinned memory beside a busy server can hold); p = nullptr
-// only frees what is parked, if it can.  Under the registry lock, so no server starts between the check and the free.
-void hfree(qpp_ctx *ctx, void *p) {
+// Frees p at once when no server of the device is resident, else parks it (up to kParkedMax bytes per device; past
+// that this context's own servers are stopped and the free waits for the others); p = nullptr only frees what is
+// parked, if it can.  Under the registry lock, so no server starts between the check and the free.
+void release(qpp_ctx *ctx, void *p, bool pinned) {
     DevServers &r = dev_servers(ctx->device);
     std::lock_guard<std::mutex> lk(r.mu);
-    bool others = false;
-    for (const qpp_txq *o : r.queues)
-        if (o->ctx != ctx && srv_resident(o)) others = true;
-    if (others && p) {
+    bool resident = false;
+    for (const qpp_txq *o : r.queues) resident = resident || srv_resident(o);
+    if (resident && p) {
         size_t bytes = 0;
         if (hipMemPtrGetInfo(p, &bytes) != hipSuccess) bytes = 0;
         if (r.parked_bytes + bytes <= kParkedMax) {
-            r.parked.push_back(p);
+            r.parked.emplace_back(p, pinned);
             r.parked_bytes += bytes;
             return;
         }
+        servers_stop(ctx);  // (srv_stop takes no registry lock)
     }
-    if (others && !p) return;
-    for (void *x : r.parked) hipHostFree(x);
+    if (resident && !p) return;
+    for (const auto &x : r.parked) {
+        if (x.second) hipHostFree(x.first);
+        else hipFree(x.first);
+    }
     r.parked.clear();
     r.parked_bytes = 0;
-    if (p) hipHostFree(p);
+    if (p) {
+        if (pinned) hipHostFree(p);
+        else hipFree(p);
+    }
 }
 
 uint32_t srv_next(uint32_t s) { return s + 1u ? s + 1u : 1u; }  // 0 is never a flush's seq
@@ -2212,7 +2194,7 @@ int qpp_txq_create_async(qpp_ctx *ctx, size_t ring_bytes, size_t max_packets, si
 void qpp_txq_destroy(qpp_txq *q) {
     if (!q) return;
     hipSetDevice(q->ctx->device);
-    quiet_for_free(q->ctx);  // this queue's server and every other one of the context (the frees below)
+    quiet_for_free(q->ctx);  // this queue's server (and the context's others: restarted by their next call)
     if (q->persistent) {
         srv_stop(q);
         std::vector<qpp_txq *> &v = q->ctx->servers;
@@ -2233,11 +2215,11 @@ void qpp_txq_destroy(qpp_txq *q) {
     if (q->d_ring) {
         hipMemsetAsync(q->d_ring, 0, q->ring_bytes, q->ctx->stream);
         hipStreamSynchronize(q->ctx->stream);
-        dfree_idle(q->ctx, q->d_ring);
+        dfree(q->ctx, q->d_ring);
     }
     for (TxqSlot &sl : q->slots) {
         hfree(q->ctx, sl.h_desc);
-        dfree_idle(q->ctx, sl.d_desc);  // (the queue's streams are synchronized above)
+        dfree(q->ctx, sl.d_desc);  // (the queue's streams are synchronized above)
         hfree(q->ctx, sl.h_perm);
         if (sl.done) hipEventDestroy(sl.done);
         hfree(q->ctx, sl.h_refused);

@@ -70,8 +70,7 @@ def test_server_matches_launched_path():
 
 
 def test_server_restarts_and_long_packets(monkeypatch):
-    """the server leaves on its idle time, and a pinned free stops it (hipHostFree waits for every stream of the
-    device); the next call restarts it.  A device free does not stop it (stream-ordered free).  A packet over the
+    """the server leaves on its idle time, or is switched off and on; the next call restarts it.  A packet over the
     ring (16 KiB) and a FIPS seal take the launched path, identical bytes."""
     monkeypatch.setenv("QPP_TXQ_SERVER_IDLE_MS", "20")
     rng = np.random.default_rng(7300)
@@ -92,9 +91,9 @@ def test_server_restarts_and_long_packets(monkeypatch):
         time.sleep(0.1)  # past the idle time: the server left
         one(2, 1200)
         assert ctx.packet_server_info()[1] >= s0 + 1
-        h = ctx.host_alloc(4096)
-        ctx.host_free(h)  # a pinned free stops the context's servers
-        one(3, 1200)
+        ctx.set_packet_server(False)  # stopped ...
+        ctx.set_packet_server(True)
+        one(3, 1200)  # ... and started again by the next call
         assert ctx.packet_server_info()[1] >= s0 + 2
         served = ctx.packet_server_info()[0]
         one(4, 20000)  # over the ring: launched
@@ -112,8 +111,9 @@ def test_server_restarts_and_long_packets(monkeypatch):
 
 
 def test_device_free_keeps_the_server(monkeypatch):
-    """qpp_dev_free is stream-ordered (hipFreeAsync behind the context's streams): the packet server stays resident
-    (one launch for every call), while a pinned free stops it and the next call restarts it"""
+    """device and pinned frees leave the packet server resident (one launch for every call): hipFree / hipHostFree
+    would wait for it, so a buffer freed while a server of the device is resident is parked and freed by the next
+    synchronize that finds none (api.cpp release)"""
     monkeypatch.setenv("QPP_TXQ_SERVER_IDLE_MS", "10000")
     rng = np.random.default_rng(7301)
     ctx = qpp.Context(0)
@@ -133,10 +133,13 @@ def test_device_free_keeps_the_server(monkeypatch):
             b.upload(np.full(1 << 20, i, dtype=np.uint8))
             b.free()
             one(2 + i)
+            h = ctx.host_alloc(1 << 16)
+            h[:] = i
+            ctx.host_free(h)
+            one(20 + i)
         assert ctx.packet_server_info()[1] == starts
-        h = ctx.host_alloc(4096)
-        ctx.host_free(h)
-        one(10)
+        ctx.synchronize()  # stops the server, frees what was parked
+        one(40)
         assert ctx.packet_server_info()[1] == starts + 1
     finally:
         ctx.close()

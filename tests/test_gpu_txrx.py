@@ -97,7 +97,7 @@ def test_tx_and_rx_with_resident_server(monkeypatch):
         d_rx, d_rxa = ctx.alloc(rx.nbytes), ctx.alloc(rx_arena.nbytes)
         d_out, d_rst = ctx.alloc(nrx * qpp.PKT_DTYPE.itemsize), ctx.alloc(nrx)
         d_rx.upload(rx)
-        # warm-up: the plan and receive scratch grow to these sizes now (a growth frees memory, which stops servers)
+        # warm-up: the plan and receive scratch grow to these sizes now
         d_arena.upload(arena)
         ctx.seal_batch(d_desc, n, d_arena, d_mask, d_status, qpp.HP_MASK_OUT)
         d_rxa.upload(rx_arena)
@@ -174,8 +174,8 @@ def test_tx_and_rx_with_resident_server(monkeypatch):
 
 def test_frees_with_resident_server_return_quickly(monkeypatch):
     """hipFree waits for every stream of the device, a resident server's too: a free (and a plan growth, which frees
-    the old plan) while a persistent queue is live stops the server first -- the call returns in milliseconds, not
-    after the server's idle time -- and the next flush restarts it, bit-exact"""
+    the old plan) while a persistent queue is live is parked instead (api.cpp release) -- the call returns in
+    milliseconds, not after the server's idle time, and the server stays resident for the next flushes, bit-exact"""
     monkeypatch.setenv("QPP_TXQ_SERVER_IDLE_MS", "30000")
     rng = np.random.default_rng(4041)
     ctx = qpp.Context(0)
@@ -209,7 +209,7 @@ def test_frees_with_resident_server_return_quickly(monkeypatch):
         q.flush()
         _check(q, want)
         served, launched, starts = q.info()
-        assert served == 3 and launched == 0 and starts >= 2
+        assert (served, launched, starts) == (3, 0, 1)  # one server launch: the frees did not stop it
         for b in (d_desc, d_arena, d_status):
             b.free()
         k.free()

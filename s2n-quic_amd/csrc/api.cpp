@@ -219,7 +219,14 @@ struct DevServers {
     std::vector<std::pair<void *, bool>> parked;  // buffers (pinned: true) freed once no server is resident (release)
     size_t parked_bytes = 0;
 };
-constexpr size_t kParkedMax = size_t(2) << 30;  // past this, release frees at once (and waits)
+// past this many parked bytes per device, release frees at once (and waits); env QPP_PARKED_MAX_MB (tests)
+size_t parked_max() {
+    static const size_t v = [] {
+        const char *e = getenv("QPP_PARKED_MAX_MB");
+        return e ? (size_t)strtoull(e, nullptr, 10) << 20 : size_t(2) << 30;
+    }();
+    return v;
+}
 DevServers &dev_servers(int device) {
     static DevServers regs[64];
     return regs[(unsigned)device & 63u];
@@ -1990,25 +1997,30 @@ uint32_t resident_wgs_locked(const DevServers &r) {
     return w;
 }
 
-// Frees p at once when no server of the device is resident, else parks it (up to kParkedMax bytes per device; past
+// Frees p at once when no server of the device is resident, else parks it (up to parked_max() bytes per device; past
 // that this context's own servers are stopped and the free waits for the others); p = nullptr only frees what is
 // parked, if it can.  Under the registry lock, so no server starts between the check and the free.
 void release(qpp_ctx *ctx, void *p, bool pinned) {
     DevServers &r = dev_servers(ctx->device);
-    std::lock_guard<std::mutex> lk(r.mu);
-    bool resident = false;
-    for (const qpp_txq *o : r.queues) resident = resident || srv_resident(o);
-    if (resident && p) {
+    std::unique_lock<std::mutex> lk(r.mu);
+    auto resident = [&r] {
+        for (const qpp_txq *o : r.queues)
+            if (srv_resident(o)) return true;
+        return false;
+    };
+    if (resident()) {
+        if (!p) return;
         size_t bytes = 0;
         if (hipMemPtrGetInfo(p, &bytes) != hipSuccess) bytes = 0;
-        if (r.parked_bytes + bytes <= kParkedMax) {
+        if (r.parked_bytes + bytes <= parked_max()) {
             r.parked.emplace_back(p, pinned);
             r.parked_bytes += bytes;
             return;
         }
-        servers_stop(ctx);  // (srv_stop takes no registry lock)
+        lk.unlock();  // (srv_stop may relaunch a server behind a posted flush: srv_start takes the lock)
+        servers_stop(ctx);
+        lk.lock();
     }
-    if (resident && !p) return;
     for (const auto &x : r.parked) {
         if (x.second) hipHostFree(x.first);
         else hipFree(x.first);

@@ -169,3 +169,43 @@ def test_server_header_protection_masks(suite):
         hk.free()
     finally:
         ctx.close()
+
+
+def test_parked_bound_stops_own_server(monkeypatch):
+    """past the parked-memory bound (QPP_PARKED_MAX_MB, here 1 MiB) a free stops the context's own servers and frees
+    at once (no other context's server is resident): it returns promptly, the bytes stay right, the next call
+    restarts the server"""
+    import subprocess
+    import sys
+    code = r'''
+import time, numpy as np, qpp, _oracle as orc
+rng = np.random.default_rng(7302)
+ctx = qpp.Context(0)
+k = ctx.key(1, rng.integers(0, 256, 32, dtype=np.uint8).tobytes())
+kk, iv, _ = k.material()
+def one(pn):
+    payload = rng.integers(0, 256, 700, dtype=np.uint8).tobytes()
+    assert k.encrypt(pn, bytes(21), payload) == b"".join(orc.seal(1, kk, orc.nonce(iv, pn), bytes(21), payload))
+one(1)
+s0 = ctx.packet_server_info()[1]
+small = ctx.alloc(1 << 16)
+small.free()  # under the bound: parked, the server stays
+one(2)
+assert ctx.packet_server_info()[1] == s0
+big = ctx.alloc(4 << 20)
+t0 = time.perf_counter()
+big.free()  # over the bound: own server stopped, freed now
+dt = time.perf_counter() - t0
+assert dt < 1.0, dt
+one(3)
+assert ctx.packet_server_info()[1] == s0 + 1
+ctx.close()
+print("ok", round(dt * 1e3, 2), "ms")
+'''
+    import os
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, QPP_PARKED_MAX_MB="1", QPP_TXQ_SERVER_IDLE_MS="10000",
+               PYTHONPATH=os.pathsep.join([here, os.path.join(os.path.dirname(here), "s2n-quic_amd")]))
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=100, cwd=here)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "ok" in r.stdout

@@ -70,7 +70,7 @@ class _Pending:
 
 HISTORY = []
 TRACE = bool(__import__("os").environ.get("QPP_FUZZ_TRACE"))
-SEEDS = [0xF022, 0xF023, 0xF024, 0xF025] + [0xF100 + i for i in range(int(__import__("os").environ.get("QPP_FUZZ_EXTRA", "0")))]
+SEEDS = [0xF022, 0xF023, 0xF024, 0xF025] + [0xF100 + i for i in range(int(__import__("os").environ.get("QPP_FUZZ_EXTRA", "8")))]
 
 
 TXQ_REGIONS, TXQ_REGION = 8, 1 << 17

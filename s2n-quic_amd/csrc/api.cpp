@@ -139,6 +139,7 @@ struct qpp_ctx {
     int kstage_next = 0;
     HostPipe *pipe = nullptr;
     std::vector<qpp_txq *> servers;  // transmit queues with a persistent server kernel (qpp_txq_create_persistent)
+    std::vector<qpp_txq *> txqs;     // every transmit queue of the context (their flush streams: ctx_streams)
     // The packet server: a persistent queue of the context's own (kPktWgs workgroups, created on the first per-packet
     // call) through which qpp_seal / qpp_open run without a kernel launch; qpp_ctx_set_packet_server, QPP_PACKET_SERVER
     qpp_txq *pkt_q = nullptr;
@@ -297,6 +298,7 @@ void put_event(qpp_ctx *ctx, hipEvent_t e) {
     if (e) ctx->event_pool.push_back(e);
 }
 
+const std::vector<hipStream_t> &txq_streams(const qpp_txq *q);  // (with qpp_txq below)
 // every stream the context's work runs on (the resident servers' excepted): its own, each batch stream's (with its
 // ChaCha side stream, and the transmit queues' flush streams, which are batch streams), the host pipeline's
 std::vector<hipStream_t> ctx_streams(const qpp_ctx *ctx) {
@@ -310,6 +312,8 @@ std::vector<hipStream_t> ctx_streams(const qpp_ctx *ctx) {
     if (ctx->pipe)
         for (hipStream_t s : {ctx->pipe->h2d, ctx->pipe->comp, ctx->pipe->d2h})
             if (s) v.push_back(s);
+    for (const qpp_txq *q : ctx->txqs)  // (zero-copy flushes run on them without a stream state; read the key table)
+        for (hipStream_t s : txq_streams(q)) v.push_back(s);
     return v;
 }
 int ctx_sync(qpp_ctx *ctx) {
@@ -1984,6 +1988,8 @@ struct qpp_txq {
 
 namespace {
 
+const std::vector<hipStream_t> &txq_streams(const qpp_txq *q) { return q->streams; }
+
 constexpr int kNoServerSlot = 1000;  // (internal) srv_start: every server slot of the device is taken
 
 // launched and its stream still busy: read-only on the queue, safe for another context's thread (registry lock held)
@@ -2011,7 +2017,7 @@ void release(qpp_ctx *ctx, void *p, bool pinned) {
     if (resident()) {
         if (!p) return;
         size_t bytes = 0;
-        if (hipMemPtrGetInfo(p, &bytes) != hipSuccess) bytes = 0;
+        if (hipMemPtrGetInfo(p, &bytes) != hipSuccess || !bytes) bytes = size_t(1) << 20;  // (unknown: counted as 1 MiB)
         if (r.parked_bytes + bytes <= parked_max()) {
             r.parked.emplace_back(p, pinned);
             r.parked_bytes += bytes;
@@ -2193,6 +2199,7 @@ static int txq_create(qpp_ctx *ctx, size_t ring_bytes, size_t max_packets, size_
     if (const char *e = getenv("QPP_TXQ_ZC_MAX")) q->zc_max = (uint32_t)strtoul(e, nullptr, 10);
     q->order.reserve(max_packets);
     memset(q->h_ring, 0, ring_bytes);
+    ctx->txqs.push_back(q);
     *out = q;
     return QPP_OK;
 }
@@ -2206,6 +2213,10 @@ int qpp_txq_create_async(qpp_ctx *ctx, size_t ring_bytes, size_t max_packets, si
 void qpp_txq_destroy(qpp_txq *q) {
     if (!q) return;
     hipSetDevice(q->ctx->device);
+    {
+        std::vector<qpp_txq *> &all = q->ctx->txqs;
+        all.erase(std::remove(all.begin(), all.end(), q), all.end());
+    }
     quiet_for_free(q->ctx);  // this queue's server (and the context's others: restarted by their next call)
     if (q->persistent) {
         srv_stop(q);

@@ -8,10 +8,10 @@ out=$root/ab; tmp=$(mktemp -d)
 mkdir -p $out
 pids=()
 for f in aes_gcm.hip quad.hip burst.hip chacha.hip plan.hip keysched.hip fips.hip api.cpp kdf.cpp; do
-  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -Wno-unused-value --offload-arch=gfx950 -munsafe-fp-atomics "$@" -c $src/$f -o $tmp/${f%.*}.o &
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -Wno-unused-value --offload-arch=${ARCH:-gfx950} -munsafe-fp-atomics "$@" -c $src/$f -o $tmp/${f%.*}.o &
   pids+=($!)
 done
 for p in "${pids[@]}"; do wait $p || { echo "compile failed (pid $p)"; rm -rf $tmp; exit 1; }; done
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $out/$name.so $tmp/*.o -Wl,-rpath,/opt/rocm/lib -Wl,--no-undefined
+/opt/rocm/bin/hipcc --offload-arch=${ARCH:-gfx950} -shared -fPIC -o $out/$name.so $tmp/*.o -Wl,-rpath,/opt/rocm/lib -Wl,--no-undefined
 rm -rf $tmp
 echo "built ab/$name.so"

@@ -10,7 +10,7 @@ for round in $(seq 1 ${ROUNDS:-2}); do
     for m in "packet|--mode packet" "txq|--mode txq --inflight 1" "b4k|--packets 4096 --steps 50"; do
       name=${m%%|*}; args=${m#*|}
       QPP_LIB=$PWD/$lib timeout -k 10 120 python bench.py $args --no-cpu > gpurun_out/$tag/r${round}_${n}_$name.json 2> gpurun_out/$tag/err.txt || { echo "fail $n $name"; tail -5 gpurun_out/$tag/err.txt; exit 1; }
-      python3 -c "import json; d=json.loads(open('gpurun_out/$tag/r${round}_${n}_$name.json').read().strip().splitlines()[-1]); c=d.get('config',{}); print('$round $n $name', d['value'], d['unit'], c.get('seal_ms',''), d.get('decrypt_us',''))"
+      python3 -c "import json; d=json.loads(open('gpurun_out/$tag/r${round}_${n}_$name.json').read().strip().splitlines()[-1]); c=d.get('config',{}); print('$round $n $name', d['value'], d['unit'], c.get('seal_ms',''), d.get('decrypt_us',''), d.get('hp_mask_us',''))"
     done
   done
 done

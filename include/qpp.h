@@ -63,7 +63,10 @@ void qpp_ctx_destroy(qpp_ctx *ctx);
 /* Default stream used by the per-packet functions and by batch calls given stream == NULL. */
 void *qpp_ctx_stream(qpp_ctx *ctx);
 /* Waits for every stream of THIS context (batch streams, key installs and retirements, the host pipeline, transmit
- * queues' flushes) and stops its resident servers; never the whole device: another context's resident server keeps
+ * queues' flushes, every stream made by qpp_stream_create and every non-null stream given to qpp_memcpy_*,
+ * qpp_memset_d, qpp_event_record or qpp_stream_wait_event -- until qpp_stream_destroy releases it; a caller's own
+ * stream handed to the context must therefore be released through qpp_stream_destroy, or outlive the context) and
+ * stops its resident servers; never the whole device: another context's resident server keeps
  * running (hipDeviceSynchronize would wait for its idle exit, or forever while it is fed).  The same holds for every
  * call of the library: no free or wait of one context waits for another context's servers (see qpp_dev_free). */
 int qpp_ctx_synchronize(qpp_ctx *ctx);

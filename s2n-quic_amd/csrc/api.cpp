@@ -128,6 +128,10 @@ struct qpp_ctx {
     uint32_t next_slot = 0;
     // per-stream state (plan scratch, last-batch event); [0] is the context stream
     std::vector<StreamState *> streams;
+    // every other stream the caller handed this context or got from it (qpp_stream_create; a non-null stream of
+    // qpp_memcpy_*, qpp_memset_d, qpp_event_record, qpp_stream_wait_event) until qpp_stream_destroy: qpp_ctx_synchronize
+    // waits for these too (a copy-only stream has no StreamState)
+    std::vector<hipStream_t> user_streams;
     std::vector<hipEvent_t> event_pool;
     // per-packet staging (pinned, zero-copy) and key staging (pinned + device)
     uint8_t *d_stage = nullptr, *h_stage = nullptr;
@@ -314,7 +318,16 @@ std::vector<hipStream_t> ctx_streams(const qpp_ctx *ctx) {
             if (s) v.push_back(s);
     for (const qpp_txq *q : ctx->txqs)  // (zero-copy flushes run on them without a stream state; read the key table)
         for (hipStream_t s : txq_streams(q)) v.push_back(s);
+    for (hipStream_t s : ctx->user_streams) v.push_back(s);
     return v;
+}
+// remember a caller's stream (see qpp_ctx::user_streams); returns it (NULL: the context stream)
+hipStream_t user_stream(qpp_ctx *ctx, void *stream) {
+    hipStream_t s = (hipStream_t)stream;
+    if (!s || s == ctx->stream) return ctx->stream;
+    if (std::find(ctx->user_streams.begin(), ctx->user_streams.end(), s) == ctx->user_streams.end())
+        ctx->user_streams.push_back(s);
+    return s;
 }
 int ctx_sync(qpp_ctx *ctx) {
     for (hipStream_t s : ctx_streams(ctx)) HIP_TRY(ctx, hipStreamSynchronize(s));
@@ -1857,26 +1870,27 @@ void qpp_host_free(qpp_ctx *ctx, void *ptr) {
 }
 int qpp_memcpy_d2d(qpp_ctx *ctx, void *dst, const void *src, size_t bytes, void *stream) {
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    HIP_TRY(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, stream ? (hipStream_t)stream : ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, user_stream(ctx, stream)));
     return QPP_OK;
 }
 
 int qpp_memcpy_h2d(qpp_ctx *ctx, void *dst, const void *src, size_t bytes, void *stream) {
-    HIP_TRY(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, stream ? (hipStream_t)stream : ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, user_stream(ctx, stream)));
     return QPP_OK;
 }
 int qpp_memcpy_d2h(qpp_ctx *ctx, void *dst, const void *src, size_t bytes, void *stream) {
-    HIP_TRY(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, stream ? (hipStream_t)stream : ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, user_stream(ctx, stream)));
     return QPP_OK;
 }
 int qpp_memset_d(qpp_ctx *ctx, void *dst, int value, size_t bytes, void *stream) {
-    HIP_TRY(ctx, hipMemsetAsync(dst, value, bytes, stream ? (hipStream_t)stream : ctx->stream));
+    HIP_TRY(ctx, hipMemsetAsync(dst, value, bytes, user_stream(ctx, stream)));
     return QPP_OK;
 }
 int qpp_stream_create(qpp_ctx *ctx, void **out) {
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     hipStream_t s;
     HIP_TRY(ctx, hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    user_stream(ctx, (void *)s);
     *out = (void *)s;
     return QPP_OK;
 }
@@ -1892,6 +1906,8 @@ void qpp_stream_destroy(qpp_ctx *ctx, void *stream) {
             ctx->streams.erase(ctx->streams.begin() + (long)i);
             break;
         }
+        ctx->user_streams.erase(std::remove(ctx->user_streams.begin(), ctx->user_streams.end(), s),
+                                ctx->user_streams.end());
     }
     hipStreamDestroy(s);
 }
@@ -1910,7 +1926,7 @@ void qpp_event_destroy(qpp_ctx *, void *event) {
     if (event) hipEventDestroy((hipEvent_t)event);
 }
 int qpp_event_record(qpp_ctx *ctx, void *event, void *stream) {
-    HIP_TRY(ctx, hipEventRecord((hipEvent_t)event, stream ? (hipStream_t)stream : ctx->stream));
+    HIP_TRY(ctx, hipEventRecord((hipEvent_t)event, user_stream(ctx, stream)));
     return QPP_OK;
 }
 int qpp_event_elapsed_ms(qpp_ctx *ctx, void *start, void *stop, float *ms) {
@@ -1920,7 +1936,7 @@ int qpp_event_elapsed_ms(qpp_ctx *ctx, void *start, void *stop, float *ms) {
 }
 
 int qpp_stream_wait_event(qpp_ctx *ctx, void *stream, void *event) {
-    HIP_TRY(ctx, hipStreamWaitEvent(stream ? (hipStream_t)stream : ctx->stream, (hipEvent_t)event, 0));
+    HIP_TRY(ctx, hipStreamWaitEvent(user_stream(ctx, stream), (hipEvent_t)event, 0));
     return QPP_OK;
 }
 

@@ -394,3 +394,28 @@ def test_single_live_key_batches_run_without_a_plan(suite):
         k.free()
     finally:
         c.close()
+
+
+def test_ctx_synchronize_covers_copy_only_streams(ctx):
+    """qpp_ctx_synchronize waits for a stream that carried only copies / memsets / event records: a d2h on a
+    qpp_stream_create stream, then qpp_ctx_synchronize, then the host bytes -- no per-stream sync in between (raw C-ABI
+    calls, not the Python wrapper's upload/download, which synchronize their own stream)."""
+    import ctypes
+    L = qpp.lib()
+    nbytes = 256 << 20  # large enough that the copies are still running when the calls return
+    d = ctx.alloc(nbytes)
+    h = ctx.host_alloc(nbytes)
+    h[:] = 0
+    st = ctx.new_stream()
+    ev = ctx.event()
+    for rnd, val in enumerate((0x5a, 0xc3)):
+        assert L.qpp_memset_d(ctx.handle, d.ptr, val, nbytes, st) == 0
+        assert L.qpp_memcpy_d2h(ctx.handle, h.ctypes.data, d.ptr, nbytes, st) == 0
+        assert L.qpp_event_record(ctx.handle, ev, st) == 0
+        assert L.qpp_ctx_synchronize(ctx.handle) == 0
+        assert (h[::4093] == val).all() and h[-1] == val, rnd
+    ctx.stream_destroy(st)
+    # a destroyed stream leaves the context's set: synchronize still works
+    assert L.qpp_ctx_synchronize(ctx.handle) == 0
+    ctx.host_free(h)
+    d.free()

@@ -341,6 +341,11 @@ int qpp_txq_server_time(const qpp_txq *q, double *us);
 /* Persistent queue: descriptors its server refused because their bytes were not inside the ring (never read or
  * written; qpp_txq_push validates every packet, so this stays 0 -- a device-side check of every ring offset). */
 int qpp_txq_server_refused(const qpp_txq *q, uint64_t *count);
+/* Device `device`: times a free past the parked-memory bound evicted the device's resident servers (every context's:
+ * each leaves at its next poll without a complete flush, and its queue relaunches it at its next post), and one-shot
+ * server launches that finished a posted flush whose server had left while every server slot of the device was taken
+ * (on the owning context's normal-priority stream).  See qpp_dev_free. */
+int qpp_dev_server_evictions(int device, uint64_t *evictions, uint64_t *oneshots);
 /* Diagnostics: the server's clock (100 MHz) at the last flush's doorbell, workgroup 0's phase stamps and shader-clock
  * cycles over its work (a build with QPP_TXS_TRACE, else 0) and its completion word:
  * {seen, broadcast, item read, packets done, arrival, done, shader cycles broadcast -> arrival}, then the low words
@@ -429,10 +434,12 @@ uint64_t qpp_pn_expand(uint64_t largest_acked, uint64_t truncated, size_t pn_len
 /* hipFree / hipHostFree wait for every stream of the device, a resident server's too (which leaves only on its idle
  * time, or never while it is fed).  So qpp_dev_free / qpp_host_free -- and every free inside the library -- free at
  * once only while no server of the device (of any context, this one's included) is resident; otherwise the buffer is
- * parked (up to 2 GiB per device; past that this context's servers are stopped and the free waits for the others')
- * and freed by the next free, qpp_ctx_synchronize or qpp_ctx_destroy of any context that finds none resident.  A free
- * never stops a server and never waits for one; work already enqueued that reads the buffer is unaffected.  No view
- * of a freed buffer may be used afterwards. */
+ * parked (up to 2 GiB per device, env QPP_PARKED_MAX_MB) and freed by the next free, qpp_ctx_synchronize or
+ * qpp_ctx_destroy of any context that finds none resident.  Past the bound the free EVICTS the device's resident
+ * servers (every context's: each leaves at its next poll that finds no complete flush, after the flush in hand) and
+ * then frees: it waits microseconds for them, never for a server's idle exit; an evicted queue relaunches its server
+ * at its next post (qpp_dev_server_evictions counts both).  Below the bound a free never stops a server.  Work already
+ * enqueued that reads the buffer is unaffected.  No view of a freed buffer may be used afterwards. */
 int qpp_dev_alloc(qpp_ctx *ctx, size_t bytes, void **out);
 void qpp_dev_free(qpp_ctx *ctx, void *ptr);
 int qpp_host_alloc(qpp_ctx *ctx, size_t bytes, void **out); /* pinned host memory */

@@ -24,6 +24,7 @@
 #include <deque>
 #include <map>
 #include <mutex>
+#include <unordered_map>
 #include <string>
 #include <vector>
 
@@ -223,8 +224,12 @@ struct DevServers {
     hipEvent_t rx_tail = nullptr;   // recorded behind the device's latest fused receive
     std::vector<std::pair<void *, bool>> parked;  // buffers (pinned: true) freed once no server is resident (release)
     size_t parked_bytes = 0;
+    // the device's eviction word (16 B, coherent pinned memory; host view / device view): non-zero makes every resident
+    // server of the device leave at its next poll without a complete flush (release past the parked bound)
+    uint32_t *h_evict = nullptr, *v_evict = nullptr;
+    uint64_t evictions = 0, oneshots = 0;  // qpp_dev_server_evictions
 };
-// past this many parked bytes per device, release frees at once (and waits); env QPP_PARKED_MAX_MB (tests)
+// past this many parked bytes per device, release evicts the device's resident servers and frees; env QPP_PARKED_MAX_MB
 size_t parked_max() {
     static const size_t v = [] {
         const char *e = getenv("QPP_PARKED_MAX_MB");
@@ -276,9 +281,33 @@ void hfree(qpp_ctx *ctx, void *p) { release(ctx, p, true); }
 void dfree(qpp_ctx *ctx, void *p) {
     if (p) release(ctx, p, false);
 }
+// Sizes of the library's device and pinned allocations, so that release() counts parked bytes exactly (hipMemPtrGetInfo
+// does not size every pinned buffer: ADVICE r5).  Process-wide: a buffer may be released by another context's call.
+std::mutex g_size_mu;
+std::unordered_map<void *, size_t> g_sizes;
+void note_size(void *p, size_t bytes) {
+    std::lock_guard<std::mutex> lk(g_size_mu);
+    g_sizes[p] = bytes;
+}
+size_t take_size(void *p) {
+    std::lock_guard<std::mutex> lk(g_size_mu);
+    auto it = g_sizes.find(p);
+    if (it == g_sizes.end()) return 0;
+    const size_t b = it->second;
+    g_sizes.erase(it);
+    return b;
+}
 template <class T>
 hipError_t dmalloc(qpp_ctx *, T **p, size_t bytes) {
-    return hipMalloc((void **)p, bytes ? bytes : 1);
+    const hipError_t e = hipMalloc((void **)p, bytes ? bytes : 1);
+    if (e == hipSuccess) note_size((void *)*p, bytes ? bytes : 1);
+    return e;
+}
+template <class T>
+hipError_t hmalloc(T **p, size_t bytes, unsigned flags) {
+    const hipError_t e = hipHostMalloc((void **)p, bytes ? bytes : 1, flags);
+    if (e == hipSuccess) note_size((void *)*p, bytes ? bytes : 1);
+    return e;
 }
 
 bool valid_suite(int s) {
@@ -452,7 +481,7 @@ int take_kstage(qpp_ctx *ctx, size_t bytes, KStage **out) {
         k.h = nullptr;
         k.cap = 0;
         HIP_TRY(ctx, dmalloc(ctx, &k.d, cap));
-        HIP_TRY(ctx, hipHostMalloc(&k.h, cap, hipHostMallocDefault));
+        HIP_TRY(ctx, hmalloc(&k.h, cap, hipHostMallocDefault));
         k.cap = cap;
     }
     *out = &k;
@@ -567,7 +596,7 @@ int ensure_stage(qpp_ctx *ctx, size_t bytes) {
     ctx->d_stage = ctx->h_stage = ctx->v_stage = nullptr;
     ctx->stage_cap = 0;
     HIP_TRY(ctx, dmalloc(ctx, &ctx->d_stage, cap));
-    HIP_TRY(ctx, hipHostMalloc(&ctx->h_stage, cap, hipHostMallocDefault));
+    HIP_TRY(ctx, hmalloc(&ctx->h_stage, cap, hipHostMallocDefault));
     void *v = nullptr;
     HIP_TRY(ctx, hipHostGetDevicePointer(&v, ctx->h_stage, 0));
     ctx->v_stage = (uint8_t *)v;
@@ -1809,7 +1838,7 @@ int qpp_ctx_set_conn_keys(qpp_ctx *ctx, const uint32_t *slots, size_t n) {
         ctx->h_connstage = nullptr;
         ctx->connstage_cap = 0;
         const size_t cap = std::max<size_t>(n, 1024);
-        HIP_TRY(ctx, hipHostMalloc(&ctx->h_connstage, 4 * cap, hipHostMallocDefault));
+        HIP_TRY(ctx, hmalloc(&ctx->h_connstage, 4 * cap, hipHostMallocDefault));
         ctx->connstage_cap = cap;
     }
     memcpy(ctx->h_connstage, slots, 4 * n);
@@ -1857,7 +1886,7 @@ void qpp_dev_free(qpp_ctx *ctx, void *ptr) {
 }
 int qpp_host_alloc(qpp_ctx *ctx, size_t bytes, void **out) {
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    HIP_TRY(ctx, hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault));
+    HIP_TRY(ctx, hmalloc(out, bytes ? bytes : 1, hipHostMallocDefault));
     return QPP_OK;
 }
 void qpp_host_free(qpp_ctx *ctx, void *ptr) {
@@ -1990,6 +2019,7 @@ struct qpp_txq {
     hipStream_t srv_stream = nullptr;
     bool srv_running = false;           // launched and not yet seen to have ended
     std::atomic<bool> srv_launched{false};  // the same, readable by other contexts' threads (device registry)
+    std::atomic<bool> evicted{false};       // release() made the server leave (another thread): srv_running is stale
     const DevKey *srv_keys = nullptr;   // the key table the running server reads
     uint32_t srv_seq = 0;               // seq of the last flush or stop written into the slots
     uint32_t srv_posted = 0;            // seq of the last flush posted (0: none)
@@ -2000,6 +2030,8 @@ struct qpp_txq {
     std::chrono::steady_clock::time_point srv_last_post{};  // the server may leave idle_ticks after it
     std::chrono::microseconds srv_host_idle{0};             // a quarter of that: past it, restart before posting
     uint64_t n_server = 0, n_launch = 0, n_starts = 0;  // flushes posted / launched; server launches
+    uint64_t n_oneshots = 0;            // of which one-shot launches finishing a posted flush (srv_oneshot)
+    hipEvent_t oneshot_ev = nullptr;    // behind the latest one
 };
 
 namespace {
@@ -2019,9 +2051,13 @@ uint32_t resident_wgs_locked(const DevServers &r) {
     return w;
 }
 
-// Frees p at once when no server of the device is resident, else parks it (up to parked_max() bytes per device; past
-// that this context's own servers are stopped and the free waits for the others); p = nullptr only frees what is
-// parked, if it can.  Under the registry lock, so no server starts between the check and the free.
+// Frees p at once when no server of the device is resident, else parks it, up to parked_max() bytes per device.  Past
+// that bound the device's resident servers -- every context's -- are EVICTED: the eviction word makes each leave at its
+// next poll that finds no complete flush (a flush it has seen is finished first), their streams are waited for (a
+// poll, or the flush in hand: microseconds), and only then does hipFree run -- it never waits for a server that keeps
+// being fed.  An evicted queue's owner relaunches its server at its next post (srv_prepare),
+// and a flush posted while its server left is picked up by the relaunched one (srv_wait).  p = nullptr only frees what
+// is parked, if it can.  Under the registry lock throughout, so no server starts between the wait and the free.
 void release(qpp_ctx *ctx, void *p, bool pinned) {
     DevServers &r = dev_servers(ctx->device);
     std::unique_lock<std::mutex> lk(r.mu);
@@ -2030,18 +2066,25 @@ void release(qpp_ctx *ctx, void *p, bool pinned) {
             if (srv_resident(o)) return true;
         return false;
     };
+    size_t bytes = p ? take_size(p) : 0;
+    if (p && !bytes) bytes = size_t(1) << 20;  // (not allocated through this library: counted as 1 MiB)
     if (resident()) {
         if (!p) return;
-        size_t bytes = 0;
-        if (hipMemPtrGetInfo(p, &bytes) != hipSuccess || !bytes) bytes = size_t(1) << 20;  // (unknown: counted as 1 MiB)
         if (r.parked_bytes + bytes <= parked_max()) {
             r.parked.emplace_back(p, pinned);
             r.parked_bytes += bytes;
             return;
         }
-        lk.unlock();  // (srv_stop may relaunch a server behind a posted flush: srv_start takes the lock)
-        servers_stop(ctx);
-        lk.lock();
+        if (r.h_evict) {
+            __atomic_store_n(r.h_evict, 1u, __ATOMIC_RELEASE);
+            for (qpp_txq *o : r.queues) {
+                if (!o->srv_launched.load(std::memory_order_acquire)) continue;
+                hipStreamSynchronize(o->srv_stream);  // (its server leaves at its next poll)
+                o->evicted.store(true, std::memory_order_release);
+            }
+            __atomic_store_n(r.h_evict, 0u, __ATOMIC_RELEASE);
+            r.evictions++;
+        }
     }
     for (const auto &x : r.parked) {
         if (x.second) hipHostFree(x.first);
@@ -2078,6 +2121,7 @@ bool srv_done(const qpp_txq *q, uint32_t seq) {
 int srv_start(qpp_txq *q, bool force = false) {
     // (no stream query while the server is believed running: a server that left on its idle timeout is found by
     // srv_wait's slow path, which relaunches it behind the posted flush)
+    if (q->srv_running && q->evicted.exchange(false, std::memory_order_acq_rel)) srv_alive(q);  // (it left)
     if (q->srv_running) return QPP_OK;
     qpp_ctx *ctx = q->ctx;
     DevServers &r = dev_servers(ctx->device);
@@ -2094,12 +2138,34 @@ int srv_start(qpp_txq *q, bool force = false) {
     const uint32_t seq0 = pending ? q->srv_posted - 1u : q->srv_seq;
     HIP_TRY(ctx, launch_txq_server(ctx->d_keys, ctx->pow, q->v_mail, q->v_slots, q->v_items, q->v_sdesc, q->v_ring,
                                    (uint32_t)std::min<size_t>(q->ring_bytes, UINT32_MAX), seq0, q->srv_idle_ticks,
-                                   q->srv_wgs, q->srv_stream));
+                                   q->srv_wgs, r.v_evict, q->srv_stream));
     q->srv_running = true;
     q->srv_launched.store(true, std::memory_order_release);
     q->srv_keys = ctx->d_keys;
     q->srv_last_post = std::chrono::steady_clock::now();  // (its idle clock starts now)
     q->n_starts++;
+    return QPP_OK;
+}
+
+// A posted flush whose server left before every workgroup saw it (idle exit, or evicted by release) while every
+// server slot of the device is taken: a relaunched server could land on a hardware queue a fed server holds and wait
+// for that server's exit.  So the flush is finished by a ONE-SHOT launch of the server kernel (idle 0: it
+// serves the posted flush in the workgroups whose `done` does not show it yet, then leaves) on the context's own
+// normal-priority stream.  At most one in flight per queue.
+int srv_oneshot(qpp_txq *q) {
+    qpp_ctx *ctx = q->ctx;
+    if (q->oneshot_ev && hipEventQuery(q->oneshot_ev) == hipErrorNotReady) return QPP_OK;
+    if (!q->oneshot_ev) HIP_TRY(ctx, hipEventCreateWithFlags(&q->oneshot_ev, hipEventDisableTiming));
+    DevServers &r = dev_servers(ctx->device);
+    std::lock_guard<std::mutex> lk(r.mu);
+    if (r.rx_tail) HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, r.rx_tail, 0));
+    HIP_TRY(ctx, launch_txq_server(ctx->d_keys, ctx->pow, q->v_mail, q->v_slots, q->v_items, q->v_sdesc, q->v_ring,
+                                   (uint32_t)std::min<size_t>(q->ring_bytes, UINT32_MAX), q->srv_posted - 1u, 0u,
+                                   q->srv_wgs, r.v_evict, ctx->stream));
+    HIP_TRY(ctx, hipEventRecord(q->oneshot_ev, ctx->stream));
+    q->n_starts++;
+    q->n_oneshots++;
+    r.oneshots++;
     return QPP_OK;
 }
 
@@ -2110,7 +2176,14 @@ int srv_wait(qpp_txq *q, uint32_t seq) {
     for (uint64_t spin = 0;; spin++) {
         if (srv_done(q, seq)) return QPP_OK;
         if ((spin & 4095u) == 4095u) {
-            if (!srv_alive(q)) RC_TRY(srv_start(q, true));  // it left (idle) before this flush was seen: a new one takes it
+            // it left (idle, evicted) before this flush was seen: a new one takes it -- unless a one-shot launch is
+            // still on it (two kernels must never serve one flush: the ring is sealed in place)
+            const bool oneshot = q->oneshot_ev && hipEventQuery(q->oneshot_ev) == hipErrorNotReady;
+            if (!oneshot && !srv_alive(q)) {
+                int rc = srv_start(q);
+                if (rc == kNoServerSlot) rc = srv_oneshot(q);
+                RC_TRY(rc);
+            }
             const auto now = std::chrono::steady_clock::now();
             if (spin == 4095u) t0 = now;
             else if (now - t0 > std::chrono::seconds(10)) {
@@ -2179,7 +2252,7 @@ static int txq_create(qpp_ctx *ctx, size_t ring_bytes, size_t max_packets, size_
         qpp_txq_destroy(q);
         return true;
     };
-    if (bad(hipHostMalloc(&q->h_ring, ring_bytes, ring_flags), "txq ring") ||
+    if (bad(hmalloc(&q->h_ring, ring_bytes, ring_flags), "txq ring") ||
         bad(dmalloc(ctx, &q->d_ring, ring_bytes), "txq ring") || bad(hipHostGetDevicePointer(&v, q->h_ring, 0), "ring view"))
         return QPP_DEVICE_ERROR;
     q->v_ring = (uint8_t *)v;
@@ -2194,12 +2267,12 @@ static int txq_create(qpp_ctx *ctx, size_t ring_bytes, size_t max_packets, size_
     for (size_t i = 0; i < in_flight; i++) {
         TxqSlot &sl = q->slots[i];
         sl.stream = q->streams[i % nstreams];
-        if (bad(hipHostMalloc(&sl.h_desc, sizeof(qpp_pkt) * max_packets, hipHostMallocDefault), "txq descs") ||
+        if (bad(hmalloc(&sl.h_desc, sizeof(qpp_pkt) * max_packets, hipHostMallocDefault), "txq descs") ||
             bad(dmalloc(ctx, &sl.d_desc, sizeof(qpp_pkt) * max_packets), "txq descs") ||
-            bad(hipHostMalloc(&sl.h_perm, 4 * (max_packets + 4) + sizeof(WorkItem) * (max_packets + 1),
+            bad(hmalloc(&sl.h_perm, 4 * (max_packets + 4) + sizeof(WorkItem) * (max_packets + 1),
                               hipHostMallocDefault), "txq plan") ||
             bad(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming), "txq event") ||
-            bad(hipHostMalloc(&sl.h_refused, 64, hipHostMallocDefault), "txq refused count"))
+            bad(hmalloc(&sl.h_refused, 64, hipHostMallocDefault), "txq refused count"))
             return QPP_DEVICE_ERROR;
         *sl.h_refused = 0;
         sl.h_nwork = sl.h_perm + max_packets;
@@ -2244,6 +2317,7 @@ void qpp_txq_destroy(qpp_txq *q) {
             r.queues.erase(std::remove(r.queues.begin(), r.queues.end(), q), r.queues.end());
         }
         if (q->srv_stream) { hipStreamSynchronize(q->srv_stream); hipStreamDestroy(q->srv_stream); }
+        if (q->oneshot_ev) { hipEventSynchronize(q->oneshot_ev); hipEventDestroy(q->oneshot_ev); }
         hfree(q->ctx, q->h_mail);
         if (q->h_slots) { secure_zero(q->h_slots, sizeof(TxsSlot) * q->srv_wgs); hfree(q->ctx, q->h_slots); }
         hfree(q->ctx, q->h_items);
@@ -2408,6 +2482,8 @@ static int srv_prepare(qpp_txq *q, std::chrono::steady_clock::time_point now) {
         q->srv_key_gen = ctx->key_gen;
         q->srv_epoch = (q->srv_epoch + 1u) & 0xffu;
     }
+    // a one-shot launch that served the last flush has left before anything is posted again (it would serve it too)
+    if (q->oneshot_ev) HIP_TRY(ctx, hipEventSynchronize(q->oneshot_ev));
     if (q->srv_running && q->srv_keys != ctx->d_keys) RC_TRY(srv_stop(q));  // (grow_keys stops servers already)
     // a server idle for long may be leaving on its own timeout: never post to it (part of it could miss the flush)
     if (q->srv_running && now - q->srv_last_post > q->srv_host_idle) RC_TRY(srv_stop(q));
@@ -2641,23 +2717,35 @@ static int txq_create_server(qpp_ctx *ctx, size_t ring_bytes, size_t max_packets
     };
     q->persistent = true;
     ctx->servers.push_back(q);
+    hipError_t ev_err = hipSuccess;
     {
         DevServers &r = dev_servers(ctx->device);
         std::lock_guard<std::mutex> lk(r.mu);
+        if (!r.h_evict) {  // (process lifetime: one 16-B word per device, never freed)
+            void *h = nullptr, *dv = nullptr;
+            ev_err = hipHostMalloc(&h, 16, fl);
+            if (ev_err == hipSuccess) ev_err = hipHostGetDevicePointer(&dv, h, 0);
+            if (ev_err == hipSuccess) {
+                memset(h, 0, 16);
+                r.h_evict = (uint32_t *)h;
+                r.v_evict = (uint32_t *)dv;
+            }
+        }
         r.queues.push_back(q);
     }
+    if (bad(ev_err, "eviction word")) return QPP_DEVICE_ERROR;
     const size_t W = kTxsWaves;
     void *v = nullptr;
-    if (bad(hipHostMalloc(&q->h_mail, sizeof(TxsMail), fl), "txq server mailbox") ||
+    if (bad(hmalloc(&q->h_mail, sizeof(TxsMail), fl), "txq server mailbox") ||
         bad(hipHostGetDevicePointer(&v, q->h_mail, 0), "mailbox view"))
         return QPP_DEVICE_ERROR;
     q->v_mail = (TxsMail *)v;
     memset(q->h_mail, 0, sizeof(TxsMail));
-    if (bad(hipHostMalloc(&q->h_items, sizeof(WorkItem) * max_packets, fl), "txq server items") ||
+    if (bad(hmalloc(&q->h_items, sizeof(WorkItem) * max_packets, fl), "txq server items") ||
         bad(hipHostGetDevicePointer(&v, q->h_items, 0), "items view"))
         return QPP_DEVICE_ERROR;
     q->v_items = (WorkItem *)v;
-    if (bad(hipHostMalloc(&q->h_sdesc, sizeof(qpp_pkt) * max_packets * W, fl), "txq server descs") ||
+    if (bad(hmalloc(&q->h_sdesc, sizeof(qpp_pkt) * max_packets * W, fl), "txq server descs") ||
         bad(hipHostGetDevicePointer(&v, q->h_sdesc, 0), "descs view"))
         return QPP_DEVICE_ERROR;
     q->v_sdesc = (qpp_pkt *)v;
@@ -2672,7 +2760,7 @@ static int txq_create_server(qpp_ctx *ctx, size_t ring_bytes, size_t max_packets
         bad(hipStreamCreateWithPriority(&q->srv_stream, hipStreamNonBlocking, prio_greatest), "txq server stream"))
         return QPP_DEVICE_ERROR;
     q->srv_wgs = std::max(1u, std::min(wgs, ctx->n_cu));
-    if (bad(hipHostMalloc(&q->h_slots, sizeof(TxsSlot) * q->srv_wgs, fl), "txq server slots") ||
+    if (bad(hmalloc(&q->h_slots, sizeof(TxsSlot) * q->srv_wgs, fl), "txq server slots") ||
         bad(hipHostGetDevicePointer(&v, q->h_slots, 0), "slots view"))
         return QPP_DEVICE_ERROR;
     q->v_slots = (TxsSlot *)v;
@@ -2722,6 +2810,15 @@ int qpp_txq_info(const qpp_txq *q, uint64_t *server_flushes, uint64_t *launched_
     if (server_flushes) *server_flushes = q->n_server;
     if (launched_flushes) *launched_flushes = q->n_launch;
     if (server_starts) *server_starts = q->n_starts;
+    return QPP_OK;
+}
+
+int qpp_dev_server_evictions(int device, uint64_t *evictions, uint64_t *oneshots) {
+    if (device < 0 || device >= 64) return QPP_INTERNAL_ERROR;
+    DevServers &r = dev_servers(device);
+    std::lock_guard<std::mutex> lk(r.mu);
+    if (evictions) *evictions = r.evictions;
+    if (oneshots) *oneshots = r.oneshots;
     return QPP_OK;
 }
 

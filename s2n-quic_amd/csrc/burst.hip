@@ -596,11 +596,14 @@ __device__ __forceinline__ void txs_two_wave(const AesLds &aes, const qpp_pkt &d
 
 // one 16-byte chunk of the slot (lane < kTxsPollLanes), in ONE load past every cache (sc0 sc1: the host writes it;
 // a chunk is read whole, so its tag vouches for its other words)
-__device__ __forceinline__ uint4 txs_poll(const TxsSlot *slot, uint32_t lane) {
+// lane kTxsPollLanes reads the device's eviction word in the same load (api.cpp release: every resident server of the
+// device leaves at its next poll without a complete flush, so that a free past the parked bound need not wait for it)
+__device__ __forceinline__ uint4 txs_poll(const TxsSlot *slot, const uint32_t *evict, uint32_t lane) {
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     uint4 v = make_uint4(0, 0, 0, 0);
-    if (lane < kTxsPollLanes) {
-        const u32x4 c = *((const volatile u32x4 *)slot + lane);
+    const u32x4 *src = lane < kTxsPollLanes ? (const u32x4 *)slot + lane : (const u32x4 *)evict;
+    if (lane <= kTxsPollLanes) {
+        const u32x4 c = *(const volatile u32x4 *)src;
         v = make_uint4(c.x, c.y, c.z, c.w);
     }
     return v;
@@ -609,7 +612,8 @@ __device__ __forceinline__ uint4 txs_poll(const TxsSlot *slot, uint32_t lane) {
 __global__ __launch_bounds__(kBurstWG) void txq_server_kernel(const DevKey *keys, const PowTables pow, TxsMail *mail,
                                                               TxsSlot *slots, const WorkItem *items,
                                                               const qpp_pkt *sdesc, uint8_t *ring, uint32_t ring_bytes,
-                                                              uint32_t seq0, uint32_t idle_ticks) {
+                                                              uint32_t seq0, uint32_t idle_ticks,
+                                                              const uint32_t *evict) {
     build_aes_tables(kBurstAes);
     __syncthreads();
     const AesLds aes = make_aes(kBurstAes);
@@ -630,10 +634,10 @@ __global__ __launch_bounds__(kBurstWG) void txq_server_kernel(const DevKey *keys
         if (wave == 0) {
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
             uint32_t stop = 0;
-            uint4 cur = txs_poll(slot, lane);
+            uint4 cur = txs_poll(slot, evict, lane);
             for (;;) {
                 __builtin_amdgcn_s_sleep(4);
-                const uint4 nxt = txs_poll(slot, lane);  // in flight while `cur` is examined
+                const uint4 nxt = txs_poll(slot, evict, lane);  // in flight while `cur` is examined
                 const uint32_t seq = __shfl((int)cur.x, 0, 64), word = __shfl((int)cur.y, 0, 64);
                 if (seq != seen) {
                     if ((word & kTxsItemsMask) == kTxsStop) {
@@ -648,7 +652,8 @@ __global__ __launch_bounds__(kBurstWG) void txq_server_kernel(const DevKey *keys
                     if (lane >= 2 && lane < kTxsPollLanes && (lane - 2) / 2 < item_cnt) ok = cur.w == seq;
                     if (__all(ok)) break;
                 }
-                if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) {
+                // idle timeout, or evicted (between flushes only: a complete flush above is served first)
+                if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks || __shfl((int)cur.x, kTxsPollLanes, 64)) {
                     stop = 1;
                     break;
                 }
@@ -840,9 +845,9 @@ hipError_t launch_aes_gcm_burst(bool seal, const DevKey *keys, const qpp_pkt *de
 
 hipError_t launch_txq_server(const DevKey *keys, const PowTables &pow, TxsMail *mail, TxsSlot *slots,
                              const WorkItem *items, const qpp_pkt *sdesc, uint8_t *ring, uint32_t ring_bytes,
-                             uint32_t seq0, uint32_t idle_ticks, uint32_t wgs, hipStream_t s) {
+                             uint32_t seq0, uint32_t idle_ticks, uint32_t wgs, const uint32_t *evict, hipStream_t s) {
     hipLaunchKernelGGL(txq_server_kernel, dim3(wgs), dim3(kBurstWG), kTxsLds, s, keys, pow, mail, slots, items,
-                       sdesc, ring, ring_bytes, seq0, idle_ticks);
+                       sdesc, ring, ring_bytes, seq0, idle_ticks, evict);
     return hipGetLastError();
 }
 

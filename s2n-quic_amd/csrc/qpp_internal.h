@@ -193,10 +193,11 @@ struct alignas(64) TxsMail {  // telemetry (s_memrealtime, 100 MHz)
     uint32_t pad2[15];
 };
 // ring_bytes: the ring's size -- a descriptor whose bytes [off, off + aad + payload + 16) do not lie inside is refused
-// (never read or written) and counted in mail->oob
+// (never read or written) and counted in mail->oob.  evict: the device's eviction word (16 B, coherent pinned memory):
+// non-zero makes every workgroup leave at its next poll that finds no complete flush.
 hipError_t launch_txq_server(const DevKey *keys, const PowTables &pow, TxsMail *mail, TxsSlot *slots,
                              const WorkItem *items, const qpp_pkt *sdesc, uint8_t *ring, uint32_t ring_bytes,
-                             uint32_t seq0, uint32_t idle_ticks, uint32_t wgs, hipStream_t s);
+                             uint32_t seq0, uint32_t idle_ticks, uint32_t wgs, const uint32_t *evict, hipStream_t s);
 // the burst power tables of keys[slots[i]] (AES packet keys with slot < pow.cap), after their V[m] are in place
 hipError_t launch_pow_setup(const DevKey *keys, const uint32_t *slots, uint32_t count, const PowTables &pow,
                             hipStream_t s);

@@ -63,7 +63,7 @@ EXPORTS = [
     "qpp_header_key_new", "qpp_header_key_new_raw", "qpp_header_key_free", "qpp_header_key_slot",
     "qpp_header_key_suite", "qpp_header_key_sample_len", "qpp_header_key_mask", "qpp_host_batch_submit",
     "qpp_host_batch_query", "qpp_host_batch_wait", "qpp_ctx_set_host_pipe", "qpp_ctx_set_fips", "qpp_key_fips",
-    "qpp_ctx_set_packet_server", "qpp_ctx_packet_server_info",
+    "qpp_ctx_set_packet_server", "qpp_ctx_packet_server_info", "qpp_dev_server_evictions",
 ]
 OP_SEAL, OP_OPEN = 0x1, 0x2
 
@@ -84,7 +84,7 @@ _lib = None
 vp, u8p, sz, u32, u64 = ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint8), ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint64
 
 
-_LATER = {"qpp_txq_server_refused"}  # entry points added in round 5
+_LATER = {"qpp_txq_server_refused", "qpp_dev_server_evictions"}  # entry points added in rounds 5, 6
 
 
 def lib():
@@ -159,6 +159,7 @@ def lib():
             "qpp_txq_info": (ctypes.c_int, [vp, ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u64)]),
             "qpp_txq_server_time": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double)]),
             "qpp_txq_server_refused": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_uint64)]),
+            "qpp_dev_server_evictions": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(u64), ctypes.POINTER(u64)]),
             "qpp_ctx_set_conn_keys": (ctypes.c_int, [vp, vp, sz]),
             "qpp_txq_server_stamps": (ctypes.c_int, [vp, vp]),
             "qpp_txq_set_coalesce": (ctypes.c_int, [vp, sz]),
@@ -706,6 +707,16 @@ def make_batch(n, pt_len, key_slots, seed, aad_len=21, pn_len=4, pn_base=0, stri
     if aad_len >= 1:
         arena.reshape(n, stride)[:, 0] = 0x43
     return descs, arena
+
+
+def server_evictions(device=0):
+    """qpp_dev_server_evictions: (frees past the parked bound that evicted the device's resident servers, one-shot server
+    launches that finished a posted flush while every server slot was taken)"""
+    a, b = u64(), u64()
+    rc = lib().qpp_dev_server_evictions(device, ctypes.byref(a), ctypes.byref(b))
+    if rc != OK:
+        raise QppError(rc, "qpp_dev_server_evictions")
+    return a.value, b.value
 
 
 def pn_truncate(pn, largest_acked):

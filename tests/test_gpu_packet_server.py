@@ -209,3 +209,86 @@ print("ok", round(dt * 1e3, 2), "ms")
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=100, cwd=here)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "ok" in r.stdout
+
+
+def test_free_past_bound_evicts_other_contexts_fed_server():
+    """past the parked-memory bound (QPP_PARKED_MAX_MB=1) a free of context A must not wait for context
+    B's resident server while a thread keeps feeding it (hipFree waits for every stream of the device: it would wait
+    for B's idle exit, i.e. for ever).  Every A free (device and pinned, 4 MiB each: over the bound every time) returns
+    in < 1 s; every B flush (64 x 100-1200 B, AES-128, persistent server) is bit-exact; the evictions are counted and
+    B's server is relaunched after them.  Runs in a child process (the bound is read once per process)."""
+    import os
+    import subprocess
+    import sys
+    code = r'''
+import threading, time, numpy as np, qpp, _oracle as orc
+STRIDE = 1536
+rng = np.random.default_rng(7303)
+stop = time.perf_counter() + 4.0
+errs, flushes = [], [0]
+started = threading.Event()
+def feeder():
+    try:
+        ctx = qpp.Context(0)
+        k = ctx.key(1, rng.integers(0, 256, 32, dtype=np.uint8).tobytes())
+        kk, iv, hp = k.material()
+        q = qpp.TxQueue(ctx, 64 * STRIDE, 64, persistent=True)
+        pn = 5000
+        while time.perf_counter() < stop:
+            want = []
+            for i in range(64):
+                header = bytes([0x43]) + rng.integers(0, 256, 16, dtype=np.uint8).tobytes()
+                payload = rng.integers(0, 256, int(rng.integers(100, 1200)), dtype=np.uint8).tobytes()
+                trunc, pn_len = qpp.pn_truncate(pn + i, pn - 1)
+                pkt = header + trunc.to_bytes(pn_len, "big") + payload
+                q.ring[i * STRIDE:i * STRIDE + len(pkt)] = np.frombuffer(pkt, dtype=np.uint8)
+                q.push(k, pn + i, i * STRIDE, len(header), pn_len, len(payload))
+                want.append((i * STRIDE, orc.protect_packet(1, kk, iv, hp, pn + i, header, pn_len, payload)[1]))
+            q.flush()
+            for off, p in want:
+                assert q.ring[off:off + len(p)].tobytes() == p, ("flush", flushes[0])
+            pn += 64
+            flushes[0] += 1
+            started.set()
+        info = q.info()
+        assert q.server_refused() == 0
+        q.close()
+        ctx.close()
+        flushes.append(info)
+    except BaseException as e:
+        errs.append(repr(e))
+        started.set()
+t = threading.Thread(target=feeder, daemon=True)
+t.start()
+started.wait(60)
+a = qpp.Context(0)
+e0 = qpp.server_evictions(0)
+worst, n = 0.0, 0
+while time.perf_counter() < stop - 0.5 and not errs:
+    b = a.alloc(4 << 20)
+    b.upload(np.full(4 << 20, n & 0xff, dtype=np.uint8))
+    t0 = time.perf_counter(); b.free(); worst = max(worst, time.perf_counter() - t0)
+    h = a.host_alloc(4 << 20)
+    h[:] = n & 0xff
+    t0 = time.perf_counter(); a.host_free(h); worst = max(worst, time.perf_counter() - t0)
+    n += 1
+    time.sleep(0.05)
+t.join(60)
+assert not t.is_alive(), "feeder stuck"
+assert not errs, errs
+e1 = qpp.server_evictions(0)
+a.close()
+assert worst < 1.0, worst
+assert e1[0] > e0[0], (e0, e1)
+srv, launched, starts = flushes[-1]
+assert srv > 0 and starts >= 2, flushes[-1]
+print("ok frees", n, "worst_ms", round(worst * 1e3, 2), "flushes", flushes[0], "server", srv, "launched", launched,
+      "starts", starts, "evictions", e1[0] - e0[0], "oneshots", e1[1] - e0[1])
+'''
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, QPP_PARKED_MAX_MB="1", QPP_TXQ_SERVER_IDLE_MS="20000",
+               PYTHONPATH=os.pathsep.join([here, os.path.join(os.path.dirname(here), "s2n-quic_amd")]))
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=110, cwd=here)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "ok" in r.stdout

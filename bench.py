@@ -47,6 +47,13 @@ def open_bytes_per_packet(pt, aad):
     return aad + pt + 16 + 24 + pt + 1
 
 
+def rx_bytes_per_packet(pt, aad):
+    """receive path (qpp_unprotect_open_batch), DESIGN.md §4: read the rx descriptor (24), AAD (the header, aad), CT (pt)
+    and tag (16; the HP sample lies inside the CT); write the unprotected first byte + PN bytes (5), the packet
+    descriptor the call returns (24), the plaintext (pt) and the status (1) -- 2P + aad + 70 (2491 B at P = 1200)"""
+    return 24 + aad + pt + 16 + 5 + 24 + pt + 1
+
+
 LDS_PEAK_CYCLES = 256 * 2.4e9  # LDS-array cycles per second: one array per CU, 256 CUs at the 2.4 GHz spec clock
 
 
@@ -339,7 +346,7 @@ def main():
                 "unit": "G wave-instructions/s", "frac": round(ins / (seal_avg / 1e3) / (VALU_PEAK_PER_NS * 1e9), 4),
                 "model": "bench.chacha_valu_per_packet (SQ_INSTS_VALU); peak measured by tools/ubench/issue.hip",
             }
-        if suite in (1, 2) and n > burst_max and args.keys * 1024 <= n:
+        if suite in (1, 2) and n > burst_max and args.keys * qpp.WAVE_KERNEL_PACKETS_PER_KEY <= n:
             # the quad kernel's own bounds: the CU's LDS array (T-table + GHASH-table lookups) and VALU issue, not HBM
             nr = 10 if suite == 1 else 14
             cyc = n * aes_lds_cycles_per_packet(pt, aad, nr)
@@ -348,7 +355,8 @@ def main():
                 "bound": "lds", "achieved": round(cyc / (seal_avg / 1e3) / 1e9, 1), "peak": LDS_PEAK_CYCLES / 1e9,
                 "unit": "G LDS-array cycles/s", "frac": round(cyc / (seal_avg / 1e3) / LDS_PEAK_CYCLES, 4),
                 "model": "bench.aes_lds_cycles_per_packet (quad layout), checked against SQ_LDS_IDX_ACTIVE; "
-                         "peak = 256 CUs x 2.4 GHz",
+                         "peak = 256 CUs x 2.4 GHz" + ("" if args.keys == 1 else
+                         "; per-packet work only: the per-key-segment table builds are not in the model"),
                 "valu": {"achieved": round(ins / (seal_avg / 1e3) / 1e9, 1), "peak": VALU_PEAK_PER_NS,
                          "unit": "G wave-instructions/s", "frac": round(ins / (seal_avg / 1e3) / (VALU_PEAK_PER_NS * 1e9), 4),
                          "model": "bench.aes_valu_per_packet, calibrated on SQ_INSTS_VALU; peak measured by "
@@ -549,11 +557,32 @@ def rx(args, ctx, keys, descs, arena, d_desc, d_mask, d_status, flags, rank, wor
     assert (st == 0).all(), f"{int((st != 0).sum())} packets failed to open"
     t = max_over_ranks(float(np.mean(ms)))
     if rank == 0:
-        print(json.dumps({
+        out = {
             "metric": "GiB/s receive path (unprotect -> PN expand -> open), device-resident, 1200 B packets",
             "value": round(n * pt * world / (t / 1e3) / GiB, 3), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
             "ms_per_step": round(t, 4), "suite": args.suite, "packets_per_gpu": n, "keys": args.keys,
-        }), flush=True)
+        }
+        suite = SUITES[args.suite]
+        achieved = n * rx_bytes_per_packet(pt, aad) / (t / 1e3) / 1e9
+        out["roofline"] = {
+            "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            "kernel": "aes_gcm_quad_rx_kernel (one launch: unprotect, group-by key, open)" if suite in (1, 2) else
+                      "chacha_kernel<open, RX>" if suite == 3 else "aes_gcm_quad_rx_kernel + chacha_kernel<open, RX>",
+            "bytes_per_packet": rx_bytes_per_packet(pt, aad),
+        }
+        if suite in (1, 2):
+            # the open phase is the quad kernel's work (E_K(J0) on the quad in place of the HP mask); the unprotect
+            # phase adds one lane-per-packet AES of the sample (16 lookups per round, 2 LDS cycles per wave instruction)
+            nr = 10 if suite == 1 else 14
+            cyc = n * (aes_lds_cycles_per_packet(pt, aad, nr) + 16 * nr * 2 / 64.0)
+            out["kernel_roofline"] = {
+                "bound": "lds", "achieved": round(cyc / (t / 1e3) / 1e9, 1), "peak": LDS_PEAK_CYCLES / 1e9,
+                "unit": "G LDS-array cycles/s", "frac": round(cyc / (t / 1e3) / LDS_PEAK_CYCLES, 4),
+                "model": "bench.aes_lds_cycles_per_packet (quad open) + the unprotect phase's sample AES; "
+                         "peak = 256 CUs x 2.4 GHz; checked against SQ_LDS_IDX_ACTIVE (profiles/r06/rx)",
+            }
+        print(json.dumps(out), flush=True)
     ctx.close()
 
 

@@ -89,8 +89,8 @@ int qpp_ctx_set_packet_server(qpp_ctx *ctx, int on);
 /* Per-packet calls the packet server has taken so far, and its kernel launches (it leaves when idle). */
 int qpp_ctx_packet_server_info(const qpp_ctx *ctx, uint64_t *calls, uint64_t *starts);
 /* AES-GCM batches larger than burst_max: the quad kernel (four lanes per packet, one workgroup per CU over a slice of
- * the key-sorted packets) serves batches with at least 1024 packets per live AES key, the wave-item kernel (one key
- * per 64-packet wave) batches with fewer (many keys, few packets each: key-update churn).  This forces one of them
+ * the key-sorted packets) serves batches with at least 128 packets per live AES key (1024 past 16384 live AES keys),
+ * the wave-item kernel (one key per 64-packet wave) batches with fewer (many keys, few packets each).  This forces one of them
  * (env QPP_AES_KERNEL=quad|wave); outputs are identical.  QPP_AES_KERNEL_LANE is the round-1..3 name of the quad
  * selector (the lane-per-packet kernel it named was replaced by the quad kernel) and is kept for source compatibility. */
 #define QPP_AES_KERNEL_AUTO 0
@@ -409,7 +409,7 @@ typedef struct qpp_rx_pkt {
  * QPP_INTERNAL_ERROR (a slot outside the table, a key_idx[0] slot holding no key -- nothing touched -- or a chosen
  * packet key that is not live: header unprotected, payload untouched).  QPP_ONLY_AES / QPP_ONLY_CHACHA: packets whose
  * (live) key is of the other family are unprotected but not opened, their status left as it was.
- * Launches: with any live AES packet key and a batch of the quad kernel's size (>= 1024 packets per live AES key),
+ * Launches: with any live AES packet key and a batch of the quad kernel's size (see qpp_ctx_set_aes_kernel),
  * ONE cooperative launch unprotects, groups by the chosen key and opens the AES packets of both sizes, and one more
  * launch on the same stream opens the ChaCha20 packets it sorted out (when ChaCha20 keys are live); with no AES record
  * live, one launch of the ChaCha20 kernel; otherwise unprotect + plan + open kernels.  Identical outputs on every path

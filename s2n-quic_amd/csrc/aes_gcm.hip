@@ -344,12 +344,12 @@ hipError_t launch_key_install(DevKey *keys, const uint32_t *slots, const DevKey 
 
 hipError_t launch_aes_gcm_single(bool seal, const DevKey *keys, const qpp_pkt *descs, uint32_t slot, uint32_t nr,
                                  uint32_t n, uint32_t n_cu, uint8_t *arena, uint8_t *masks, int8_t *status,
-                                 uint32_t flags, hipStream_t s) {
+                                 uint32_t flags, const PowTables &pow, hipStream_t s) {
     if (!n) return hipSuccess;
     const PlanBuffers none{};
     const uint32_t waves = (n + 15) / 16;  // quad layout: 16 packets per wave
     const dim3 grid(waves < n_cu ? waves : n_cu);
-    return launch_aes_gcm_quad(seal, nr, grid, s, keys, descs, none, arena, masks, status, flags, slot, n);
+    return launch_aes_gcm_quad(seal, nr, grid, s, keys, descs, none, arena, masks, status, flags, slot, n, pow);
 }
 
 hipError_t launch_aes_gcm_wave(bool seal, const DevKey *keys, const qpp_pkt *descs, const PlanBuffers &pb, uint32_t n,
@@ -379,7 +379,7 @@ hipError_t launch_aes_gcm_wave(bool seal, const DevKey *keys, const qpp_pkt *des
 
 hipError_t launch_aes_gcm(bool seal, const DevKey *keys, const qpp_pkt *descs, const PlanBuffers &pb, uint32_t n,
                           uint32_t n_cu, uint8_t *arena, uint8_t *masks, int8_t *status, uint32_t flags,
-                          uint32_t suites, hipStream_t s) {
+                          uint32_t suites, const PowTables &pow, hipStream_t s) {
     if (!n) return hipSuccess;
     // one slice per CU (quad.hip); a batch smaller than a wave per CU takes fewer workgroups
     const uint32_t waves = (n + 15) / 16;
@@ -389,7 +389,7 @@ hipError_t launch_aes_gcm(bool seal, const DevKey *keys, const qpp_pkt *descs, c
     // two serial full-chip launches
     if (a128 || a256)
         launch_aes_gcm_quad(seal, a128 && a256 ? 0u : a128 ? 10u : 14u, grid, s, keys, descs, pb, arena, masks, status,
-                            flags, 0xffffffffu, 0);
+                            flags, 0xffffffffu, 0, pow);
     return hipGetLastError();
 }
 

@@ -737,7 +737,8 @@ AesPath aes_path(const qpp_ctx *ctx, uint32_t n) {
     if (ctx->aes_kernel) return ctx->aes_kernel == QPP_AES_KERNEL_QUAD ? AesPath::quad : AesPath::wave;
     const uint64_t aes_keys = (uint64_t)ctx->live_by_suite[QPP_SUITE_TLS_AES_128_GCM_SHA256] +
                               ctx->live_by_suite[QPP_SUITE_TLS_AES_256_GCM_SHA384];
-    return (uint64_t)n < kWaveKernelPacketsPerKey * aes_keys ? AesPath::wave : AesPath::quad;
+    const uint64_t per_key = aes_keys <= kPowSlots ? kWaveKernelPacketsPerKey : kWaveKernelPacketsPerKeyNoPow;
+    return (uint64_t)n < per_key * aes_keys ? AesPath::wave : AesPath::quad;
 }
 uint32_t aes_per_item(const qpp_ctx *ctx, AesPath p, uint32_t n) {
     return p == AesPath::burst ? burst_packets_per_item(n, ctx->n_cu)
@@ -756,7 +757,7 @@ hipError_t launch_aes(const qpp_ctx *ctx, AesPath p, bool seal, const qpp_pkt *d
                                        flags, suite_mask(ctx), s);
         default:
             return launch_aes_gcm(seal, ctx->d_keys, descs, pb, n, cu_avail(ctx), arena, masks, status, flags,
-                                  suite_mask(ctx), s);
+                                  suite_mask(ctx), ctx->pow, s);
     }
 }
 
@@ -822,7 +823,7 @@ int enqueue_seal(qpp_ctx *ctx, StreamState *st, const qpp_pkt *descs, uint32_t n
         const uint32_t one = path == AesPath::quad ? single_aes_slot(ctx) : UINT32_MAX;
         if (one != UINT32_MAX) {
             HIP_TRY(ctx, launch_aes_gcm_single(true, ctx->d_keys, descs, one, ctx->h_keys[one].nr, n, cu_avail(ctx), arena,
-                                               masks, status, flags, s));
+                                               masks, status, flags, ctx->pow, s));
         } else {
             RC_TRY(ensure_plan(ctx, st, n));
             HIP_TRY(ctx, launch_plan(ctx->d_keys, ctx->key_cap, descs, n, st->plan, aes_per_item(ctx, path, n), s));
@@ -845,7 +846,7 @@ int enqueue_open(qpp_ctx *ctx, StreamState *st, const qpp_pkt *descs, uint32_t n
         const uint32_t one = path == AesPath::quad ? single_aes_slot(ctx) : UINT32_MAX;
         if (one != UINT32_MAX) {
             HIP_TRY(ctx, launch_aes_gcm_single(false, ctx->d_keys, descs, one, ctx->h_keys[one].nr, n, cu_avail(ctx), arena,
-                                               nullptr, status, 0, s));
+                                               nullptr, status, 0, ctx->pow, s));
         } else {
             RC_TRY(ensure_plan(ctx, st, n));
             HIP_TRY(ctx, launch_plan(ctx->d_keys, ctx->key_cap, descs, n, st->plan, aes_per_item(ctx, path, n), s));
@@ -911,7 +912,7 @@ int run_one(const qpp_key *k, bool seal, uint64_t pn, const uint8_t *header, siz
                                               1u << k->suite, ctx->pow, s));
         else
             HIP_TRY(ctx, launch_aes_gcm(seal, ctx->d_keys, vd, pb, 1, 1, v + kOnePkt, v + 80, vst, 0, 1u << k->suite,
-                                        s));
+                                        ctx->pow, s));
     } else {
         HIP_TRY(ctx, launch_chacha(seal, ctx->d_keys, ctx->key_cap, vd, 1, v + kOnePkt, v + 80, vst, 0,
                                    ctx->burst_max > 0, s));
@@ -1657,7 +1658,7 @@ int qpp_unprotect_open_batch(qpp_ctx *ctx, const qpp_rx_pkt *rx, size_t n, uint8
             const uint32_t grid = std::min<uint32_t>(free_cu, std::max<uint32_t>(1, (uint32_t)((n + 191) / 192)));
             HIP_TRY(ctx, launch_aes_gcm_quad_rx(a256 ? (a128 ? 0u : 14u) : 10u, grid, st->stream, ctx->d_keys, kc, rx,
                                                 (uint32_t)n, arena, descs_out, status, st->rx_scratch, st->plan.perm,
-                                                ctx->d_diag, chacha));
+                                                ctx->d_diag, chacha, ctx->pow));
             HIP_TRY(ctx, hipEventRecord(r.rx_tail, st->stream));
         }
         if (chacha)

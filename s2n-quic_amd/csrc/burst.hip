@@ -98,14 +98,16 @@ __device__ void burst_tables(const DevKey *__restrict__ key, uint32_t slot, cons
     burst_t0(key);
     if (slot < pow.cap) {
         const uint4 *src = (const uint4 *)(pow.base + (size_t)slot * kPowBytes);
-        for (uint32_t i = threadIdx.x; i < kPowBytes / 16; i += blockDim.x) lds_st128(tab(1) + 16u * i, src[i]);
+        for (uint32_t i = threadIdx.x; i < kPowTables * 8192u / 16; i += blockDim.x) lds_st128(tab(1) + 16u * i, src[i]);
         __syncthreads();
     } else {
         burst_powers();
     }
 }
 
-// One workgroup per listed slot: T_1 .. T_6 of an AES packet key into its pow slot.
+// One workgroup per listed slot: T_1 .. T_6 of an AES packet key into its pow slot, then the table of H^3 = T_1's
+// entries times H (through T_0) -- the quad kernels' 4-bit tables of H^2, H^3, H^4 (quad.hip quad_tables).
+constexpr uint32_t kPowSetupLds = kBurstGh + 8u * kBurstTab;  // T_0 .. T_6 and H^3's table: 128 KiB
 __global__ __launch_bounds__(512) void pow_setup_kernel(const DevKey *__restrict__ keys,
                                                         const uint32_t *__restrict__ slots, const PowTables pow) {
     const uint32_t slot = slots[blockIdx.x];
@@ -114,6 +116,10 @@ __global__ __launch_bounds__(512) void pow_setup_kernel(const DevKey *__restrict
     if (key->live != 1 || key->suite == QPP_SUITE_TLS_CHACHA20_POLY1305_SHA256) return;
     burst_t0(key);
     burst_powers();
+    for (uint32_t e = threadIdx.x; e < 512; e += blockDim.x)
+        lds_st128(tab(7) + 16u * e, gmul(tab(0), lds_ld128(tab(1) + 16u * e)));
+    __syncthreads();
+    static_assert(kPowBytes == 7u * 8192u, "pow slot = T_1 .. T_6 + H^3");
     uint4 *dst = (uint4 *)(pow.base + (size_t)slot * kPowBytes);
     for (uint32_t i = threadIdx.x; i < kPowBytes / 16; i += blockDim.x) dst[i] = lds_ld128(tab(1) + 16u * i);
 }
@@ -854,7 +860,7 @@ hipError_t launch_txq_server(const DevKey *keys, const PowTables &pow, TxsMail *
 hipError_t launch_pow_setup(const DevKey *keys, const uint32_t *slots, uint32_t count, const PowTables &pow,
                             hipStream_t s) {
     if (!count || !pow.cap) return hipSuccess;
-    hipLaunchKernelGGL(pow_setup_kernel, dim3(count), dim3(512), kBurstLds, s, keys, slots, pow);
+    hipLaunchKernelGGL(pow_setup_kernel, dim3(count), dim3(512), kPowSetupLds, s, keys, slots, pow);
     return hipGetLastError();
 }
 

@@ -173,7 +173,12 @@ struct Ghash4T {
     }
     // 32 reads, ~9 in flight: the running xor takes two per step and the next two are issued behind it (4096 keys x
     // 2 Mi packets: seal 3.64 -> 3.50 ms over the word-by-word form the scheduler serialised)
-    __device__ __forceinline__ uint4 prod(const uint4 &w, uint4 c) const {
+    __device__ __forceinline__ uint4 prod(const uint4 &w, uint4 c) const { return prod_impl<true>(w, c); }
+    // W * H alone (no zero operand kept live: the quad kernels' final products, where a zero uint4 held across the
+    // packet loop was spilled)
+    __device__ __forceinline__ uint4 prod(const uint4 &w) const { return prod_impl<false>(w, w); }
+    template <bool C>
+    __device__ __forceinline__ uint4 prod_impl(const uint4 &w, uint4 c) const {
         const uint32_t wk[4] = {w.x, w.y, w.z, w.w};
         uint32_t hs[4], ls[4];
 #pragma unroll
@@ -191,7 +196,8 @@ struct Ghash4T {
         uint4 acc = c;
         static_for<16>([&](auto tc) {
             constexpr int t = decltype(tc)::value;
-            acc = xor3(acc, r[2 * t], r[2 * t + 1]);
+            if constexpr (!C && t == 0) acc = r[0] ^ r[1];
+            else acc = xor3(acc, r[2 * t], r[2 * t + 1]);
             if constexpr (2 * t + 9 < 32) issue(std::integral_constant<int, 2 * t + 9>{});
             if constexpr (2 * t + 10 < 32) issue(std::integral_constant<int, 2 * t + 10>{});
             __builtin_amdgcn_sched_barrier(0);

@@ -94,7 +94,11 @@ struct WorkItem {
 
 constexpr int kMinPacketsPerItem = 4;
 constexpr uint32_t kWavePacketsPerItem = 64;  // aes_gcm_wave_kernel: one wave, one key, <= 64 packets per work item
-constexpr uint32_t kWaveKernelPacketsPerKey = 1024;  // batches with fewer packets per live AES key take the wave kernel
+// batches with fewer packets per live AES key take the wave kernel: 128 while every live key can have a pow slot (the quad
+// kernel's per-segment tables come from it), else 1024 (round 6 crossover, profiles/r06/manykey: 4096 keys x 64 / 128 /
+// 256 / 512 packets per key, quad vs wave 386 / 645 / 781 / 876 vs 489 / 610 / 668 / 666 GiB/s)
+constexpr uint32_t kWaveKernelPacketsPerKey = 128;
+constexpr uint32_t kWaveKernelPacketsPerKeyNoPow = 1024;
 constexpr uint32_t kQuadPerItem = 0x7fffffffu;  // aes_gcm_quad_kernel: one work item per key (workgroups take equal slices)
 constexpr uint32_t kBurstMaxDefault = 16384;  // AES batches up to this many packets run one wave per packet
 constexpr uint32_t kChachaBurstShift = 2;     // ChaCha20-Poly1305 batches up to burst_max >> 2 do (its lane kernel
@@ -106,8 +110,12 @@ constexpr int kMaxPlanKeys = 8192;      // keys binned in LDS by the plan kernel
 // Per-key GHASH power tables of the burst kernel (burst.hip): T_t = 4-bit tables of H^(2^t), t = 1..6, 48 KiB per
 // key slot below `cap`, computed when the key is installed (they used to be rebuilt by every workgroup of every
 // burst launch: about half of a 64-packet flush).  Slots >= cap (huge key tables) still build them per launch.
-constexpr uint32_t kPowBytes = 6u * 8192u;
-constexpr uint32_t kPowSlots = 4096;  // at most 192 MiB per context
+// A slot: T_1 .. T_6, the 4-bit tables of H^(2^t) (burst kernels, servers), then the 4-bit table of H^3 (with T_1 =
+// H^2 and T_2 = H^4: the quad kernels' per-key-segment tables come from the slot instead of being derived in LDS)
+constexpr uint32_t kPowTables = 6;
+constexpr uint32_t kPowH3 = kPowTables * 8192u;
+constexpr uint32_t kPowBytes = kPowH3 + 8192u;
+constexpr uint32_t kPowSlots = 16384;  // at most 896 MiB per context (allocated as the key table grows)
 struct PowTables {
     uint8_t *base;  // [cap][kPowBytes]
     uint32_t cap;
@@ -205,12 +213,12 @@ hipError_t launch_pow_setup(const DevKey *keys, const uint32_t *slots, uint32_t 
 // plan with per = kQuadPerItem; one workgroup per CU, each an equal slice of the key-sorted packets
 hipError_t launch_aes_gcm(bool seal, const DevKey *keys, const qpp_pkt *descs, const PlanBuffers &pb, uint32_t n,
                           uint32_t n_cu, uint8_t *arena, uint8_t *masks, int8_t *status, uint32_t flags,
-                          uint32_t suites, hipStream_t s);
+                          uint32_t suites, const PowTables &pow, hipStream_t s);
 // one live AES key (slot, nr): the quad kernel over descs[0, n) without a plan; packets of any other slot are refused
 // (status INTERNAL_ERROR)
 hipError_t launch_aes_gcm_single(bool seal, const DevKey *keys, const qpp_pkt *descs, uint32_t slot, uint32_t nr,
                                  uint32_t n, uint32_t n_cu, uint8_t *arena, uint8_t *masks, int8_t *status,
-                                 uint32_t flags, hipStream_t s);
+                                 uint32_t flags, const PowTables &pow, hipStream_t s);
 // quad.hip: the quad-layout (4 lanes per packet, 768-thread workgroups) throughput kernel behind the two above
 // quad.hip: fused unprotect -> PN expand -> key-phase choice -> open for any mix of live packet keys (AES-128 and
 // AES-256 opened in the launch -- aes = 10 / 14 when only one size is live, 0 for both; ChaCha20 packets, when `chacha`, sorted to perm[scratch[3], + scratch[2]) for
@@ -221,7 +229,8 @@ hipError_t launch_aes_gcm_single(bool seal, const DevKey *keys, const qpp_pkt *d
 uint32_t quad_rx_max_keys();
 hipError_t launch_aes_gcm_quad_rx(uint32_t aes, uint32_t grid, hipStream_t s, const DevKey *keys, uint32_t key_cap,
                                   const qpp_rx_pkt *rx, uint32_t n, uint8_t *arena, qpp_pkt *descs_out, int8_t *status,
-                                  uint32_t *scratch, uint32_t *perm, uint32_t *timeouts, bool chacha);
+                                  uint32_t *scratch, uint32_t *perm, uint32_t *timeouts, bool chacha,
+                                  const PowTables &pow);
 // chacha.hip: open descs[sel[sel_meta[1] + i]] for i < min(n_max, sel_meta[0]) (count and base on the device)
 hipError_t launch_chacha_sel(const DevKey *keys, uint32_t key_cap, const qpp_pkt *descs, uint32_t n_max,
                              uint8_t *arena, int8_t *status, const uint32_t *sel, const uint32_t *sel_meta, hipStream_t s);
@@ -231,7 +240,8 @@ hipError_t launch_chacha_sel_batch(bool seal, const DevKey *keys, uint32_t key_c
                                    const uint32_t *sel_meta, hipStream_t s);
 hipError_t launch_aes_gcm_quad(bool seal, uint32_t nr, dim3 grid, hipStream_t s, const DevKey *keys,
                                const qpp_pkt *descs, const PlanBuffers &pb, uint8_t *arena, uint8_t *masks,
-                               int8_t *status, uint32_t flags, uint32_t single, uint32_t n_single);
+                               int8_t *status, uint32_t flags, uint32_t single, uint32_t n_single,
+                               const PowTables &pow);
 // many keys: work items of <= kWavePacketsPerItem packets (plan with per = kWavePacketsPerItem), one wave each
 hipError_t launch_aes_gcm_wave(bool seal, const DevKey *keys, const qpp_pkt *descs, const PlanBuffers &pb, uint32_t n,
                                uint32_t key_cap, uint32_t n_cu, uint8_t *arena, uint8_t *masks, int8_t *status,

@@ -74,6 +74,9 @@ constexpr int kQuadWG = NR == 14 ? QPP_QUAD_WG256 : QPP_QUAD_WG;
 #ifndef QPP_QUAD_NB
 #define QPP_QUAD_NB 4
 #endif
+#ifndef QPP_QUAD_TRACE
+#define QPP_QUAD_TRACE 0  // 1: workgroups 0 and grid/2 print their table-build and total cycles (s_memtime)
+#endif
 constexpr int kQNB = QPP_QUAD_NB, kQSG = 4 * kQNB;
 static_assert(kQNB >= 2 && kQNB <= 4, "group size");
 
@@ -98,8 +101,46 @@ __device__ __forceinline__ void build8(uint32_t v) {
     }
 }
 
+// The tables of one key segment from the key's pow slot (slot < pow.cap; burst.hip pow_setup_kernel fills it at install):
+// the 4-bit tables of H^2, H^4 (T_1, T_2) and H^3 are copied (burst layout, entry (pos = 2 b + h, n) at 256 pos + 16 n,
+// transposed to this kernel's 4096 h + 256 n + 16 b), H's are built from V[m], and the 8-bit tables of H^4 are two
+// lookups each in H^4's 4-bit tables (T_j[x] = high nibble (x >> 4) at byte j ^ low nibble (x & 15) at byte j, times
+// H^4).  The AES tables are not touched.  Round 6: the derivation in LDS below (V_e by three
+// dependent products, two 8-bit builds with up to 8 reads per entry, the AES tables rebuilt over its scratch) took a
+// tenth of a 4096-key batch's seal (QPP_QUAD_TRACE: 35 k of 349 k s_memtime ticks per segment).  Ends with a barrier.
+__device__ void quad_tables_pow(const DevKey *__restrict__ key, const uint4 *__restrict__ src) {
+    const uint32_t tid = threadIdx.x, nthr = blockDim.x;
+    for (uint32_t idx = tid; idx < 4 * 512; idx += nthr) {
+        const uint32_t t = idx >> 9, ent = idx & 511u, pos = ent >> 4, n = ent & 15u, b = pos >> 1, h = pos & 1u;
+        uint4 v;
+        uint32_t e;  // power
+        if (t == 0) {  // H: xor of V[8 b + 4 h + i] over the set bits (bit 3 - i) of n
+            e = 1;
+            const uint4 *V = (const uint4 *)key->V;
+            v = make_uint4(0, 0, 0, 0);
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const uint4 x = V[8 * b + 4 * h + i];
+                const uint32_t m = 0u - ((n >> (3 - i)) & 1u);
+                v = v ^ make_uint4(x.x & m, x.y & m, x.z & m, x.w & m);
+            }
+        } else {  // t = 1: T_1 = H^2, 2: T_2 = H^4, 3: H^3
+            e = t == 1 ? 2u : t == 2 ? 4u : 3u;
+            v = src[(t == 3 ? kPowH3 / 16 : (t - 1) * 512u) + ent];
+        }
+        lds_st128(kQLdsPow + 8192 * (e - 1) + 4096 * h + 256 * n + 16 * b, v);
+    }
+    __syncthreads();
+    constexpr uint32_t h4 = kQLdsPow + 3 * 8192;
+    for (uint32_t ent = tid; ent < 4096; ent += nthr) {
+        const uint32_t j = ent & 15u, x = ent >> 4;
+        lds_st128(256 * x + 16 * j, lds_ld128(h4 + 256 * (x >> 4) + 16 * j) ^ lds_ld128(h4 + 4096 + 256 * (x & 15u) + 16 * j));
+    }
+    __syncthreads();
+}
+
 // All tables of one key (every thread takes part; ends with a barrier).  The caller synced before (the previous
-// key's tables are no longer read).
+// key's tables are no longer read).  (Keys without a pow slot: the derivation in LDS, AES tables rebuilt after it.)
 __device__ void quad_tables(const DevKey *__restrict__ key) {
     const uint32_t tid = threadIdx.x, nthr = blockDim.x;
     for (uint32_t i = tid; i < 128; i += nthr) {
@@ -197,7 +238,10 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
     // (w = rot(x): no product of zero); a lane with no AAD block starts at w = 0 and its first data step multiplies zero
     // (one product more for those lanes, in exchange for no started-flag control flow in the group loop).  With the
     // usual 1..2 AAD blocks no lane has a second one and the product loop is skipped by the whole wave.
-    uint4 w = make_uint4(0, 0, 0, 0);
+    // (a zero made here, per packet: a zero uint4 kept from the kernel's start was spilled in the receive kernel)
+    uint32_t z0;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(z0));
+    uint4 w = make_uint4(z0, z0, z0, z0);
     {
         auto aad_block = [&](int t) {
             const uint32_t i = (uint32_t)(t + a - 1);
@@ -371,7 +415,7 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
     fin.g.q2 = gh.q2;
     fin.hi_or = 0x01010101u * ((2u * (e - 1u)) << 4);
     fin.lo_or = 0x01010101u * ((2u * (e - 1u) + 1u) << 4);
-    uint4 y = fin.prod(w, make_uint4(0, 0, 0, 0));
+    uint4 y = fin.prod(w);
     y = y ^ qperm<kQuadSwap1>(y);
     y = y ^ qperm<kQuadSwap2>(y);
 
@@ -409,7 +453,10 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
                           : s == 1 ? key->iv[1] ^ bswap32((uint32_t)(dt.pn >> 32))
                           : s == 2 ? key->iv[2] ^ bswap32((uint32_t)dt.pn)
                                    : bswap32(1u);
-        const uint32_t ek0 = aes_quad<NR>(aes, key->rk, j0, s);
+        uint32_t sl = s;
+        asm volatile("" : "+v"(sl));  // (left alone, the compiler kept &key->rk[s] in a VGPR pair across the packet loop
+                                      // of each key segment and spilled it: 4 VGPRs of scratch in every open instance)
+        const uint32_t ek0 = aes_quad<NR>(aes, key->rk, j0, sl);
         uint32_t want;
         __builtin_memcpy(&want, at(pay + len + 4 * s), 4);
         const uint32_t ys = s == 0 ? y.x : s == 1 ? y.y : s == 2 ? y.z : y.w;
@@ -435,7 +482,7 @@ __device__ __forceinline__ void quad_slices(const DevKey *__restrict__ keys, con
                                             const uint32_t *__restrict__ perm, const WorkItem *__restrict__ work,
                                             const uint32_t *__restrict__ meta, uint8_t *__restrict__ arena,
                                             uint8_t *masks, int8_t *status, uint32_t flags, uint32_t single,
-                                            uint32_t n_single) {
+                                            uint32_t n_single, const PowTables pow) {
     const bool one = single != 0xffffffffu;  // uniform
     uint32_t i_lo = 0, i_hi = 1, p0 = 0, n = n_single;
     if (!one) {
@@ -457,6 +504,11 @@ __device__ __forceinline__ void quad_slices(const DevKey *__restrict__ keys, con
     const QAes aes = make_qaes();
     const GhashT<true> gh = GhashT<true>::make();
     const uint32_t s = threadIdx.x & 3u, q = threadIdx.x >> 2;
+    build_qaes();  // once: the segments' table builds from a pow slot leave them alone (the first barrier below orders it)
+#if QPP_QUAD_TRACE
+    uint64_t t_beg = __builtin_amdgcn_s_memtime(), t_tab = 0;
+    uint32_t n_seg = 0;
+#endif
     for (; lo < hi; i++) {  // key segments of the slice
         WorkItem w = one ? WorkItem{single, 0u, n, (uint32_t)NR} : work[i];
         // (uniform; the fused receive kernel's work items are written by the same launch, so not scalar-loaded)
@@ -466,7 +518,15 @@ __device__ __forceinline__ void quad_slices(const DevKey *__restrict__ keys, con
         const uint32_t end = min(hi, w.begin + w.count);
         const DevKey *__restrict__ key = keys + w.key;
         __syncthreads();  // every wave is done with the previous segment's tables
-        quad_tables(key);
+#if QPP_QUAD_TRACE
+        const uint64_t t0 = __builtin_amdgcn_s_memtime();
+#endif
+        if (w.key < pow.cap) quad_tables_pow(key, (const uint4 *)(pow.base + (size_t)w.key * kPowBytes));
+        else quad_tables(key);
+#if QPP_QUAD_TRACE
+        t_tab += __builtin_amdgcn_s_memtime() - t0;
+        n_seg++;
+#endif
         for (uint32_t t0 = lo; t0 < end; t0 += WG / 4) {
             const uint32_t t = t0 + q;
             const bool real = t < end;
@@ -481,6 +541,12 @@ __device__ __forceinline__ void quad_slices(const DevKey *__restrict__ keys, con
         }
         lo = end;
     }
+#if QPP_QUAD_TRACE
+    __syncthreads();
+    if (threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x / 2))
+        printf("quad wg %u seal %d nr %d: %u segments, tables %llu of %llu cycles\n", blockIdx.x, (int)SEAL, NR, n_seg,
+               (unsigned long long)t_tab, (unsigned long long)(__builtin_amdgcn_s_memtime() - t_beg));
+#endif
 }
 
 // NR = 10 / 14: one AES size; NR = 0: a planned batch holding both sizes in ONE launch -- each workgroup opens its
@@ -494,10 +560,10 @@ __global__ __launch_bounds__(kQuadWG<NR>) void aes_gcm_quad_kernel(const DevKey 
                                                               const uint32_t *__restrict__ meta,
                                                               uint8_t *__restrict__ arena, uint8_t *masks,
                                                               int8_t *status, uint32_t flags, uint32_t single,
-                                                              uint32_t n_single) {
+                                                              uint32_t n_single, const PowTables pow) {
     constexpr int WG = kQuadWG<NR>;
-    if constexpr (NR != 14) quad_slices<SEAL, 10, WG>(keys, descs, perm, work, meta, arena, masks, status, flags, single, n_single);
-    if constexpr (NR != 10) quad_slices<SEAL, 14, WG>(keys, descs, perm, work, meta, arena, masks, status, flags, single, n_single);
+    if constexpr (NR != 14) quad_slices<SEAL, 10, WG>(keys, descs, perm, work, meta, arena, masks, status, flags, single, n_single, pow);
+    if constexpr (NR != 10) quad_slices<SEAL, 14, WG>(keys, descs, perm, work, meta, arena, masks, status, flags, single, n_single, pow);
 }
 
 // ---------------------------------------------------------------- fused receive path, any key mix, ONE launch
@@ -568,7 +634,7 @@ __global__ __launch_bounds__(kRxWG<AES>) void aes_gcm_quad_rx_kernel(const DevKe
                                                                  uint32_t key_cap, const qpp_rx_pkt *__restrict__ rx,
                                                                  uint32_t n, uint8_t *arena, qpp_pkt *descs_out,
                                                                  int8_t *status, uint32_t *scratch, uint32_t *perm,
-                                                                 uint32_t *timeouts, uint32_t chacha) {
+                                                                 uint32_t *timeouts, uint32_t chacha, const PowTables pow) {
     uint32_t *counts = scratch + 16, *cursor = counts + key_cap, *meta = cursor + key_cap;
     WorkItem *work = (WorkItem *)(meta + 4);  // 16-byte aligned: key_cap is even
 #if QPP_RX_TRACE
@@ -713,8 +779,8 @@ __global__ __launch_bounds__(kRxWG<AES>) void aes_gcm_quad_rx_kernel(const DevKe
     RX_TS(6);
     // D: open, key-sorted slices (tables per key segment, as a planned batch): the AES-128 packets, then the AES-256 ones
     constexpr int WG = kRxWG<AES>;
-    if constexpr (AES != 14) quad_slices<false, 10, WG>(keys, descs_out, perm, work, meta, arena, nullptr, status, 0u, ~0u, 0u);
-    if constexpr (AES != 10) quad_slices<false, 14, WG>(keys, descs_out, perm, work, meta, arena, nullptr, status, 0u, ~0u, 0u);
+    if constexpr (AES != 14) quad_slices<false, 10, WG>(keys, descs_out, perm, work, meta, arena, nullptr, status, 0u, ~0u, 0u, pow);
+    if constexpr (AES != 10) quad_slices<false, 14, WG>(keys, descs_out, perm, work, meta, arena, nullptr, status, 0u, ~0u, 0u, pow);
 #if QPP_RX_TRACE
     RX_TS(7);
     if (threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1 || blockIdx.x == gridDim.x / 2))
@@ -726,9 +792,10 @@ __global__ __launch_bounds__(kRxWG<AES>) void aes_gcm_quad_rx_kernel(const DevKe
 
 template <bool SEAL, int NR>
 void launch_quad(dim3 grid, hipStream_t s, const DevKey *keys, const qpp_pkt *descs, const PlanBuffers &pb,
-                 uint8_t *arena, uint8_t *masks, int8_t *status, uint32_t flags, uint32_t single, uint32_t n_single) {
+                 uint8_t *arena, uint8_t *masks, int8_t *status, uint32_t flags, uint32_t single, uint32_t n_single,
+                 const PowTables &pow) {
     hipLaunchKernelGGL((aes_gcm_quad_kernel<SEAL, NR>), grid, dim3(kQuadWG<NR>), kLdsMax, s, keys, descs, pb.perm, pb.work,
-                       pb.n_work, arena, masks, status, flags, single, n_single);
+                       pb.n_work, arena, masks, status, flags, single, n_single, pow);
 }
 }  // namespace
 
@@ -736,10 +803,12 @@ uint32_t quad_rx_max_keys() { return kRxHistMax; }
 
 hipError_t launch_aes_gcm_quad_rx(uint32_t aes, uint32_t grid, hipStream_t s, const DevKey *keys, uint32_t key_cap,
                                   const qpp_rx_pkt *rx, uint32_t n, uint8_t *arena, qpp_pkt *descs_out, int8_t *status,
-                                  uint32_t *scratch, uint32_t *perm, uint32_t *timeouts, bool chacha) {
+                                  uint32_t *scratch, uint32_t *perm, uint32_t *timeouts, bool chacha,
+                                  const PowTables &pow) {
     if (key_cap > kRxHistMax || (key_cap & 1u)) return hipErrorInvalidValue;
     uint32_t ch = chacha ? 1u : 0u;
-    void *args[] = {&keys, &key_cap, &rx, &n, &arena, &descs_out, &status, &scratch, &perm, &timeouts, &ch};
+    PowTables pw = pow;
+    void *args[] = {&keys, &key_cap, &rx, &n, &arena, &descs_out, &status, &scratch, &perm, &timeouts, &ch, &pw};
     // cooperative: the grid barriers need every workgroup resident (one per CU: grid <= the CUs it may use)
     const void *f = aes == 10   ? reinterpret_cast<const void *>(&aes_gcm_quad_rx_kernel<10>)
                     : aes == 14 ? reinterpret_cast<const void *>(&aes_gcm_quad_rx_kernel<14>)
@@ -763,16 +832,17 @@ hipError_t launch_aes_gcm_quad_rx(uint32_t aes, uint32_t grid, hipStream_t s, co
 // planned batch (pb), else the one live AES key's slot (descs[0, n_single) in order, other slots refused).
 hipError_t launch_aes_gcm_quad(bool seal, uint32_t nr, dim3 grid, hipStream_t s, const DevKey *keys,
                                const qpp_pkt *descs, const PlanBuffers &pb, uint8_t *arena, uint8_t *masks,
-                               int8_t *status, uint32_t flags, uint32_t single, uint32_t n_single) {
+                               int8_t *status, uint32_t flags, uint32_t single, uint32_t n_single,
+                               const PowTables &pow) {
     if (nr == 10) {
-        if (seal) launch_quad<true, 10>(grid, s, keys, descs, pb, arena, masks, status, flags, single, n_single);
-        else launch_quad<false, 10>(grid, s, keys, descs, pb, arena, masks, status, flags, single, n_single);
+        if (seal) launch_quad<true, 10>(grid, s, keys, descs, pb, arena, masks, status, flags, single, n_single, pow);
+        else launch_quad<false, 10>(grid, s, keys, descs, pb, arena, masks, status, flags, single, n_single, pow);
     } else if (nr == 14) {
-        if (seal) launch_quad<true, 14>(grid, s, keys, descs, pb, arena, masks, status, flags, single, n_single);
-        else launch_quad<false, 14>(grid, s, keys, descs, pb, arena, masks, status, flags, single, n_single);
+        if (seal) launch_quad<true, 14>(grid, s, keys, descs, pb, arena, masks, status, flags, single, n_single, pow);
+        else launch_quad<false, 14>(grid, s, keys, descs, pb, arena, masks, status, flags, single, n_single, pow);
     } else {  // both sizes (a planned batch)
-        if (seal) launch_quad<true, 0>(grid, s, keys, descs, pb, arena, masks, status, flags, single, n_single);
-        else launch_quad<false, 0>(grid, s, keys, descs, pb, arena, masks, status, flags, single, n_single);
+        if (seal) launch_quad<true, 0>(grid, s, keys, descs, pb, arena, masks, status, flags, single, n_single, pow);
+        else launch_quad<false, 0>(grid, s, keys, descs, pb, arena, masks, status, flags, single, n_single, pow);
     }
     return hipGetLastError();
 }

@@ -39,6 +39,7 @@ PKT_DTYPE = np.dtype([("pn", "<u8"), ("key_idx", "<u4"), ("off", "<u4"), ("aad_l
 assert PKT_DTYPE.itemsize == 24
 PKT_SKIP = 0x1
 BURST_MAX_DEFAULT = 16384  # kBurstMaxDefault (qpp_internal.h): larger AES batches run one lane per packet
+WAVE_KERNEL_PACKETS_PER_KEY = 128  # kWaveKernelPacketsPerKey: fewer packets per live AES key take the wave-item kernel
 # qpp_rx_pkt (24 bytes): one received, still protected packet
 RX_DTYPE = np.dtype([("largest_pn", "<u8"), ("key_idx", "<u4", (2,)), ("off", "<u4"), ("header_len", "<u2"),
                      ("len", "<u2")])

@@ -77,7 +77,24 @@ constexpr int kQuadWG = NR == 14 ? QPP_QUAD_WG256 : QPP_QUAD_WG;
 #ifndef QPP_QUAD_TRACE
 #define QPP_QUAD_TRACE 0  // 1: workgroups 0 and grid/2 print their table-build and total cycles (s_memtime)
 #endif
+#ifndef QPP_QUAD_ABL
+#define QPP_QUAD_ABL 0  // ablation bits for timing A/Bs only (wrong bytes): 1 no interior payload loads, 2 no interior
+                        // stores, 4 no header protection, 8 no final H^e product (the quad sums the chains as they are); DESIGN §5
+                        // round 6 has what each cost
+#endif
+#ifndef QPP_QUAD_PF
+#define QPP_QUAD_PF 0  // L2 touches: 1 the next group's payload lines at a group's start, 2 the next packet's descriptor
+#endif
 constexpr int kQNB = QPP_QUAD_NB, kQSG = 4 * kQNB;
+// An L2 touch: a 4-byte LDS-DMA load (no VGPR destination), so that a later load of the same line hits the L2 instead
+// of HBM.  A wave's DMA writes 4 bytes per lane at its LDS base + 4 lane: the two half-waves each land their 128 bytes
+// in the unused upper half of AES table row 0 (AesQ4 uses the lower 128 B of every 256-B row), which nothing reads.
+__device__ __forceinline__ void l2_touch(const uint8_t *p) {
+    typedef __attribute__((address_space(3))) void lds_void;
+    const void *g = (const void *)((uintptr_t)p & ~(uintptr_t)3);
+    if (__lane_id() < 32) __builtin_amdgcn_global_load_lds(g, (lds_void *)(size_t)(kLdsAes + 128u), 4, 0, 0);
+    else __builtin_amdgcn_global_load_lds(g, (lds_void *)(size_t)(kLdsAes), 4, 0, 0);
+}
 static_assert(kQNB >= 2 && kQNB <= 4, "group size");
 
 
@@ -228,6 +245,7 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
                                             uint32_t flags, uint32_t s) {
     // loop state
     const uint32_t aad_len = d.aad_len, len = has ? d.pt_len : 0u, pay = d.off + aad_len;
+    const uint32_t pn_len = SEAL ? (uint32_t)d.pn_len : 0u;  // (seal: header protection)
     const uint32_t n0 = key->iv[0], n1 = key->iv[1] ^ bswap32((uint32_t)(d.pn >> 32)),  // Iv::nonce (iv.rs:27-39)
                    n2 = key->iv[2] ^ bswap32((uint32_t)d.pn);
     const int nfull = (int)(len >> 4), rem = (int)(len & 15), m = nfull + (rem ? 1 : 0);
@@ -274,6 +292,9 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
     const int G = (int)wave_max((uint32_t)ngroups);
     const int min_full = (int)__builtin_amdgcn_readfirstlane(wave_min(has ? (uint32_t)nfull : 0u));
     auto interior = [&](int g) { return g >= 1 && kQSG * g + kQSG - 1 <= min_full; };  // every slot a whole payload block
+    // group 0 when slots 1..15 are whole payload blocks in every packet of the wave: the interior path, with slot 0
+    // (J0: keystream only, neither stored nor hashed) masked per lane
+    const bool head_ok = kQSG - 1 <= min_full;  // uniform
     // counter blocks per lane the last group needs (uniform): the longest packet's slots past 16 (G - 1)
     const int tail_slots = (int)wave_max(has ? (uint32_t)max(0, m + 1 - kQSG * (G - 1)) : 0u);
     // length block: be64(aad bits) || be64(payload bits)
@@ -289,10 +310,12 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
     // payload.rs:151-169) lies in ciphertext blocks 0 and 1 -- slots 1 and 2, group 0, lanes 1 and 2 -- when the payload
     // has at least 20 - pn_len bytes.  The header bytes are then written while the packet's first 64-byte segment still
     // holds group 0's ciphertext in L2 (one memory write for both, not two), and nothing is read back.
+    // The header bytes the mask applies to (the first byte and the PN's 4-byte window) are loaded with group 0's payload
+    // (one memory round trip for both), the descriptor fields are the packet's own (no reload)
+    const bool hp_at0 = want_hp && has && pn_len >= 1 && pn_len <= 4 && len + pn_len >= 20;  // quad-uniform
+    HdrBytes hb{0u, 0u};
     auto hp_early = [&](const uint4 &ct) {
-        const qpp_pkt dt = reload_desc(descs, pkt_index);
-        const uint32_t pn_len = dt.pn_len;
-        if (!(want_hp && has && pn_len >= 1 && pn_len <= 4 && len + pn_len >= 20)) return;  // quad-uniform
+        if (!hp_at0) return;
         const uint4 b0 = qperm<kQuadBcast1>(ct), b1 = qperm<kQuadBcast2>(ct);  // ciphertext blocks 0 and 1
         const uint32_t lo = s == 0 ? b0.x : s == 1 ? b0.y : s == 2 ? b0.z : b0.w;
         const uint32_t hi = s == 0 ? b0.y : s == 1 ? b0.z : s == 2 ? b0.w : b1.x;
@@ -306,7 +329,7 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
                 mo[3] = (uint8_t)(m0 >> 24); mo[4] = (uint8_t)m1;
             }
             const uint32_t hdr_len = aad_len - pn_len;
-            if (flags & QPP_HP_APPLY) hdr_apply(at(dt.off), hdr_len, pn_len, hdr_load(at(dt.off), hdr_len), m0, m1);
+            if (flags & QPP_HP_APPLY) hdr_apply(at(pay - aad_len), hdr_len, pn_len, hb, m0, m1);
         }
         hp_done = true;
     };
@@ -314,6 +337,14 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
     // one group: slots t = kQSG g + 4 k + s, k < NBG; slot t holds counter t + 1 and ciphertext block t - 1
     auto group = [&](auto nbc, int g) __attribute__((always_inline)) {
         constexpr int NBG = decltype(nbc)::value;
+        const bool head = NBG == kQNB && g == 0 && head_ok;  // uniform
+        if ((QPP_QUAD_PF & 1) && g + 1 < G) {
+            // group g + 1's 256 bytes [A, A + 256) span at most 3 lines: lanes touch A, A + 64, A + 128, A + 255
+            // (clamped to the packet's tag)
+            const uint32_t A = pay + 16u * (uint32_t)(kQSG * (g + 1) - 1), lim = pay + len + 15u;
+            const uint32_t x = A + (s == 3 ? 255u : 64u * s);
+            l2_touch(at(x < lim ? x : lim));
+        }
         const bool inner = NBG == kQNB && interior(g);  // uniform
         const RkPtr rkp = round_keys();
         const int t0 = kQSG * g + (int)s;
@@ -345,10 +376,19 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
         // payload after the keystream (loading the next interior group's payload while this group hashes measured 8 %
         // slower: 1.248 vs 1.152 ms seal, 8 VGPRs spilled, profiles/r04h_ab)
         uint4 in[NBG];
-        if (inner) {
+        if (SEAL && g == 0 && hp_at0 && (flags & QPP_HP_APPLY) && s == 0) hb = hdr_load(at(pay - aad_len), aad_len - pn_len);
+        if (head) {
+            // slot 0 (lane 0, k = 0) reads the payload's first block instead of the bytes before it (never used)
             const uint32_t b = pay + 16 * (uint32_t)(t0 - 1);
 #pragma unroll
-            for (int k = 0; k < NBG; k++) in[k] = ld_payload(at(b + 64 * k));
+            for (int k = 0; k < NBG; k++) in[k] = ld_payload(at(k == 0 && s == 0 ? pay : b + 64 * k));
+        } else if (inner) {
+            const uint32_t b = pay + 16 * (uint32_t)(t0 - 1);
+#pragma unroll
+            for (int k = 0; k < NBG; k++) {
+                if (QPP_QUAD_ABL & 1) in[k] = make_uint4(b + k, b ^ k, b, k);
+                else in[k] = ld_payload(at(b + 64 * k));
+            }
         } else {
 #pragma unroll
             for (int k = 0; k < NBG; k++) {
@@ -364,14 +404,32 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
             // the end instead)
             if (g == 0) ek0 = ks[0];
         }
-        if (inner) {
+        if (head) {
+            const uint32_t b = pay + 16 * (uint32_t)(t0 - 1);
+#pragma unroll
+            for (int k = 0; k < NBG; k++)
+                if (k != 0 || s != 0) st_payload(at(b + 64 * k), out[k]);
+#pragma unroll
+            for (int k = 0; k < NBG; k++) {
+                const uint4 wn = gh.mulx(w, SEAL ? out[k] : in[k]);
+                if (k != 0) {
+                    w = wn;
+                } else {  // slot 0 is not hashed (per component: a select of the whole vector went through scratch)
+                    w.x = s != 0 ? wn.x : w.x;
+                    w.y = s != 0 ? wn.y : w.y;
+                    w.z = s != 0 ? wn.z : w.z;
+                    w.w = s != 0 ? wn.w : w.w;
+                }
+            }
+        } else if (inner) {
             const uint32_t b = pay + 16 * (uint32_t)(t0 - 1);
             // (Every chunk in its own group.  Deferring the last 64 bytes of an interior group to the next group's
             // first store, and holding the packet's first 64 ciphertext bytes and its header bytes to its end next to
             // the tag, were both measured to write MORE, not less, and to run slower: round 5, profiles/r05/r05i --
             // seal WRITE_SIZE 1.473 / 1.491 vs 1.457 MB per launch, seal 1.161 / 1.173 vs 1.152 ms.)
 #pragma unroll
-            for (int k = 0; k < NBG; k++) st_payload(at(b + 64 * k), out[k]);
+            for (int k = 0; k < NBG; k++)
+                if (!(QPP_QUAD_ABL & 2)) st_payload(at(b + 64 * k), out[k]);
 #pragma unroll
             for (int k = 0; k < NBG; k++) w = gh.mulx(w, SEAL ? out[k] : in[k]);
         } else {
@@ -392,7 +450,7 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
                 len_done = len_done || lenslot;
             }
         }
-        if (SEAL && g == 0) hp_early(out[0]);
+        if (SEAL && g == 0 && !(QPP_QUAD_ABL & 4)) hp_early(out[0]);
     };
     for (int g = 0; g + 1 < G; g++) group(std::integral_constant<int, kQNB>{}, g);
     if (G > 0) {  // the last group with as few counter blocks per lane as its longest packet needs
@@ -415,15 +473,13 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
     fin.g.q2 = gh.q2;
     fin.hi_or = 0x01010101u * ((2u * (e - 1u)) << 4);
     fin.lo_or = 0x01010101u * ((2u * (e - 1u) + 1u) << 4);
-    uint4 y = fin.prod(w);
+    uint4 y = (QPP_QUAD_ABL & 8) ? w : fin.prod(w);
     y = y ^ qperm<kQuadSwap1>(y);
     y = y ^ qperm<kQuadSwap2>(y);
 
     if constexpr (SEAL) {
         if (has && s == 0) st16(at(pay + len), y ^ ek0);  // tag = GHASH ^ E_K(J0)
-        const qpp_pkt dt = reload_desc(descs, pkt_index);
-        const uint32_t pn_len = dt.pn_len;
-        const bool hp = want_hp && has && pn_len >= 1 && pn_len <= 4 && len >= 4 - pn_len;  // quad-uniform
+        const bool hp = !(QPP_QUAD_ABL & 4) && want_hp && has && pn_len >= 1 && pn_len <= 4 && len >= 4 - pn_len;
         if (hp && !hp_done) {  // short payloads: the sample runs into the tag
             // header-protection sample = ciphertext||tag bytes [4 - pn_len, 20 - pn_len) (payload.rs:151-169), column s
             // read back (the quad's lanes stored the blocks and lane 0 the tag: a wavefront fence orders them first;
@@ -440,7 +496,7 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
                     mo[3] = (uint8_t)(m0 >> 24); mo[4] = (uint8_t)m1;
                 }
                 const uint32_t hdr_len = aad_len - pn_len;
-                if (flags & QPP_HP_APPLY) hdr_apply(at(dt.off), hdr_len, pn_len, hdr_load(at(dt.off), hdr_len), m0, m1);
+                if (flags & QPP_HP_APPLY) hdr_apply(at(pay - aad_len), hdr_len, pn_len, hdr_load(at(pay - aad_len), hdr_len), m0, m1);
             }
         }
         if (!has || s != 0) return;
@@ -532,6 +588,7 @@ __device__ __forceinline__ void quad_slices(const DevKey *__restrict__ keys, con
             const bool real = t < end;
             const uint32_t pi = one ? (real ? t : lo) : perm[real ? t : lo];
             const qpp_pkt d = descs[pi];  // (any valid descriptor for quads without a packet)
+            if ((QPP_QUAD_PF & 2) && one && s == 0 && t + WG / 4 < end) l2_touch((const uint8_t *)(descs + t + WG / 4));
             bool has = real && !(d.flags & QPP_PKT_SKIP);
             if (one && has && d.key_idx != single) {  // not the live key: refused, untouched
                 if (status && s == 0) status[pi] = QPP_INTERNAL_ERROR;

@@ -237,7 +237,7 @@ __device__ __forceinline__ qpp_pkt reload_desc(const qpp_pkt *descs, uint32_t i)
 
 // One packet per quad; s = lane % 4.  has = false: the quad has no packet (its lanes only keep the wave's loop shape).
 // Addresses are 32-bit offsets into the arena (SGPR base + VGPR offset).
-template <int NR, bool SEAL>
+template <int NR, bool SEAL, bool HEAD>
 __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> &gh, const DevKey *__restrict__ key,
                                             bool has, const qpp_pkt &d,
                                             const qpp_pkt *__restrict__ descs, uint32_t pkt_index,
@@ -294,7 +294,9 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
     auto interior = [&](int g) { return g >= 1 && kQSG * g + kQSG - 1 <= min_full; };  // every slot a whole payload block
     // group 0 when slots 1..15 are whole payload blocks in every packet of the wave: the interior path, with slot 0
     // (J0: keystream only, neither stored nor hashed) masked per lane
-    const bool head_ok = kQSG - 1 <= min_full;  // uniform
+    // (HEAD: AES-128-only kernels; in the AES-256 and both-sizes instances the extra path cost 10-14 VGPRs of spills
+    // and 3 % of AES-256's seal time, round 6)
+    const bool head_ok = HEAD && kQSG - 1 <= min_full;  // uniform
     // counter blocks per lane the last group needs (uniform): the longest packet's slots past 16 (G - 1)
     const int tail_slots = (int)wave_max(has ? (uint32_t)max(0, m + 1 - kQSG * (G - 1)) : 0u);
     // length block: be64(aad bits) || be64(payload bits)
@@ -533,7 +535,7 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
 
 // One workgroup per CU (grid = CUs) over an equal slice of the key-sorted packets (plan meta,
 // same single-key mode), 256 packets per pass.
-template <bool SEAL, int NR, int WG = kQuadWG<NR>>
+template <bool SEAL, int NR, int WG = kQuadWG<NR>, bool HEAD = false>
 __device__ __forceinline__ void quad_slices(const DevKey *__restrict__ keys, const qpp_pkt *__restrict__ descs,
                                             const uint32_t *__restrict__ perm, const WorkItem *__restrict__ work,
                                             const uint32_t *__restrict__ meta, uint8_t *__restrict__ arena,
@@ -594,7 +596,7 @@ __device__ __forceinline__ void quad_slices(const DevKey *__restrict__ keys, con
                 if (status && s == 0) status[pi] = QPP_INTERNAL_ERROR;
                 has = false;
             }
-            quad_packet<NR, SEAL>(aes, gh, key, has, d, descs, pi, arena, masks, status, flags, s);
+            quad_packet<NR, SEAL, HEAD>(aes, gh, key, has, d, descs, pi, arena, masks, status, flags, s);
         }
         lo = end;
     }
@@ -619,7 +621,7 @@ __global__ __launch_bounds__(kQuadWG<NR>) void aes_gcm_quad_kernel(const DevKey 
                                                               int8_t *status, uint32_t flags, uint32_t single,
                                                               uint32_t n_single, const PowTables pow) {
     constexpr int WG = kQuadWG<NR>;
-    if constexpr (NR != 14) quad_slices<SEAL, 10, WG>(keys, descs, perm, work, meta, arena, masks, status, flags, single, n_single, pow);
+    if constexpr (NR != 14) quad_slices<SEAL, 10, WG, NR == 10>(keys, descs, perm, work, meta, arena, masks, status, flags, single, n_single, pow);
     if constexpr (NR != 10) quad_slices<SEAL, 14, WG>(keys, descs, perm, work, meta, arena, masks, status, flags, single, n_single, pow);
 }
 

@@ -365,8 +365,8 @@ int ctx_sync(qpp_ctx *ctx) {
 
 // (the plan's stream has been synchronized)
 void free_plan(qpp_ctx *ctx, PlanBuffers &p) {
-    for (void *b : {(void *)p.counts, (void *)p.cursor, (void *)p.istart, (void *)p.perm, (void *)p.work,
-                    (void *)p.n_work})
+    for (void *b : {(void *)p.counts, (void *)p.cursor, (void *)p.istart, (void *)p.perm, (void *)p.kq,
+                    (void *)p.work, (void *)p.n_work})
         dfree(ctx, b);
     p = PlanBuffers{};
 }
@@ -544,6 +544,7 @@ int ensure_plan(qpp_ctx *ctx, StreamState *st, uint32_t n) {
     HIP_TRY(ctx, dmalloc(ctx, &p.cursor, sizeof(uint32_t) * kcap));
     HIP_TRY(ctx, dmalloc(ctx, &p.istart, sizeof(uint32_t) * 2 * (kcap + 1)));
     HIP_TRY(ctx, dmalloc(ctx, &p.perm, sizeof(uint32_t) * std::max<uint32_t>(ncap, 1)));
+    HIP_TRY(ctx, dmalloc(ctx, &p.kq, sizeof(uint32_t) * std::max<uint32_t>(ncap, 1)));
     HIP_TRY(ctx, dmalloc(ctx, &p.work, sizeof(WorkItem) * (plan_max_work(ncap, kcap, kMinPacketsPerItem) + 1)));
     HIP_TRY(ctx, dmalloc(ctx, &p.n_work, 8 * sizeof(uint32_t)));
     HIP_TRY(ctx, hipMemsetAsync(p.n_work, 0, 8 * sizeof(uint32_t), st->stream));  // (meta[6] is a running count)
@@ -898,7 +899,10 @@ int run_one(const qpp_key *k, bool seal, uint64_t pn, const uint8_t *header, siz
     meta[3] = nr == 10 ? 0 : 1;
     *(WorkItem *)(h + 52) = WorkItem{k->slot, 0, 1, nr};
     h[72] = (uint8_t)QPP_INTERNAL_ERROR;  // overwritten by the kernel
-    const PlanBuffers pb{nullptr, nullptr, nullptr, (uint32_t *)(v + 32), (WorkItem *)(v + 52), (uint32_t *)(v + 36)};
+    PlanBuffers pb{};
+    pb.perm = (uint32_t *)(v + 32);
+    pb.work = (WorkItem *)(v + 52);
+    pb.n_work = (uint32_t *)(v + 36);
     hipStream_t s = ctx->stream;
     const qpp_pkt *vd = (const qpp_pkt *)v;
     int8_t *vst = (int8_t *)(v + 72);

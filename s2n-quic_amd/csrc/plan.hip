@@ -27,7 +27,8 @@ __device__ __forceinline__ bool is_aes(const DevKey *keys, uint32_t k) {
 // key_cap <= kMaxPlanKeys: bins in LDS.  Larger key tables use global atomics directly.
 __global__ __launch_bounds__(kPlanBlock) void plan_hist(const DevKey *__restrict__ keys, uint32_t key_cap,
                                                        const qpp_pkt *__restrict__ descs, uint32_t n,
-                                                       uint32_t *__restrict__ counts, uint32_t *__restrict__ meta) {
+                                                       uint32_t *__restrict__ counts, uint32_t *__restrict__ kq,
+                                                       uint32_t *__restrict__ meta) {
     __shared__ uint32_t bins[kMaxPlanKeys];
     __shared__ uint32_t others;
     const bool local = key_cap <= (uint32_t)kMaxPlanKeys;
@@ -42,6 +43,7 @@ __global__ __launch_bounds__(kPlanBlock) void plan_hist(const DevKey *__restrict
         if (pi < n) {
             k = descs[pi].key_idx;
             if (k >= key_cap || !is_aes(keys, k)) k = ~0u;
+            kq[pi] = k;  // (plan_scatter reads this instead of the descriptor and the key record again)
         }
         // a run of same-key packets fills whole waves (one connection's burst; a single-key batch): one atomic per
         // wave instead of 64 serialised same-address LDS atomics
@@ -77,47 +79,85 @@ __global__ __launch_bounds__(kPlanBlock) void plan_scan(const DevKey *__restrict
                                                        uint32_t *__restrict__ counts, uint32_t *__restrict__ cursor,
                                                        uint32_t *__restrict__ istart_g, WorkItem *__restrict__ work,
                                                        uint32_t *__restrict__ meta, uint32_t per) {
-    __shared__ uint32_t sc[kPlanBlock], si[kPlanBlock];
+    // Round 6: one pass over the keys, kpt consecutive keys per thread, the four sums (packets and items of each
+    // class) scanned together -- wave scans by shuffles and one 16-entry scan of the wave totals -- instead of a
+    // Hillis-Steele scan per 1024 keys and class (20 barriers each): 35 -> a few us for 4096 keys (plan_small's scan)
     __shared__ uint32_t istart_l[2 * (kMaxPlanKeys + 1)];
-    __shared__ uint32_t carry_c, carry_i, cls_i[2], cls_c[2];
+    __shared__ uint32_t wt[4][kPlanBlock / 64];
     const bool local = key_cap <= (uint32_t)kMaxPlanKeys;
     uint32_t *istart = local ? istart_l : istart_g;  // [2][key_cap + 1]: per class, non-decreasing in k
-    if (threadIdx.x == 0) { carry_c = 0; carry_i = 0; }
-    __syncthreads();
-    for (uint32_t cls = 0; cls < 2; cls++) {
-        uint32_t *ist = istart + cls * (key_cap + 1);
-        for (uint32_t base = 0; base < key_cap; base += kPlanBlock) {
-            const uint32_t k = base + threadIdx.x;
-            uint32_t c = k < key_cap ? counts[k] : 0;
-            if (c && (keys[k].nr == 14) != (cls == 1)) c = 0;  // the other class's key
-            const uint32_t items = c ? (c - 1) / per + 1 : 0;
-            sc[threadIdx.x] = c;
-            si[threadIdx.x] = items;
-            __syncthreads();
-            for (uint32_t off = 1; off < kPlanBlock; off <<= 1) {  // Hillis-Steele inclusive scan
-                uint32_t a = threadIdx.x >= off ? sc[threadIdx.x - off] : 0;
-                uint32_t b = threadIdx.x >= off ? si[threadIdx.x - off] : 0;
-                __syncthreads();
-                sc[threadIdx.x] += a;
-                si[threadIdx.x] += b;
-                __syncthreads();
-            }
-            if (k < key_cap) {
-                if (c) cursor[k] = carry_c + sc[threadIdx.x] - c;
-                ist[k] = carry_i + si[threadIdx.x] - items;
-            }
-            __syncthreads();
-            if (threadIdx.x == kPlanBlock - 1) { carry_c += sc[threadIdx.x]; carry_i += si[threadIdx.x]; }
-            __syncthreads();
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint32_t kpt = (key_cap + kPlanBlock - 1) / kPlanBlock, k0 = tid * kpt;
+    auto cls_of = [&](uint32_t k) { return keys[k].nr == 14 ? 1u : 0u; };
+    // this thread's counts and classes, loaded once (all loads issued together; up to kMaxPlanKeys keys)
+    constexpr uint32_t kKpt = kMaxPlanKeys / kPlanBlock;
+    uint32_t cc[kKpt], cl[kKpt];
+#pragma unroll
+    for (uint32_t j = 0; j < kKpt; j++) {
+        const uint32_t k = k0 + j;
+        cc[j] = j < kpt && k < key_cap ? counts[k] : 0u;
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < kKpt; j++) cl[j] = cc[j] ? cls_of(k0 + j) : 0u;
+    uint32_t v[4] = {0, 0, 0, 0};  // packets of class 0, 1; items of class 0, 1 (this thread's keys)
+    for (uint32_t j = 0; j < kpt; j++) {
+        const uint32_t k = k0 + j;
+        if (k >= key_cap) break;
+        const uint32_t c = j < kKpt ? cc[j] : counts[k];
+        if (!c) continue;
+        const uint32_t cls = j < kKpt ? cl[j] : cls_of(k);
+        v[cls] += c;
+        v[2 + cls] += (c - 1) / per + 1;
+    }
+    uint32_t sc[4];  // inclusive wave scans
+#pragma unroll
+    for (int i = 0; i < 4; i++) sc[i] = v[i];
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const uint32_t a = (uint32_t)__shfl_up((int)sc[i], o, 64);
+            if (lane >= (uint32_t)o) sc[i] += a;
         }
-        if (threadIdx.x == 0) { ist[key_cap] = carry_i; cls_i[cls] = carry_i; cls_c[cls] = carry_c; }
-        __syncthreads();
     }
-    const uint32_t total = cls_i[1], i10 = cls_i[0];
-    if (threadIdx.x == 0) {
-        meta[0] = total; meta[1] = i10; meta[2] = cls_c[0]; meta[3] = cls_c[1] - cls_c[0];
-        meta[4] = meta[6]; meta[5] = cls_c[1]; meta[6] = 0; meta[7] = cls_c[1];
+    if (lane == 63) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) wt[i][wave] = sc[i];
     }
+    __syncthreads();
+    uint32_t pre[4], tot[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        pre[i] = sc[i] - v[i];
+        tot[i] = 0;
+        for (uint32_t w = 0; w < kPlanBlock / 64; w++) {
+            if (w < wave) pre[i] += wt[i][w];
+            tot[i] += wt[i][w];
+        }
+    }
+    // class-major: class 0's packets and items from 0, class 1's behind them
+    uint32_t pc[2] = {pre[0], tot[0] + pre[1]}, pw[2] = {pre[2], tot[2] + pre[3]};
+    uint32_t *ist0 = istart, *ist1 = istart + key_cap + 1;
+    for (uint32_t j = 0; j < kpt; j++) {
+        const uint32_t k = k0 + j;
+        if (k >= key_cap) break;
+        const uint32_t c = j < kKpt ? cc[j] : counts[k];
+        ist0[k] = pw[0];
+        ist1[k] = pw[1];
+        if (!c) continue;
+        const uint32_t cls = j < kKpt ? cl[j] : cls_of(k);
+        cursor[k] = pc[cls];
+        pc[cls] += c;
+        pw[cls] += (c - 1) / per + 1;
+    }
+    const uint32_t total = tot[2] + tot[3], i10 = tot[2];
+    if (tid == 0) {
+        ist0[key_cap] = i10;
+        ist1[key_cap] = total;
+        meta[0] = total; meta[1] = i10; meta[2] = tot[0]; meta[3] = tot[1];
+        meta[4] = meta[6]; meta[5] = tot[0] + tot[1]; meta[6] = 0; meta[7] = tot[0] + tot[1];
+    }
+    __syncthreads();
     for (uint32_t w = threadIdx.x; w < total; w += kPlanBlock) {
         const uint32_t *ist = istart + (w >= i10 ? key_cap + 1 : 0);
         uint32_t lo = 0, hi = key_cap;  // largest k with ist[k] <= w (keys with no items share a start)
@@ -136,8 +176,7 @@ __global__ __launch_bounds__(kPlanBlock) void plan_scan(const DevKey *__restrict
     for (uint32_t k = threadIdx.x; k < key_cap; k += kPlanBlock) counts[k] = 0;
 }
 
-__global__ __launch_bounds__(kPlanBlock) void plan_scatter(const DevKey *__restrict__ keys, uint32_t key_cap,
-                                                          const qpp_pkt *__restrict__ descs, uint32_t n,
+__global__ __launch_bounds__(kPlanBlock) void plan_scatter(uint32_t key_cap, const uint32_t *__restrict__ kq, uint32_t n,
                                                           uint32_t *__restrict__ cursor, uint32_t *__restrict__ perm,
                                                           uint32_t *__restrict__ meta) {
     __shared__ uint32_t bins[kMaxPlanKeys];
@@ -152,12 +191,8 @@ __global__ __launch_bounds__(kPlanBlock) void plan_scatter(const DevKey *__restr
 #pragma unroll
     for (uint32_t j = 0; j < kPlanPerThread; j++) {
         const uint32_t pi = (blockIdx.x * kPlanPerThread + j) * blockDim.x + threadIdx.x;
-        uint32_t k = 0xffffffffu;
+        const uint32_t k = pi < n ? kq[pi] : 0xffffffffu;
         rank[j] = 0;
-        if (pi < n) {
-            k = descs[pi].key_idx;
-            if (k >= key_cap || !is_aes(keys, k)) k = 0xffffffffu;
-        }
         const uint32_t k0 = __builtin_amdgcn_readfirstlane(k);
         if (__all(k == k0)) {  // whole wave on one key (see plan_hist): one reservation of 64 consecutive ranks
             if (k0 != 0xffffffffu) {
@@ -316,10 +351,10 @@ hipError_t launch_plan(const DevKey *keys, uint32_t key_cap, const qpp_pkt *desc
         return hipGetLastError();
     }
     const dim3 grid((n + kPlanBlock * kPlanPerThread - 1) / (kPlanBlock * kPlanPerThread));
-    hipLaunchKernelGGL(plan_hist, grid, dim3(kPlanBlock), 0, s, keys, key_cap, descs, n, pb.counts, pb.n_work);
+    hipLaunchKernelGGL(plan_hist, grid, dim3(kPlanBlock), 0, s, keys, key_cap, descs, n, pb.counts, pb.kq, pb.n_work);
     hipLaunchKernelGGL(plan_scan, dim3(1), dim3(kPlanBlock), 0, s, keys, key_cap, pb.counts, pb.cursor, pb.istart, pb.work,
                        pb.n_work, per);
-    hipLaunchKernelGGL(plan_scatter, grid, dim3(kPlanBlock), 0, s, keys, key_cap, descs, n, pb.cursor, pb.perm, pb.n_work);
+    hipLaunchKernelGGL(plan_scatter, grid, dim3(kPlanBlock), 0, s, key_cap, pb.kq, n, pb.cursor, pb.perm, pb.n_work);
     return hipGetLastError();
 }
 

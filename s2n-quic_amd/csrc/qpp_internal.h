@@ -127,6 +127,7 @@ struct PlanBuffers {
     uint32_t *cursor;   // [key_cap] scatter cursors
     uint32_t *istart;   // [2][key_cap + 1] first work item per key and AES size (used when key_cap > kMaxPlanKeys)
     uint32_t *perm;     // [n_cap] packet indices grouped by key
+    uint32_t *kq;       // [n_cap] each packet's planned key (0xffffffff: not a live AES key), plan_hist -> plan_scatter
     WorkItem *work;     // [n_cap / kMinPacketsPerItem + key_cap + 1]
     uint32_t *n_work;   // [8] plan meta: work items, AES-128 items, AES-128 packets, AES-256 packets, other packets
                         // (ChaCha20, refused) and their first perm index, and plan-internal [6] count and [7] cursor

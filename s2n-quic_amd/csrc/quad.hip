@@ -82,19 +82,7 @@ constexpr int kQuadWG = NR == 14 ? QPP_QUAD_WG256 : QPP_QUAD_WG;
                         // stores, 4 no header protection, 8 no final H^e product (the quad sums the chains as they are); DESIGN §5
                         // round 6 has what each cost
 #endif
-#ifndef QPP_QUAD_PF
-#define QPP_QUAD_PF 0  // L2 touches: 1 the next group's payload lines at a group's start, 2 the next packet's descriptor
-#endif
 constexpr int kQNB = QPP_QUAD_NB, kQSG = 4 * kQNB;
-// An L2 touch: a 4-byte LDS-DMA load (no VGPR destination), so that a later load of the same line hits the L2 instead
-// of HBM.  A wave's DMA writes 4 bytes per lane at its LDS base + 4 lane: the two half-waves each land their 128 bytes
-// in the unused upper half of AES table row 0 (AesQ4 uses the lower 128 B of every 256-B row), which nothing reads.
-__device__ __forceinline__ void l2_touch(const uint8_t *p) {
-    typedef __attribute__((address_space(3))) void lds_void;
-    const void *g = (const void *)((uintptr_t)p & ~(uintptr_t)3);
-    if (__lane_id() < 32) __builtin_amdgcn_global_load_lds(g, (lds_void *)(size_t)(kLdsAes + 128u), 4, 0, 0);
-    else __builtin_amdgcn_global_load_lds(g, (lds_void *)(size_t)(kLdsAes), 4, 0, 0);
-}
 static_assert(kQNB >= 2 && kQNB <= 4, "group size");
 
 
@@ -340,17 +328,11 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
     auto group = [&](auto nbc, int g) __attribute__((always_inline)) {
         constexpr int NBG = decltype(nbc)::value;
         const bool head = NBG == kQNB && g == 0 && head_ok;  // uniform
-        if ((QPP_QUAD_PF & 1) && g + 1 < G) {
-            // group g + 1's 256 bytes [A, A + 256) span at most 3 lines: lanes touch A, A + 64, A + 128, A + 255
-            // (clamped to the packet's tag)
-            const uint32_t A = pay + 16u * (uint32_t)(kQSG * (g + 1) - 1), lim = pay + len + 15u;
-            const uint32_t x = A + (s == 3 ? 255u : 64u * s);
-            l2_touch(at(x < lim ? x : lim));
-        }
         const bool inner = NBG == kQNB && interior(g);  // uniform
         const RkPtr rkp = round_keys();
         const int t0 = kQSG * g + (int)s;
         uint4 ks[NBG];
+        uint4 in[NBG];
         const uint32_t c0 = (uint32_t)t0 + 1u;
         // The nonce words are laundered where the loop uses them (a new page; the straddling group): left alone, the
         // compiler hoisted the page build's first-round lookups addresses out of the loop as loop invariants and
@@ -376,8 +358,9 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
             });
         }
         // payload after the keystream (loading the next interior group's payload while this group hashes measured 8 %
-        // slower: 1.248 vs 1.152 ms seal, 8 VGPRs spilled, profiles/r04h_ab)
-        uint4 in[NBG];
+        // slower: 1.248 vs 1.152 ms seal, 8 VGPRs spilled, profiles/r04h_ab; loading this group's before the keystream
+        // 4 % slower at 3 waves/SIMD (14 VGPRs spilled) and 7.5 % slower at 2 waves/SIMD (256 VGPRs, no spill); an L2
+        // touch of the next group's lines 3.7 % slower: round 6, profiles/r06/head)
         if (SEAL && g == 0 && hp_at0 && (flags & QPP_HP_APPLY) && s == 0) hb = hdr_load(at(pay - aad_len), aad_len - pn_len);
         if (head) {
             // slot 0 (lane 0, k = 0) reads the payload's first block instead of the bytes before it (never used)
@@ -590,7 +573,6 @@ __device__ __forceinline__ void quad_slices(const DevKey *__restrict__ keys, con
             const bool real = t < end;
             const uint32_t pi = one ? (real ? t : lo) : perm[real ? t : lo];
             const qpp_pkt d = descs[pi];  // (any valid descriptor for quads without a packet)
-            if ((QPP_QUAD_PF & 2) && one && s == 0 && t + WG / 4 < end) l2_touch((const uint8_t *)(descs + t + WG / 4));
             bool has = real && !(d.flags & QPP_PKT_SKIP);
             if (one && has && d.key_idx != single) {  // not the live key: refused, untouched
                 if (status && s == 0) status[pi] = QPP_INTERNAL_ERROR;

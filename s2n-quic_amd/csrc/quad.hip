@@ -75,7 +75,7 @@ constexpr int kQuadWG = NR == 14 ? QPP_QUAD_WG256 : QPP_QUAD_WG;
 #define QPP_QUAD_NB 4
 #endif
 #ifndef QPP_QUAD_TRACE
-#define QPP_QUAD_TRACE 0  // 1: workgroups 0 and grid/2 print their table-build and total cycles (s_memtime)
+#define QPP_QUAD_TRACE 0  // 1: workgroups 0 and grid/2 print their table-build and total cycles (s_memtime); 2: all
 #endif
 #ifndef QPP_QUAD_ABL
 #define QPP_QUAD_ABL 0  // ablation bits for timing A/Bs only (wrong bytes): 1 no interior payload loads, 2 no interior
@@ -547,7 +547,7 @@ __device__ __forceinline__ void quad_slices(const DevKey *__restrict__ keys, con
     const uint32_t s = threadIdx.x & 3u, q = threadIdx.x >> 2;
     build_qaes();  // once: the segments' table builds from a pow slot leave them alone (the first barrier below orders it)
 #if QPP_QUAD_TRACE
-    uint64_t t_beg = __builtin_amdgcn_s_memtime(), t_tab = 0;
+    uint64_t t_beg = __builtin_amdgcn_s_memtime(), t_tab = 0, r_beg = __builtin_amdgcn_s_memrealtime();
     uint32_t n_seg = 0;
 #endif
     for (; lo < hi; i++) {  // key segments of the slice
@@ -584,9 +584,10 @@ __device__ __forceinline__ void quad_slices(const DevKey *__restrict__ keys, con
     }
 #if QPP_QUAD_TRACE
     __syncthreads();
-    if (threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x / 2))
-        printf("quad wg %u seal %d nr %d: %u segments, tables %llu of %llu cycles\n", blockIdx.x, (int)SEAL, NR, n_seg,
-               (unsigned long long)t_tab, (unsigned long long)(__builtin_amdgcn_s_memtime() - t_beg));
+    if (threadIdx.x == 0 && (QPP_QUAD_TRACE == 2 || blockIdx.x == 0 || blockIdx.x == gridDim.x / 2))
+        printf("quad wg %u seal %d nr %d: %u segments, tables %llu of %llu cycles, real %llu-%llu\n", blockIdx.x,
+               (int)SEAL, NR, n_seg, (unsigned long long)t_tab, (unsigned long long)(__builtin_amdgcn_s_memtime() - t_beg),
+               (unsigned long long)r_beg, (unsigned long long)__builtin_amdgcn_s_memrealtime());
 #endif
 }
 

@@ -564,9 +564,19 @@ def rx(args, ctx, keys, descs, arena, d_desc, d_mask, d_status, flags, rank, wor
         }
         suite = SUITES[args.suite]
         achieved = n * rx_bytes_per_packet(pt, aad) / (t / 1e3) / 1e9
+        traffic = None  # HBM bytes per receive launch from the committed PMC profile (tools/traffic.py rx: key)
+        try:
+            tr = json.load(open(os.path.join(ROOT, "profiles", "traffic.json"))).get(f"rx:{args.suite}/{pt}/{args.keys}")
+            if tr and n == 1 << 20 and aad == 21:
+                traffic = {"bytes": tr["traffic_bytes"], "per_alg": round(tr["traffic_bytes"] / (n * rx_bytes_per_packet(pt, aad)), 3),
+                           "read_per_alg": tr["read_per_alg"], "write_per_alg": tr["write_per_alg"],
+                           "source": "profiles/traffic.json: " + tr["source"]}
+        except (OSError, ValueError, KeyError):
+            traffic = None
         out["roofline"] = {
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic and traffic["bytes"],
+            "traffic_detail": traffic,
             "kernel": "aes_gcm_quad_rx_kernel (one launch: unprotect, group-by key, open)" if suite in (1, 2) else
                       "chacha_kernel<open, RX>" if suite == 3 else "aes_gcm_quad_rx_kernel + chacha_kernel<open, RX>",
             "bytes_per_packet": rx_bytes_per_packet(pt, aad),

@@ -106,7 +106,7 @@ def test_limits_and_lengths(ctx):
 # ------------------------------------------------------------------ golden fixtures through the per-packet API
 
 @pytest.mark.parametrize("name,suite", [("aead_aes128gcm.json", 1), ("aead_aes256gcm.json", 2),
-                                        ("aead_chacha20poly1305.json", 3)])
+                                        ("aead_chacha20poly1305.json", 3), ("gcm_spec_aes256.json", 2)])
 def test_aead_fixtures(ctx, name, suite, path):
     for c in load_golden(name)["cases"]:
         k = ctx.raw_key(suite, H(c["key"]), H(c["iv"]), bytes(qpp.KEY_LEN[suite]))
@@ -117,6 +117,43 @@ def test_aead_fixtures(ctx, name, suite, path):
         bad[len(bad) // 2] ^= 0x80
         with pytest.raises(qpp.DecryptError):
             k.decrypt(c["pn"], H(c["aad"]), bytes(bad))
+        k.free()
+
+
+def test_gcm_spec_aes256_batches(ctx, path):
+    """The GCM specification's AES-256 test cases 13-16 (tests/golden/gcm_spec_aes256.json: the published vectors, the
+    reference holds none for AES-256) through the batch kernels: 512 copies of each case in one 2048-packet batch over
+    the two raw keys they use, sealed and opened on every AES kernel path, every packet's ciphertext and tag compared."""
+    cases = load_golden("gcm_spec_aes256.json")["cases"]
+    keys = {}
+    for c in cases:
+        if (c["key"], c["iv"]) not in keys:
+            keys[(c["key"], c["iv"])] = ctx.raw_key(2, H(c["key"]), H(c["iv"]), bytes(32))
+    reps, n = 512, 512 * len(cases)
+    sizes = [len(H(c["aad"])) + len(H(c["pt"])) + 16 for c in cases]
+    stride = (max(sizes) + 15) // 16 * 16
+    descs = np.zeros(n, dtype=qpp.PKT_DTYPE)
+    arena = np.zeros(n * stride, dtype=np.uint8)
+    want = arena.copy()
+    for i in range(n):
+        c = cases[i % len(cases)]
+        aad, pt = H(c["aad"]), H(c["pt"])
+        o = i * stride
+        descs[i] = (0, keys[(c["key"], c["iv"])].slot, o, len(aad), len(pt), 1, 0, 0)
+        arena[o:o + len(aad) + len(pt)] = np.frombuffer(aad + pt, np.uint8)
+        want[o:o + len(aad) + len(pt) + 16] = np.frombuffer(aad + H(c["ct"] + c["tag"]), np.uint8)
+    got, _, st = _run_seal(ctx, descs, arena, 0)
+    assert (st == 0).all()
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, f"first mismatch at arena byte {bad[:8]}"
+    opened, st = _run_open(ctx, descs, want)
+    plain = want.copy()  # the open leaves the tag in place and the plaintext where the ciphertext was
+    for i in range(n):
+        c = cases[i % len(cases)]
+        a, p = len(H(c["aad"])), len(H(c["pt"]))
+        plain[i * stride + a:i * stride + a + p] = arena[i * stride + a:i * stride + a + p]
+    assert (st == 0).all() and (opened == plain).all()
+    for k in keys.values():
         k.free()
 
 

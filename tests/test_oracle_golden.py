@@ -130,7 +130,7 @@ def test_a5_key_update(rfc):
 
 
 @pytest.mark.parametrize("name,suite", [("aead_aes128gcm.json", 1), ("aead_aes256gcm.json", 2),
-                                        ("aead_chacha20poly1305.json", 3)])
+                                        ("aead_chacha20poly1305.json", 3), ("gcm_spec_aes256.json", 2)])
 def test_aead_fixtures(name, suite):
     fx = load_golden(name)
     assert fx["suite"] == suite

@@ -282,8 +282,9 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
     auto interior = [&](int g) { return g >= 1 && kQSG * g + kQSG - 1 <= min_full; };  // every slot a whole payload block
     // group 0 when slots 1..15 are whole payload blocks in every packet of the wave: the interior path, with slot 0
     // (J0: keystream only, neither stored nor hashed) masked per lane
-    // (HEAD: the AES-128-only seal kernel; in the AES-256 and both-sizes instances the extra path cost 10-14 VGPRs of
-    // spills and 3 % of AES-256's seal time, in the open 4 VGPRs of spills for no gain: round 6)
+    // (HEAD: the AES-128-only kernels; in the AES-256 and both-sizes instances the extra path cost 10-14 VGPRs of
+    // spills and 3 % of AES-256's seal time.  The AES-128 open spills 4 VGPRs with it -- one reload per packet, none in
+    // the group loop -- and still runs 0.6 % faster than without it, 6 alternating rounds: round 6)
     const bool head_ok = HEAD && kQSG - 1 <= min_full;  // uniform
     // counter blocks per lane the last group needs (uniform): the longest packet's slots past 16 (G - 1)
     const int tail_slots = (int)wave_max(has ? (uint32_t)max(0, m + 1 - kQSG * (G - 1)) : 0u);
@@ -604,7 +605,7 @@ __global__ __launch_bounds__(kQuadWG<NR>) void aes_gcm_quad_kernel(const DevKey 
                                                               int8_t *status, uint32_t flags, uint32_t single,
                                                               uint32_t n_single, const PowTables pow) {
     constexpr int WG = kQuadWG<NR>;
-    if constexpr (NR != 14) quad_slices<SEAL, 10, WG, SEAL && NR == 10>(keys, descs, perm, work, meta, arena, masks, status, flags, single, n_single, pow);
+    if constexpr (NR != 14) quad_slices<SEAL, 10, WG, NR == 10>(keys, descs, perm, work, meta, arena, masks, status, flags, single, n_single, pow);
     if constexpr (NR != 10) quad_slices<SEAL, 14, WG>(keys, descs, perm, work, meta, arena, masks, status, flags, single, n_single, pow);
 }
 

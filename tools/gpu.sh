@@ -49,7 +49,7 @@ for step in "$@"; do
     prof)
       bash tools/profile.sh ${tag}_prof $args || exit 1
       python tools/summarize_prof.py gpurun_out/${tag}_prof > $o/prof_summary.txt && head -14 $o/prof_summary.txt || exit 1
-      [ -z "$args" ] && { python tools/traffic.py gpurun_out/${tag}_prof aes128gcm/1200/1 1048576 $o/traffic.json || exit 1; } ;;
+      if [ -z "$args" ]; then python tools/traffic.py gpurun_out/${tag}_prof aes128gcm/1200/1 1048576 $o/traffic.json || exit 1; fi ;;
     rxtrace)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $o/rxtrace -o trace -- python3 bench.py --mode rx --keys 64 --steps 4 --warmup 1 --no-cpu > $o/rxtrace.log 2>&1
       rc=$?; echo "rx trace exit $rc" | tee $o/rxtrace.rc; [ $rc -eq 0 ] || exit 1 ;;

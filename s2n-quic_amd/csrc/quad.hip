@@ -77,6 +77,10 @@ constexpr int kQuadWG = NR == 14 ? QPP_QUAD_WG256 : QPP_QUAD_WG;
 #ifndef QPP_QUAD_TRACE
 #define QPP_QUAD_TRACE 0  // 1: workgroups 0 and grid/2 print their table-build and total cycles (s_memtime); 2: all
 #endif
+#ifndef QPP_QUAD_EK0C
+#define QPP_QUAD_EK0C 1  // E_K(J0) kept as one column per lane from group 0's keystream (0: seal keeps the block in every
+                         // lane, open recomputes it on the quad at the end)
+#endif
 #ifndef QPP_QUAD_ABL
 #define QPP_QUAD_ABL 0  // ablation bits for timing A/Bs only (wrong bytes): 1 no interior payload loads, 2 no interior
                         // stores, 4 no header protection, 8 no final H^e product (the quad sums the chains as they are); DESIGN §5
@@ -187,6 +191,7 @@ __device__ __forceinline__ uint4 qperm(uint4 v) {
 }
 constexpr int kQuadSwap1 = 0xb1;   // [1, 0, 3, 2]
 constexpr int kQuadSwap2 = 0x4e;   // [2, 3, 0, 1]
+constexpr int kQuadBcast0 = 0x00;  // [0, 0, 0, 0]
 constexpr int kQuadBcast1 = 0x55;  // [1, 1, 1, 1]
 constexpr int kQuadBcast2 = 0xaa;  // [2, 2, 2, 2]
 
@@ -295,6 +300,7 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
     constexpr int HNR = NR == 10 ? 10 : 14;
     const bool want_hp = SEAL && (flags & (QPP_HP_MASK_OUT | QPP_HP_APPLY)) != 0;
     uint4 ek0 = make_uint4(0, 0, 0, 0);  // seal: E_K(J0) (slot 0: lane 0, group 0)
+    uint32_t ek0c = 0;                    // (QPP_QUAD_EK0C) column s of E_K(J0) in lane s
 
     bool hp_done = false;                // seal: header protection applied after group 0 (quad-uniform)
     // Header protection as soon as the sample exists: the sample (ciphertext bytes [4 - pn_len, 20 - pn_len),
@@ -388,7 +394,13 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
         if constexpr (SEAL) {
             // E_K(J0) (slot 0, lane 0) kept in a register until the tag is known (opening recomputes it on the quad at
             // the end instead)
-            if (g == 0) ek0 = ks[0];
+            if (g == 0 && !QPP_QUAD_EK0C) ek0 = ks[0];
+        }
+        if (QPP_QUAD_EK0C && g == 0) {
+            // slot 0 of group 0 is counter block 1 = J0 in lane 0: its column s to lane s (quad broadcasts of lane 0)
+            const uint32_t c0w = qperm<kQuadBcast0>(ks[0].x), c1w = qperm<kQuadBcast0>(ks[0].y),
+                           c2w = qperm<kQuadBcast0>(ks[0].z), c3w = qperm<kQuadBcast0>(ks[0].w);
+            ek0c = s == 0 ? c0w : s == 1 ? c1w : s == 2 ? c2w : c3w;
         }
         if (head) {
             const uint32_t b = pay + 16 * (uint32_t)(t0 - 1);
@@ -464,7 +476,12 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
     y = y ^ qperm<kQuadSwap2>(y);
 
     if constexpr (SEAL) {
-        if (has && s == 0) st16(at(pay + len), y ^ ek0);  // tag = GHASH ^ E_K(J0)
+        if (QPP_QUAD_EK0C) {  // tag = GHASH ^ E_K(J0), column s by lane s
+            const uint32_t t = (s == 0 ? y.x : s == 1 ? y.y : s == 2 ? y.z : y.w) ^ ek0c;
+            if (has) __builtin_memcpy(at(pay + len + 4 * s), &t, 4);
+        } else if (has && s == 0) {
+            st16(at(pay + len), y ^ ek0);
+        }
         const bool hp = !(QPP_QUAD_ABL & 4) && want_hp && has && pn_len >= 1 && pn_len <= 4 && len >= 4 - pn_len;
         if (hp && !hp_done) {  // short payloads: the sample runs into the tag
             // header-protection sample = ciphertext||tag bytes [4 - pn_len, 20 - pn_len) (payload.rs:151-169), column s
@@ -490,15 +507,18 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
     } else {
         // E_K(J0) on the quad (column s in lane s; J0 = nonce || be32(1)), compared column by column with the received
         // tag, the verdict OR-ed over the quad: all 16 bytes compared, no early exit
-        const qpp_pkt dt = reload_desc(descs, pkt_index);
-        const uint32_t j0 = s == 0 ? key->iv[0]
-                          : s == 1 ? key->iv[1] ^ bswap32((uint32_t)(dt.pn >> 32))
-                          : s == 2 ? key->iv[2] ^ bswap32((uint32_t)dt.pn)
-                                   : bswap32(1u);
-        uint32_t sl = s;
-        asm volatile("" : "+v"(sl));  // (left alone, the compiler kept &key->rk[s] in a VGPR pair across the packet loop
-                                      // of each key segment and spilled it: 4 VGPRs of scratch in every open instance)
-        const uint32_t ek0 = aes_quad<NR>(aes, key->rk, j0, sl);
+        uint32_t ek0 = ek0c;
+        if (!QPP_QUAD_EK0C) {
+            const qpp_pkt dt = reload_desc(descs, pkt_index);
+            const uint32_t j0 = s == 0 ? key->iv[0]
+                              : s == 1 ? key->iv[1] ^ bswap32((uint32_t)(dt.pn >> 32))
+                              : s == 2 ? key->iv[2] ^ bswap32((uint32_t)dt.pn)
+                                       : bswap32(1u);
+            uint32_t sl = s;
+            asm volatile("" : "+v"(sl));  // (left alone, the compiler kept &key->rk[s] in a VGPR pair across the packet
+                                          // loop of each key segment and spilled it: 4 VGPRs of scratch per open)
+            ek0 = aes_quad<NR>(aes, key->rk, j0, sl);
+        }
         uint32_t want;
         __builtin_memcpy(&want, at(pay + len + 4 * s), 4);
         const uint32_t ys = s == 0 ? y.x : s == 1 ? y.y : s == 2 ? y.z : y.w;

@@ -81,6 +81,9 @@ constexpr int kQuadWG = NR == 14 ? QPP_QUAD_WG256 : QPP_QUAD_WG;
 #define QPP_QUAD_EK0C 1  // E_K(J0) kept as one column per lane from group 0's keystream (0: seal keeps the block in every
                          // lane, open recomputes it on the quad at the end)
 #endif
+#ifndef QPP_QUAD_TAGEARLY
+#define QPP_QUAD_TAGEARLY 1  // open: the received tag loaded before the last group (0: after the final product)
+#endif
 #ifndef QPP_QUAD_ABL
 #define QPP_QUAD_ABL 0  // ablation bits for timing A/Bs only (wrong bytes): 1 no interior payload loads, 2 no interior
                         // stores, 4 no header protection, 8 no final H^e product (the quad sums the chains as they are); DESIGN §5
@@ -239,12 +242,37 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
     // loop state
     const uint32_t aad_len = d.aad_len, len = has ? d.pt_len : 0u, pay = d.off + aad_len;
     const uint32_t pn_len = SEAL ? (uint32_t)d.pn_len : 0u;  // (seal: header protection)
-    const uint32_t n0 = key->iv[0], n1 = key->iv[1] ^ bswap32((uint32_t)(d.pn >> 32)),  // Iv::nonce (iv.rs:27-39)
-                   n2 = key->iv[2] ^ bswap32((uint32_t)d.pn);
+    // Iv::nonce (iv.rs:27-39); the key's iv by scalar loads (a uniform pointer through the constant address space:
+    // as a vector load it waited behind every memory operation of the previous packet, once per packet)
+    // (not in the AES-256 seal: there the scalar iv and the AAD load moved behind the page build below measured 2.6 %
+    // slower, 6 alternating rounds; everywhere else 0.6-2.5 % faster, round 6)
+    constexpr bool kLatePro = !SEAL || NR == 10;
+    uint32_t iv0, iv1, iv2;
+    if constexpr (kLatePro) {
+        uint64_t iva = (uint64_t)key->iv;
+        asm volatile("" : "+s"(iva));
+        const __attribute__((address_space(4))) uint32_t *ivp = (const __attribute__((address_space(4))) uint32_t *)iva;
+        iv0 = ivp[0]; iv1 = ivp[1]; iv2 = ivp[2];
+    } else {
+        iv0 = key->iv[0]; iv1 = key->iv[1]; iv2 = key->iv[2];
+    }
+    const uint32_t n0 = iv0, n1 = iv1 ^ bswap32((uint32_t)(d.pn >> 32)), n2 = iv2 ^ bswap32((uint32_t)d.pn);
     const int nfull = (int)(len >> 4), rem = (int)(len & 15), m = nfull + (rem ? 1 : 0);
     const int a = has ? (int)((aad_len + 15) >> 4) : 0;
     auto at = [&](uint32_t off) { return arena + off; };
 
+    // Round keys: scalar loads where they are used (the key record stays in the scalar cache), through a pointer
+    // laundered per group so that no load is hoisted out of the group loop (held for the whole loop, 44 / 60 words
+    // exhausted the SGPRs and went to VGPRs); a group's keystream loads rounds 3..NR, the page build rounds 0..2
+    auto round_keys = [&]() {
+        uint64_t a = (uint64_t)key->rk;
+        asm volatile("" : "+s"(a));  // reloaded here, not hoisted into SGPRs for the whole loop
+        // Through the constant address space: a uniform load from a global pointer is a scalar load only when the
+        // compiler can prove no store of the kernel clobbers it, which the laundering hides -- the round keys were
+        // FLAT loads into 32-44 VGPRs (uniform values in vector registers, the register budget of the waves)
+        return (RkPtr)a;
+    };
+    QPage pg;
     // AAD blocks of this lane: virtual slots t = 1 - a .. 0, t = s (mod 4).  A lane's first AAD block starts its chain
     // (w = rot(x): no product of zero); a lane with no AAD block starts at w = 0 and its first data step multiplies zero
     // (one product more for those lanes, in exchange for no started-flag control flow in the group loop).  With the
@@ -261,26 +289,27 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
             return r < 16 ? keep_bytes(x, r) : x;
         };
         int t = (1 - a) + (((int)s - (1 - a)) & 3);
-        if (t <= 0) {
-            w = gh.rot(aad_block(t));
+        // the lane's first AAD block is loaded here and taken into the chain after the page build below, whose LDS
+        // work covers the load's round trip
+        // (loaded by every lane, a lane without an AAD block reading the packet's first bytes: a conditional load
+        // joins into a copy that waits for it; masked below, after the page build: a use here waits)
+        const bool has_aad = t <= 0;
+        const uint32_t i0 = (uint32_t)(t + a - 1), r0 = aad_len - 16 * i0;
+        if constexpr (!kLatePro) {
+            if (has_aad) {
+                w = gh.rot(aad_block(t));
+                t += 4;
+            }
+        }
+        const uint4 x0 = kLatePro ? ld16(at(d.off + (has_aad ? 16 * i0 : 0u))) : make_uint4(z0, z0, z0, z0);
+        pg.build(aes, round_keys(), n0, n1, n2, 0);
+        if (kLatePro && has_aad) {
+            w = gh.rot(r0 < 16 ? keep_bytes(x0, r0) : x0);
             t += 4;
         }
         for (; t <= 0; t += 4) w = gh.mulx(w, aad_block(t));
     }
 
-    // Round keys: scalar loads where they are used (the key record stays in the scalar cache), through a pointer
-    // laundered per group so that no load is hoisted out of the group loop (held for the whole loop, 44 / 60 words
-    // exhausted the SGPRs and went to VGPRs); a group's keystream loads rounds 3..NR, the page build rounds 0..2
-    auto round_keys = [&]() {
-        uint64_t a = (uint64_t)key->rk;
-        asm volatile("" : "+s"(a));  // reloaded here, not hoisted into SGPRs for the whole loop
-        // Through the constant address space: a uniform load from a global pointer is a scalar load only when the
-        // compiler can prove no store of the kernel clobbers it, which the laundering hides -- the round keys were
-        // FLAT loads into 32-44 VGPRs (uniform values in vector registers, the register budget of the waves)
-        return (RkPtr)a;
-    };
-    QPage pg;
-    pg.build(aes, round_keys(), n0, n1, n2, 0);
     const int ngroups = has ? (m + kQSG) / kQSG : 0;  // counter slots 0 (J0) .. m
     const int G = (int)wave_max((uint32_t)ngroups);
     const int min_full = (int)__builtin_amdgcn_readfirstlane(wave_min(has ? (uint32_t)nfull : 0u));
@@ -392,8 +421,7 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
 #pragma unroll
         for (int k = 0; k < NBG; k++) out[k] = in[k] ^ ks[k];
         if constexpr (SEAL) {
-            // E_K(J0) (slot 0, lane 0) kept in a register until the tag is known (opening recomputes it on the quad at
-            // the end instead)
+            // (QPP_QUAD_EK0C=0: E_K(J0), slot 0 of lane 0, kept whole in every lane until the tag is known)
             if (g == 0 && !QPP_QUAD_EK0C) ek0 = ks[0];
         }
         if (QPP_QUAD_EK0C && g == 0) {
@@ -451,6 +479,10 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
         if (SEAL && g == 0 && !(QPP_QUAD_ABL & 4)) hp_early(out[0]);
     };
     for (int g = 0; g + 1 < G; g++) group(std::integral_constant<int, kQNB>{}, g);
+    // open: the received tag's column s, loaded before the last group so that its round trip passes under that
+    // group's work (it was loaded after the final product, its latency exposed once per packet)
+    uint32_t want = 0;
+    if (!SEAL && QPP_QUAD_TAGEARLY) __builtin_memcpy(&want, at(pay + len + 4 * s), 4);
     if (G > 0) {  // the last group with as few counter blocks per lane as its longest packet needs
         // (small packets: a 300-B packet's second group needs 1 block per lane, not 3)
         if (tail_slots <= 4) group(std::integral_constant<int, 1>{}, G - 1);
@@ -505,8 +537,9 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
         if (!has || s != 0) return;
         if (status) status[pkt_index] = want_hp && !hp ? QPP_DECODE_ERROR : QPP_OK;
     } else {
-        // E_K(J0) on the quad (column s in lane s; J0 = nonce || be32(1)), compared column by column with the received
-        // tag, the verdict OR-ed over the quad: all 16 bytes compared, no early exit
+        // E_K(J0) column s in lane s (from group 0's keystream; QPP_QUAD_EK0C=0: recomputed on the quad here, J0 = nonce ||
+        // be32(1)), compared column by column with the received tag, the verdict OR-ed over the quad: all 16 bytes
+        // compared, no early exit
         uint32_t ek0 = ek0c;
         if (!QPP_QUAD_EK0C) {
             const qpp_pkt dt = reload_desc(descs, pkt_index);
@@ -519,8 +552,7 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
                                           // loop of each key segment and spilled it: 4 VGPRs of scratch per open)
             ek0 = aes_quad<NR>(aes, key->rk, j0, sl);
         }
-        uint32_t want;
-        __builtin_memcpy(&want, at(pay + len + 4 * s), 4);
+        if (!QPP_QUAD_TAGEARLY) __builtin_memcpy(&want, at(pay + len + 4 * s), 4);
         const uint32_t ys = s == 0 ? y.x : s == 1 ? y.y : s == 2 ? y.z : y.w;
         uint32_t diff = ys ^ ek0 ^ want;
         diff |= qperm<kQuadSwap1>(diff);

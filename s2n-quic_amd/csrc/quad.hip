@@ -576,7 +576,10 @@ __device__ __forceinline__ void quad_slices(const DevKey *__restrict__ keys, con
                                             const uint32_t *__restrict__ perm, const WorkItem *__restrict__ work,
                                             const uint32_t *__restrict__ meta, uint8_t *__restrict__ arena,
                                             uint8_t *masks, int8_t *status, uint32_t flags, uint32_t single,
-                                            uint32_t n_single, const PowTables pow) {
+                                            uint32_t n_single, const PowTables pow, uint32_t fix_lo = 0,
+                                            uint32_t fix_hi = 0) {
+    // fix_hi != 0 (with a single key): this workgroup alone takes descs [fix_lo, fix_hi) (the fused receive's local
+    // slices), not its share of the grid's split
     const bool one = single != 0xffffffffu;  // uniform
     uint32_t i_lo = 0, i_hi = 1, p0 = 0, n = n_single;
     if (!one) {
@@ -587,8 +590,8 @@ __device__ __forceinline__ void quad_slices(const DevKey *__restrict__ keys, con
         n = NR == 10 ? n10 : n14;
     }
     const uint32_t P = ((n + gridDim.x - 1) / gridDim.x + 15u) & ~15u;  // whole waves (16 packets) per slice
-    uint32_t lo = p0 + min(n, blockIdx.x * P);
-    const uint32_t hi = p0 + min(n, (blockIdx.x + 1) * P);
+    uint32_t lo = fix_hi ? fix_lo : p0 + min(n, blockIdx.x * P);
+    const uint32_t hi = fix_hi ? fix_hi : p0 + min(n, (blockIdx.x + 1) * P);
     if (lo >= hi) return;  // uniform
     uint32_t i = i_lo, j = i_hi;  // the item holding lo: largest i with work[i].begin <= lo
     while (!one && j - i > 1) {
@@ -668,11 +671,14 @@ __global__ __launch_bounds__(kQuadWG<NR>) void aes_gcm_quad_kernel(const DevKey 
 //   A. each workgroup unprotects its slice of rx[] (one lane per packet: rx_unprotect_one -- HP mask of any suite,
 //      first byte and PN unmasked in place, PN expanded, key chosen), writes descs_out[], and counts its packets per
 //      chosen key in LDS (the GHASH table area is free until phase D);
-//   B. workgroup 0 turns the global counts into each key's first perm index -- AES-128 keys first, then AES-256, then
-//      ChaCha20 -- and one work item per AES key;
+//   B. the last workgroup past A turns the global counts into each key's first perm index -- AES-128 keys first, then
+//      AES-256, then ChaCha20 -- and one work item per AES key;
 //   C. each workgroup reserves a block per key it saw (one atomic per key) and scatters its packets into perm[];
 //   D. the quad open over the key-sorted AES-128 packets, then the AES-256 ones, exactly as aes_gcm_quad_kernel runs a
 //      planned batch (both round counts in one launch: the segment's NR is a template instance, the tables per key).
+// A local slice (all its packets bound for the open under one AES key) skips B-C: its workgroup opens it in place right
+// after A, counted in no plan, then takes its share of D.  A batch of one key is all local slices: no workgroup waits
+// for another (round 6: the barriers and phases B-C were 60-130 us of a 1.35 ms 1 Mi-packet receive).
 // The ChaCha20-Poly1305 packets (perm[scratch[3], + scratch[2])) are opened by chacha_kernel in selection mode, launched
 // right behind on the same stream (no host round trip).  It replaces unprotect_kernel + the three plan launches + the
 // open launches (tests/test_gpu_rx_fused.py: bit-exact against that path and the oracle).  A barrier that does not
@@ -688,16 +694,32 @@ constexpr uint32_t kRxHistMax = 16384;    // LDS bins [0, 64 KiB): keys per work
 constexpr uint64_t kRxBarrierTicks = 100000000ull;  // 1 s of s_memrealtime (100 MHz)
 constexpr int8_t kRxOpen = 0x7f;  // status of a packet bound for the open phase (never a final status)
 
-// scratch (device, words): [0] barrier count, [1] failed, [2] ChaCha packets, [3] their first perm index |
-// counts[key_cap] @16 | cursor[key_cap] | meta[4] | work[]  (the first 16 + 2 key_cap words are zeroed before each launch)
-__device__ bool rx_grid_sync(uint32_t *scratch, uint32_t target) {
+// scratch (device, words): [0] workgroups past phase A, [1] failed, [2] ChaCha packets, [3] their first perm index,
+// [4] phase B done, [5] workgroups past phase C | counts[key_cap] @16 | cursor[key_cap] | meta[4] | work[]  (the first
+// 16 + 2 key_cap words are zeroed before each launch)
+constexpr uint32_t kRxLocal = kRxCtl + 8;  // LDS: the slice's one key (0xffffffff: none) and its class, after phase A
+
+// a workgroup's arrival at a counter (every thread calls; its global writes so far are released with it): the count
+// before it, acquired (the last arrival at [0] sees every other workgroup's phase-A counts)
+__device__ uint32_t rx_arrive(uint32_t *ctr) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        const uint32_t old = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        lds_st32(kRxCtl, old);
+    }
+    __syncthreads();
+    return lds_ld32(kRxCtl);
+}
+
+// wait until *ctr >= target (every thread calls); false: a barrier of this launch timed out (1 s) -- leave
+__device__ bool rx_wait(uint32_t *scratch, uint32_t *ctr, uint32_t target) {
     __syncthreads();
     if (threadIdx.x == 0) {
         uint32_t ok = 1;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        __hip_atomic_fetch_add(&scratch[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (__hip_atomic_load(&scratch[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
             if (__hip_atomic_load(&scratch[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ||
                 __builtin_amdgcn_s_memrealtime() - t0 > kRxBarrierTicks) {
                 __hip_atomic_store(&scratch[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -733,7 +755,7 @@ __global__ __launch_bounds__(kRxWG<AES>) void aes_gcm_quad_rx_kernel(const DevKe
     uint32_t *counts = scratch + 16, *cursor = counts + key_cap, *meta = cursor + key_cap;
     WorkItem *work = (WorkItem *)(meta + 4);  // 16-byte aligned: key_cap is even
 #if QPP_RX_TRACE
-    uint64_t ts[8];
+    uint64_t ts[8] = {};
     ts[0] = __builtin_amdgcn_s_memrealtime();
 #define RX_TS(i) ts[i] = __builtin_amdgcn_s_memrealtime()
 #else
@@ -743,6 +765,7 @@ __global__ __launch_bounds__(kRxWG<AES>) void aes_gcm_quad_rx_kernel(const DevKe
     const uint32_t bins = min(key_cap, kRxHistMax);  // (the launch requires key_cap <= kRxHistMax)
     build_qaes();
     for (uint32_t i = tid; i < bins; i += nt) lds_st32(4 * i, 0);
+    if (tid == 0) lds_st32(kRxLocal, 0xffffffffu);
     __syncthreads();
     const QAes aes = make_qaes();
     RX_TS(1);
@@ -781,16 +804,35 @@ __global__ __launch_bounds__(kRxWG<AES>) void aes_gcm_quad_rx_kernel(const DevKe
             if (status[t] == kRxOpen) status[t] = QPP_INTERNAL_ERROR;
     };
     __syncthreads();
+    // A local slice: every packet of the slice goes to the open phase under ONE AES key this instance opens (a GRO batch
+    // of one connection, or of many connections' packets already grouped) -- the workgroup opens it itself, right
+    // after phase A and in rx order, outside the global plan (no counts, no scatter, no wait for the other slices).
+    // The other slices go through phases B-D as before; the local ones take their share of phase D afterwards.
     for (uint32_t k = tid; k < bins; k += nt) {
         const uint32_t c = lds_ld32(4 * k);
-        if (c) __hip_atomic_fetch_add(&counts[k], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (c && c == hi - lo) {  // (one bin at most)
+            const uint32_t cls = rx_class(*(const uint4 *)(keys + k), chacha != 0);
+            if ((cls == 0 && AES != 14) || (cls == 1 && AES != 10)) {
+                lds_st32(kRxLocal, k);
+                lds_st32(kRxLocal + 4, cls);
+            }
+        }
+    }
+    __syncthreads();
+    const uint32_t local = lds_ld32(kRxLocal), lcls = local != 0xffffffffu ? lds_ld32(kRxLocal + 4) : 2u;  // uniform
+    if (local == 0xffffffffu) {
+        for (uint32_t k = tid; k < bins; k += nt) {
+            const uint32_t c = lds_ld32(4 * k);
+            if (c) __hip_atomic_fetch_add(&counts[k], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
     RX_TS(2);
-    if (!rx_grid_sync(scratch, gridDim.x)) return bail();
+    // B: the last workgroup past phase A -- each key's first perm index (cursor; AES-128 keys, then AES-256, then
+    // ChaCha20) and one work item per AES key with packets (AES-128 items first: the planned-batch layout quad_slices
+    // reads from meta); then it raises [4]
+    const bool last = rx_arrive(&scratch[0]) == gridDim.x - 1;  // uniform
     RX_TS(3);
-    // B: workgroup 0 -- each key's first perm index (cursor; AES-128 keys, then AES-256, then ChaCha20) and one work
-    // item per AES key with packets (AES-128 items first: the planned-batch layout quad_slices reads from meta)
-    if (blockIdx.x == 0) {
+    if (last) {
         const uint32_t chunk = (key_cap + nt - 1) / nt, k0 = min(key_cap, tid * chunk), k1 = min(key_cap, k0 + chunk);
         auto cls_of = [&](uint32_t k) { return rx_class(*(const uint4 *)(keys + k), chacha != 0); };
         // per thread: packets of each class (0..2) and AES keys with packets of each AES class (3, 4)
@@ -858,22 +900,33 @@ __global__ __launch_bounds__(kRxWG<AES>) void aes_gcm_quad_rx_kernel(const DevKe
             if (cls < 2) work[item[cls]++] = WorkItem{k, off[cls], c, cls ? 14u : 10u};
             off[cls] += c;
         }
+        rx_arrive(&scratch[4]);
     }
-    if (!rx_grid_sync(scratch, 2 * gridDim.x)) return bail();
-    RX_TS(4);
-    // C: one block of perm per key this workgroup saw, then its packets into it
-    for (uint32_t k = tid; k < bins; k += nt) {
-        const uint32_t c = lds_ld32(4 * k);
-        if (c) lds_st32(4 * k, __hip_atomic_fetch_add(&cursor[k], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    if (local == 0xffffffffu) {
+        if (!rx_wait(scratch, &scratch[4], 1)) return bail();
+        RX_TS(4);
+        // C: one block of perm per key this workgroup saw, then its packets into it
+        for (uint32_t k = tid; k < bins; k += nt) {
+            const uint32_t c = lds_ld32(4 * k);
+            if (c) lds_st32(4 * k, __hip_atomic_fetch_add(&cursor[k], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        }
+        __syncthreads();
+        for (uint32_t t = lo + tid; t < hi; t += nt)
+            if (status[t] == kRxOpen) perm[lds_add32(4 * descs_out[t].key_idx, 1u)] = t;
+        RX_TS(5);
     }
-    __syncthreads();
-    for (uint32_t t = lo + tid; t < hi; t += nt)
-        if (status[t] == kRxOpen) perm[lds_add32(4 * descs_out[t].key_idx, 1u)] = t;
-    RX_TS(5);
-    if (!rx_grid_sync(scratch, 3 * gridDim.x)) return bail();
-    RX_TS(6);
-    // D: open, key-sorted slices (tables per key segment, as a planned batch): the AES-128 packets, then the AES-256 ones
+    rx_arrive(&scratch[5]);  // (a local slice scatters nothing)
+    // D: pass 0 (local slices): the workgroup's own slice under its key; pass 1: the key-sorted global plan (tables per
+    // key segment, as a planned batch), the AES-128 packets, then the AES-256 ones, once every slice is scattered
     constexpr int WG = kRxWG<AES>;
+    if (local != 0xffffffffu) {
+        if constexpr (AES != 14)
+            if (lcls == 0) quad_slices<false, 10, WG>(keys, descs_out, perm, work, meta, arena, nullptr, status, 0u, local, hi, pow, lo, hi);
+        if constexpr (AES != 10)
+            if (lcls == 1) quad_slices<false, 14, WG>(keys, descs_out, perm, work, meta, arena, nullptr, status, 0u, local, hi, pow, lo, hi);
+    }
+    if (!rx_wait(scratch, &scratch[5], gridDim.x)) return bail();
+    RX_TS(6);
     if constexpr (AES != 14) quad_slices<false, 10, WG>(keys, descs_out, perm, work, meta, arena, nullptr, status, 0u, ~0u, 0u, pow);
     if constexpr (AES != 10) quad_slices<false, 14, WG>(keys, descs_out, perm, work, meta, arena, nullptr, status, 0u, ~0u, 0u, pow);
 #if QPP_RX_TRACE

@@ -119,6 +119,66 @@ def test_fused_rx_equals_two_launch_path_and_oracle(ctx, suite, monkeypatch):
 
 
 @pytest.mark.parametrize("suite", [1, 2])
+def test_fused_rx_local_and_planned_slices(ctx, suite, monkeypatch):
+    """Local slices beside planned ones in one launch: the first half of the batch is one connection's phase-0 packets
+    only (some tampered), so every workgroup slice there has one key and opens itself right after phase A; the second
+    half mixes both live phases (a key update in progress) and long headers, so those slices go through the global
+    plan (counts, scan, scatter) -- and the last slice can be either.  Bit-exact with the multi-launch path and the
+    oracle; no barrier timeout."""
+    rng = np.random.default_rng(140 + suite)
+    ctx.set_burst_max(0)
+    try:
+        k0 = ctx.key(suite, rng.integers(0, 256, qpp.HASH_LEN[suite], dtype=np.uint8).tobytes())
+        k1 = k0.derive_next_key()
+        mats = [(suite, *k0.material()), (suite, *k1.material())]
+        n = 6000
+        chunks, rx, orx = [], [], []
+        off = 0
+        for i in range(n):
+            largest = int(rng.integers(0, 2**40))
+            pn = largest + int(rng.integers(0, 300))
+            _, _, pn_len = orc.truncate_pn(pn, largest)
+            uniform = i < n // 2
+            phase = 0 if uniform else int(rng.integers(0, 2))
+            if not uniform and i % 5 == 0:
+                first = 0xc0 | (int(rng.integers(0, 4)) << 4) | (pn_len - 1)
+                header = bytes([first]) + rng.integers(0, 256, int(rng.integers(6, 40)), dtype=np.uint8).tobytes()
+                phase = 0
+            else:
+                header = bytes([0x40 | (phase << 2) | (pn_len - 1)]) + rng.integers(0, 256, 16, dtype=np.uint8).tobytes()
+            payload = rng.integers(0, 256, int(rng.integers(4, 1400)), dtype=np.uint8).tobytes()
+            _, k, iv, hp = mats[phase]
+            rc, pkt = orc.protect_packet(suite, k, iv, hp, pn, header, pn_len, payload)
+            assert rc == 0
+            pkt = bytearray(pkt)
+            if i % 23 == 6:
+                pkt[-1 - i % 16] ^= 0x04  # tampered -> DECRYPT_ERROR (still a local slice's packet)
+            chunks.append(bytes(pkt) + bytes(int(rng.integers(0, 5))))
+            rx.append((largest, (k0.slot, k1.slot), off, len(header), len(pkt)))
+            orx.append((largest, (0, 1), off, len(header), len(pkt)))
+            off += len(chunks[-1])
+        rx, orx = np.array(rx, dtype=qpp.RX_DTYPE), np.array(orx, dtype=qpp.RX_DTYPE)
+        arena = np.frombuffer(b"".join(chunks) + bytes(64), dtype=np.uint8).copy()
+        t0 = ctx.rx_timeouts()
+        a_f, o_f, s_f = _run(ctx, rx, arena, monkeypatch, fused=True)
+        a_2, o_2, s_2 = _run(ctx, rx, arena, monkeypatch, fused=False)
+        assert ctx.rx_timeouts() == t0
+        assert (s_f == s_2).all(), "status differs between the fused and the multi-launch path"
+        assert (a_f == a_2).all(), "arena differs between the fused and the multi-launch path"
+        assert (o_f.view(np.uint8) == o_2.view(np.uint8)).all(), "descriptors differ"
+        want_arena = arena.copy()
+        want_out, want_st = orc.unprotect_open_batch(orc.make_keys(mats), orx, want_arena)
+        want_st = np.array(want_st, dtype=np.int8)
+        assert (s_f == want_st).all()
+        assert (s_f == 0).sum() > n * 9 // 10 and (s_f == qpp.DECRYPT_ERROR).sum() > 100
+        assert (a_f == want_arena).all()
+        k1.free()
+        k0.free()
+    finally:
+        ctx.set_burst_max(16384)
+
+
+@pytest.mark.parametrize("suite", [1, 2])
 def test_fused_rx_many_keys(suite, monkeypatch):
     """64 live packet keys (32 connections, both key phases live: a key update in progress everywhere), 4 more
     connections whose phase-1 key is already dropped, packets of all of them interleaved at random in one GRO batch:

@@ -685,7 +685,7 @@ __global__ __launch_bounds__(kQuadWG<NR>) void aes_gcm_quad_kernel(const DevKey 
 // complete within a second (a workgroup that never became resident) makes every workgroup leave: its packets bound for
 // the open phase report INTERNAL_ERROR, payload untouched, and the context's timeout counter is raised.
 #ifndef QPP_RX_TRACE
-#define QPP_RX_TRACE 0  // 1: workgroups 0, grid/2 and the last print their phase times (s_memrealtime)
+#define QPP_RX_TRACE 0  // 1: workgroups 0, grid/2 and the last print their phase times (s_memrealtime); 2: all
 #endif
 constexpr uint32_t kRxCtl = kQLdsPow;     // LDS: barrier verdict; [kRxCtl + 64, +320 B) phase B scan sums
 constexpr uint32_t kRxCls = kRxCtl + 1024;  // LDS: phase B's class byte per key (<= kRxHistMax)
@@ -919,11 +919,13 @@ __global__ __launch_bounds__(kRxWG<AES>) void aes_gcm_quad_rx_kernel(const DevKe
     // D: pass 0 (local slices): the workgroup's own slice under its key; pass 1: the key-sorted global plan (tables per
     // key segment, as a planned batch), the AES-128 packets, then the AES-256 ones, once every slice is scattered
     constexpr int WG = kRxWG<AES>;
-    if (local != 0xffffffffu) {
+    if (local != 0xffffffffu) {  // (trace: "C" is the local open)
+        RX_TS(4);
         if constexpr (AES != 14)
             if (lcls == 0) quad_slices<false, 10, WG>(keys, descs_out, perm, work, meta, arena, nullptr, status, 0u, local, hi, pow, lo, hi);
         if constexpr (AES != 10)
             if (lcls == 1) quad_slices<false, 14, WG>(keys, descs_out, perm, work, meta, arena, nullptr, status, 0u, local, hi, pow, lo, hi);
+        RX_TS(5);
     }
     if (!rx_wait(scratch, &scratch[5], gridDim.x)) return bail();
     RX_TS(6);
@@ -931,10 +933,11 @@ __global__ __launch_bounds__(kRxWG<AES>) void aes_gcm_quad_rx_kernel(const DevKe
     if constexpr (AES != 10) quad_slices<false, 14, WG>(keys, descs_out, perm, work, meta, arena, nullptr, status, 0u, ~0u, 0u, pow);
 #if QPP_RX_TRACE
     RX_TS(7);
-    if (threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1 || blockIdx.x == gridDim.x / 2))
-        printf("rx wg %u: tables %.2f A %.2f bar1 %.2f B %.2f C %.2f bar3 %.2f D %.2f us\n", blockIdx.x,
-               (ts[1] - ts[0]) / 100.0, (ts[2] - ts[1]) / 100.0, (ts[3] - ts[2]) / 100.0, (ts[4] - ts[3]) / 100.0,
-               (ts[5] - ts[4]) / 100.0, (ts[6] - ts[5]) / 100.0, (ts[7] - ts[6]) / 100.0);
+    if (threadIdx.x == 0 && (QPP_RX_TRACE == 2 || blockIdx.x == 0 || blockIdx.x == gridDim.x - 1 || blockIdx.x == gridDim.x / 2))
+        printf("rx wg %u: tables %.2f A %.2f bar1 %.2f B %.2f C %.2f bar3 %.2f D %.2f us start %llu end %llu last %d\n",
+               blockIdx.x, (ts[1] - ts[0]) / 100.0, (ts[2] - ts[1]) / 100.0, (ts[3] - ts[2]) / 100.0,
+               (ts[4] - ts[3]) / 100.0, (ts[5] - ts[4]) / 100.0, (ts[6] - ts[5]) / 100.0, (ts[7] - ts[6]) / 100.0,
+               (unsigned long long)ts[0], (unsigned long long)ts[7], (int)last);
 #endif
 }
 

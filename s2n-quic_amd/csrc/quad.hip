@@ -204,19 +204,37 @@ constexpr int kQuadBcast2 = 0xaa;  // [2, 2, 2, 2]
 // block costs.  rk_g: a key schedule in the key record (lane s reads word s of each round).  Returns column s of E(in).
 constexpr int kQuadRot1 = 0x39;  // [1, 2, 3, 0]
 constexpr int kQuadRot3 = 0x93;  // [3, 0, 1, 2]
+// QPP_QUAD_HPS: rk_g is uniform (the segment's key record): each round's four words by one scalar load where the
+// round uses them, the lane's column selected in VGPRs -- instead of NR + 1 vector loads per packet, which queue
+// behind the packet's payload loads and stores (0: the vector loads)
+#ifndef QPP_QUAD_HPS
+#define QPP_QUAD_HPS 1
+#endif
 template <int NR>
 __device__ __forceinline__ uint32_t aes_quad(const QAes &a, const uint32_t *__restrict__ rk_g, uint32_t col, uint32_t s) {
     uint32_t rk[NR + 1];
+    RkPtr hp{};
+    if (QPP_QUAD_HPS) {
+        uint64_t p = (uint64_t)rk_g;
+        asm volatile("" : "+s"(p));  // (uniform; not hoisted)
+        hp = (RkPtr)p;
+    } else {
 #pragma unroll
-    for (int r = 0; r <= NR; r++) rk[r] = rk_g[4 * r + s];
-    uint32_t x = a.rot(col ^ rk[0]);  // (the lane's convention: AesQ4 rotates every word by 8 q)
+        for (int r = 0; r <= NR; r++) rk[r] = rk_g[4 * r + s];
+    }
+    auto rkey = [&](int r) {
+        if (!QPP_QUAD_HPS) return rk[r];
+        const uint4 v = hp[r];
+        return s == 0 ? v.x : s == 1 ? v.y : s == 2 ? v.z : v.w;
+    };
+    uint32_t x = a.rot(col ^ rkey(0));  // (the lane's convention: AesQ4 rotates every word by 8 q)
 #pragma unroll
     for (int r = 1; r <= NR; r++) {
         const uint32_t b = qperm<kQuadRot1>(x), c = qperm<kQuadSwap2>(x), d = qperm<kQuadRot3>(x);
         if (r < NR) {
-            x = a.col(x, b, c, d, a.rot(rk[r]));
+            x = a.col(x, b, c, d, a.rot(rkey(r)));
         } else {
-            x = a.last(x, b, c, d, rk[r]);
+            x = a.last(x, b, c, d, rkey(r));
         }
     }
     return x;

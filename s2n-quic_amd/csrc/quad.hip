@@ -75,6 +75,18 @@ constexpr int kQuadWG = NR == 14 ? QPP_QUAD_WG256 : QPP_QUAD_WG;
 #define QPP_QUAD_NB 4
 #endif
 #ifndef QPP_QUAD_TRACE
+// A wave's priority is raised (s_setprio) from its group's payload loads to the group's end (the XOR, the stores and
+// the GHASH steps) and dropped for the next group's keystream: the arbiter then favours the wave that holds a group's
+// memory round trip over the waves in their keystream, so loads and stores go out earlier and the LDS array is fed from
+// both.  Round 6, same box, alternating rounds: seal 1.1630 -> 1.1450 ms (4 rounds), then 1.1387 -> 1.1123 ms
+// (3 rounds; levels 1 and 3: 1.1210 / 1.1232), 300 B 1.5652 -> 1.5458 ms, receive neutral (profiles/r06/prio).
+// QPP_QUAD_PRIO 0 turns it off; QPP_QUAD_PRIO_DROP 1 drops it right after the stores instead (same time).
+#ifndef QPP_QUAD_PRIO
+#define QPP_QUAD_PRIO 2
+#endif
+#ifndef QPP_QUAD_PRIO_DROP
+#define QPP_QUAD_PRIO_DROP 0
+#endif
 #define QPP_QUAD_TRACE 0  // 1: workgroups 0 and grid/2 print their table-build and total cycles (s_memtime); 2: all
 #endif
 #ifndef QPP_QUAD_EK0C
@@ -415,6 +427,7 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
         // slower: 1.248 vs 1.152 ms seal, 8 VGPRs spilled, profiles/r04h_ab; loading this group's before the keystream
         // 4 % slower at 3 waves/SIMD (14 VGPRs spilled) and 7.5 % slower at 2 waves/SIMD (256 VGPRs, no spill); an L2
         // touch of the next group's lines 3.7 % slower: round 6, profiles/r06/head)
+        if (QPP_QUAD_PRIO) __builtin_amdgcn_s_setprio(QPP_QUAD_PRIO);
         if (SEAL && g == 0 && hp_at0 && (flags & QPP_HP_APPLY) && s == 0) hb = hdr_load(at(pay - aad_len), aad_len - pn_len);
         if (head) {
             // slot 0 (lane 0, k = 0) reads the payload's first block instead of the bytes before it (never used)
@@ -474,6 +487,7 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
 #pragma unroll
             for (int k = 0; k < NBG; k++)
                 if (!(QPP_QUAD_ABL & 2)) st_payload(at(b + 64 * k), out[k]);
+            if (QPP_QUAD_PRIO && QPP_QUAD_PRIO_DROP == 1) __builtin_amdgcn_s_setprio(0);
 #pragma unroll
             for (int k = 0; k < NBG; k++) w = gh.mulx(w, SEAL ? out[k] : in[k]);
         } else {
@@ -495,6 +509,7 @@ __device__ __forceinline__ void quad_packet(const QAes &aes, const GhashT<true> 
             }
         }
         if (SEAL && g == 0 && !(QPP_QUAD_ABL & 4)) hp_early(out[0]);
+        if (QPP_QUAD_PRIO) __builtin_amdgcn_s_setprio(0);
     };
     for (int g = 0; g + 1 < G; g++) group(std::integral_constant<int, kQNB>{}, g);
     // open: the received tag's column s, loaded before the last group so that its round trip passes under that
